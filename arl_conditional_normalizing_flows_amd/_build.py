@@ -1,0 +1,50 @@
+"""In-tree build of libcnf_hip.so (hipcc, gfx950). The .so is git-ignored but travels
+to the GPU box with the repository snapshot."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / 'csrc'
+LIB = PKG / 'lib' / 'libcnf_hip.so'
+SOURCES = ['cnf_kernels.hip', 'cnf_runtime.cpp', 'cnf_plan.cpp']
+HEADERS = ['cnf_kernels.h', 'cnf_plan.h']
+ARCH = os.environ.get('CNF_OFFLOAD_ARCH', 'gfx950')
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', 'hipcc'):
+        if cand and (os.path.sep not in cand or os.path.exists(cand)):
+            return cand
+    raise RuntimeError('hipcc not found')
+
+
+def needs_build() -> bool:
+    if not LIB.exists():
+        return True
+    t = LIB.stat().st_mtime
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / 'include' / 'cnf.h']
+    return any(p.stat().st_mtime > t for p in deps if p.exists())
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if not force and not needs_build():
+        return LIB
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    tmp = LIB.with_suffix('.so.tmp')
+    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared',
+           '-Wno-pass-failed', '-o', str(tmp)] + [str(CSRC / s) for s in SOURCES]
+    if verbose:
+        print(' '.join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv, verbose=True))

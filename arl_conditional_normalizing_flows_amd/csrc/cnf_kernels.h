@@ -1,0 +1,71 @@
+// cnf_kernels.h — kernel argument blocks and launch helpers (host <-> device contract).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cnf {
+
+constexpr float LRELU_ALPHA = 0.3f;      // keras.layers.LeakyReLU() default
+constexpr float LN_EPS = 1e-3f;          // keras.layers.LayerNormalization() default
+constexpr double LOG_2PI_D = 1.8378770664093453;
+
+constexpr int MAXPROB = 12;
+
+// kernel roles: distinct symbols so per-kernel profiles separate the ResNeXt stages
+enum { ROLE_CONV_IN = 0, ROLE_CONV_A = 1, ROLE_GC = 2, ROLE_CONV_B = 3, ROLE_CONV_OUT = 4 };
+
+// One convolution problem of a k_conv launch (blockIdx.y selects the problem).
+struct ConvProb {
+    const float* in;          // NHWC, image 0
+    const double* in_stats;   // LN partials of the input tensor [B][in_nparts][3] or null (no LN)
+    const float* gamma;       // LN gamma over the full in_cs-channel tensor (per h,w,c)
+    const float* beta;
+    const float* wt;          // [K = KS*KS*cin][cout] (HWIO flattened)
+    const float* bias;        // [cout]
+    const float* res;         // residual, same layout as out, or null
+    float* out;
+    double* out_stats;        // LN partials of LeakyReLU(out) [B][out_nparts][3] or null
+    int in_cs, in_off, cin, in_nparts;
+    int out_cs, out_off, cout, out_nparts, out_part_base;
+    int dil, act;
+    int lds_in_off, lds_w_off, lds_k_off;  // byte offsets in dynamic LDS
+    int S, Kpad, NS, nr;                   // LDS pixel stride, padded K, B row stride, N-subtiles
+    uint32_t cin_mag, wp_mag;              // magic multipliers: x / cin == umulhi(x, cin_mag) (3x3 staging)
+    uint32_t st_mask_lo, st_mask_hi;       // output channels actually stored (bit per channel < 64)
+};
+
+struct ConvArgs {
+    ConvProb p[MAXPROB];
+    int H, W, TH, tiles_per_img, nprob, B;
+    int P;   // 1x1 kernels: pixels per tile (tiles are runs of pixels inside one image)
+};
+
+struct CoupArgs {
+    const float* u;
+    float* v;
+    const float* s_pre;      // raw conv_out of net A (before tanh)
+    const float* t;          // conv_out of net b
+    const float* tanh_w;     // device scalar
+    double* ld_part;         // [B][gridDim.x] or null
+    int H, W, D, mask, mask_c, hc, wc, dc1, dc2, dir;
+};
+
+void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
+                       hipStream_t st);
+void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st);
+void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st);
+void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st);
+void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
+                        int B, hipStream_t st);
+void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st);
+void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
+                   hipStream_t st);
+void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, int B, int HW,
+                int D, int x_d, float lambda_y, hipStream_t st);
+void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st);
+
+}  // namespace cnf

@@ -1,0 +1,804 @@
+// cnf_kernels.hip — gfx950 (CDNA4) kernels of the conditional-RealNVP hot path.
+//
+//   k_conv      fused ResNeXt convolution: [LeakyReLU -> per-image LayerNorm (per-element
+//               gamma/beta) on load] -> 1x1 or 3x3 dilated conv as an implicit GEMM on
+//               v_mfma_f32_16x16x4_f32 -> [+bias, +residual] -> store -> per-tile LN-stat
+//               partials (n, mean, M2) of LeakyReLU(out) for the NEXT LayerNorm.
+//               (conv_cINN_base_functions.py:330-413, 501-627; conv_cINN_make_model.py:1107-1195)
+//   k_gather_u1c mask compress of u into u1c (conv_cINN_make_model.py:720-759)
+//   k_coupling  tanh*w, exp, affine law fwd/inv, decompress scatter, u1 copy and the per-image
+//               log-det partial sum (conv_cINN_make_model.py:1198-1205, 1215-1328, 1333-1394)
+//   k_ld_reduce deterministic per-image log-det reduction
+//   k_map_*     squeeze/factor boundary gathers/scatters via index maps (:130-329, :1762-1770)
+//   k_squeeze   space_to_depth / depth_to_space in TF channel order (:179, :211)
+//   k_chcopy    channel-window copy (factor split/concat, :276-327)
+//   k_nll       per-image NLL terms; k_nll_sums batch sums (:1815-1848)
+//
+// All reductions are two-level and atomic-free (bitwise-deterministic).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cnf_kernels.h"
+
+namespace cnf {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : LRELU_ALPHA * x; }
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Chan et al. pairwise merge of (n, mean, M2)
+__device__ __forceinline__ void chan_merge(double& n, double& m, double& M2, double nb, double mb, double M2b) {
+    if (nb == 0.0) return;
+    if (n == 0.0) {
+        n = nb;
+        m = mb;
+        M2 = M2b;
+        return;
+    }
+    double nn = n + nb;
+    double delta = mb - m;
+    m = m + delta * (nb / nn);
+    M2 = M2 + M2b + delta * delta * (n * nb / nn);
+    n = nn;
+}
+
+// One wave merges `nparts` LN-stat partials of image `img` (lane 0 holds the result).
+__device__ __forceinline__ void merge_stats(const double* __restrict__ st, int img, int nparts, int lane,
+                                            double& n, double& m, double& M2) {
+    n = 0.0;
+    m = 0.0;
+    M2 = 0.0;
+    for (int base = 0; base < nparts; base += 64) {
+        double pn = 0.0, pm = 0.0, pM = 0.0;
+        if (base + lane < nparts) {
+            const double* q = st + ((size_t)img * nparts + base + lane) * 3;
+            pn = q[0];
+            pm = q[1];
+            pM = q[2];
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            double on = __shfl_xor(pn, o, 64), om = __shfl_xor(pm, o, 64), oM = __shfl_xor(pM, o, 64);
+            chan_merge(pn, pm, pM, on, om, oM);
+        }
+        chan_merge(n, m, M2, pn, pm, pM);
+    }
+}
+
+__device__ __forceinline__ bool stored(const ConvProb& P, int ch) {
+    return ((ch < 32 ? (P.st_mask_lo >> ch) : (P.st_mask_hi >> (ch - 32))) & 1u) != 0u;
+}
+
+// Per-tile LN-stat partial (n, mean, M2) of the values a thread holds in vals[0..cnt) (already
+// LeakyReLU'd), reduced over the 256-thread block; written by thread 0. `red` = 8 doubles of LDS.
+template <int N>
+__device__ __forceinline__ void tile_stats(const float (&vals)[N], const bool (&valid)[N], double* red,
+                                           double* dst) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float lsum = 0.f;
+    int lcnt = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (valid[i]) {
+            lsum += vals[i];
+            lcnt++;
+        }
+    double ws = wave_sum((double)lsum);
+    double wc = wave_sum((double)lcnt);
+    __syncthreads();
+    if (lane == 0) {
+        red[wave] = ws;
+        red[4 + wave] = wc;
+    }
+    __syncthreads();
+    const double tot = red[0] + red[1] + red[2] + red[3];
+    const double cnt = red[4] + red[5] + red[6] + red[7];
+    const double mean = cnt > 0 ? tot / cnt : 0.0;
+    const float meanf = (float)mean;
+    float lm2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (valid[i]) {
+            float dl = vals[i] - meanf;
+            lm2 += dl * dl;
+        }
+    double wm2 = wave_sum((double)lm2);
+    __syncthreads();
+    if (lane == 0) red[wave] = wm2;
+    __syncthreads();
+    if (tid == 0) {
+        double m2 = red[0] + red[1] + red[2] + red[3];
+        const double dm = mean - (double)meanf;   // sum (x-m')^2 = M2 + n (m-m')^2
+        m2 -= cnt * dm * dm;
+        if (m2 < 0.0) m2 = 0.0;
+        dst[0] = cnt;
+        dst[1] = mean;
+        dst[2] = m2;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_conv1: 1x1 convolution (conv_a / conv_b of dilated_residual_block,
+// conv_cINN_base_functions.py:561-565, 609-613) with the A operand streamed from HBM straight
+// into registers. The K (input-channel) axis is permuted so that lane (i, q) of the
+// 16x16x4 MFMA holds channels 16g + 4q + s at k-steps s = 0..3 of channel group g: one float4
+// load of x, gamma, beta per lane per group, normalised in registers (LeakyReLU -> LN), and
+// one ds_read_b128 of B per N-subtile per group (B stored [g][q][j][s] in LDS).
+// ---------------------------------------------------------------------------------------------
+template <int MR, bool VEC, int ROLE>
+__global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ConvProb& P = a.p[blockIdx.y];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int HW = a.H * a.W;
+    const int tile = blockIdx.x;
+    const int img = tile / a.tiles_per_img;
+    const int tr = tile - img * a.tiles_per_img;
+    const int px0 = tr * a.P;
+    const int Pv = min(a.P, HW - px0);
+    const int cin = P.cin, cout = P.cout, nr = P.nr;
+    const int G = (cin + 15) >> 4;
+    const int NSJ = 16 * nr;
+    double* red = reinterpret_cast<double*>(smem);
+    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
+
+    if (P.in_stats != nullptr && wave == 0) {
+        double n, m, M2;
+        merge_stats(P.in_stats, img, P.in_nparts, lane, n, m, M2);
+        if (lane == 0) {
+            red[8] = m;
+            red[9] = 1.0 / sqrt(M2 / n + (double)LN_EPS);
+        }
+    }
+    // B image [g][q][j][s]: element (c = 16g+4q+s, j)
+    {
+        const int total = G * 16 * NSJ;
+        for (int base = 0; base < total; base += 256 * 4) {
+            float wv[4];
+            int li[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int idx = base + u * 256 + tid;
+                const int sidx = idx & 3;
+                const int rest = idx >> 2;
+                const int gq = rest / NSJ;
+                const int j = rest - gq * NSJ;
+                const int c = (gq >> 2) * 16 + (gq & 3) * 4 + sidx;
+                li[u] = idx < total ? idx : -1;
+                wv[u] = (idx < total && c < cin && j < cout) ? P.wt[(size_t)c * cout + j] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (li[u] >= 0) lw[li[u]] = wv[u];
+        }
+    }
+    __syncthreads();
+    const bool has_ln = P.in_stats != nullptr;
+    float mu = 0.f, rstd = 1.f;
+    if (has_ln) {
+        mu = (float)red[8];
+        rstd = (float)red[9];
+    }
+    const int act = P.act;
+    const int i16 = lane & 15, kq = lane >> 4;
+    bool sact[MR], pval[MR];
+    size_t xoff[MR];
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        const int s = wave + 4 * m;
+        sact[m] = s * 16 < Pv;
+        const int p = s * 16 + i16;
+        pval[m] = p < Pv;
+        xoff[m] = (size_t)(px0 + (pval[m] ? p : 0)) * P.in_cs + P.in_off;
+    }
+    const float* __restrict__ xb = P.in + (size_t)img * HW * P.in_cs;
+    const float* __restrict__ gp = P.gamma;
+    const float* __restrict__ bp = P.beta;
+
+    f4 acc[MR][4];
+#pragma unroll
+    for (int m = 0; m < MR; m++)
+#pragma unroll
+        for (int n = 0; n < 4; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
+
+    auto load_group = [&](int g, f4 (&xr)[MR], f4 (&gr)[MR], f4 (&br)[MR]) {
+        const int c0 = 16 * g + 4 * kq;
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            if (VEC) {
+                const bool ok = c0 < cin;
+                const size_t e = xoff[m] + (ok ? c0 : 0);
+                xr[m] = *reinterpret_cast<const f4*>(xb + e);
+                if (has_ln) {
+                    gr[m] = *reinterpret_cast<const f4*>(gp + e);
+                    br[m] = *reinterpret_cast<const f4*>(bp + e);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const bool ok = c0 + j < cin;
+                    const size_t e = xoff[m] + (ok ? c0 + j : 0);
+                    xr[m][j] = xb[e];
+                    if (has_ln) {
+                        gr[m][j] = gp[e];
+                        br[m][j] = bp[e];
+                    }
+                }
+            }
+        }
+    };
+
+    f4 xr[MR], gr[MR], br[MR];
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        gr[m] = f4{1.f, 1.f, 1.f, 1.f};
+        br[m] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    load_group(0, xr, gr, br);
+    for (int g = 0; g < G; g++) {
+        f4 xn[MR], gn[MR], bn[MR];
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            gn[m] = gr[m];
+            bn[m] = br[m];
+            xn[m] = xr[m];
+        }
+        if (g + 1 < G) load_group(g + 1, xn, gn, bn);
+        const int c0 = 16 * g + 4 * kq;
+        float av[MR][4];
+#pragma unroll
+        for (int m = 0; m < MR; m++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float x = xr[m][j];
+                if (act) x = lrelu(x);
+                if (has_ln) x = (x - mu) * rstd * gr[m][j] + br[m][j];
+                av[m][j] = (pval[m] && c0 + j < cin) ? x : 0.f;
+            }
+        f4 bq[4];
+        const float* brow = lw + ((size_t)(g * 4 + kq) * NSJ + i16) * 4;
+#pragma unroll
+        for (int n = 0; n < 4; n++)
+            bq[n] = (n < nr) ? *reinterpret_cast<const f4*>(brow + n * 64) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int m = 0; m < MR; m++) {
+                if (!sact[m]) continue;
+#pragma unroll
+                for (int n = 0; n < 4; n++)
+                    if (n < nr) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][s], bq[n][s], acc[m][n], 0, 0, 0);
+            }
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            xr[m] = xn[m];
+            gr[m] = gn[m];
+            br[m] = bn[m];
+        }
+    }
+
+    // epilogue: lane holds out[pixel = 16s + 4q + r][ch = 16n + i]
+    float vals[MR * 16];
+    bool valid[MR * 16];
+    const size_t obase = (size_t)img * HW + px0;
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        const int s = wave + 4 * m;
+#pragma unroll
+        for (int n = 0; n < 4; n++) {
+            const int ch = n * 16 + i16;
+            const bool chv = sact[m] && n < nr && ch < cout;
+            const float bias = chv ? P.bias[ch] : 0.f;
+            const bool st = chv && stored(P, ch);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int p = s * 16 + kq * 4 + r;
+                const bool ok = chv && p < Pv;
+                float v = acc[m][n][r] + bias;
+                if (ok) {
+                    const size_t oe = (obase + p) * P.out_cs + P.out_off + ch;
+                    if (P.res) v += P.res[oe];
+                    if (st) P.out[oe] = v;
+                }
+                vals[(m * 4 + n) * 4 + r] = lrelu(v);
+                valid[(m * 4 + n) * 4 + r] = ok;
+            }
+        }
+    }
+    if (P.out_stats != nullptr)
+        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_conv
+// ---------------------------------------------------------------------------------------------
+template <int KS, int MR, int ROLE>
+__global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ConvProb& P = a.p[blockIdx.y];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = blockIdx.x;
+    const int img = tile / a.tiles_per_img;
+    const int tr = tile - img * a.tiles_per_img;
+    const int H = a.H, W = a.W, TH = a.TH;
+    const int HW = H * W;
+    const int r0 = tr * TH;
+    const int rows = min(TH, H - r0);
+    const int Pv = rows * W;      // valid output pixels of this tile
+    const int PT = TH * W;        // staged (padded) pixels
+    const int d = (KS == 3) ? P.dil : 0;
+    const int WP = W + 2 * d;
+    const int S = P.S, cin = P.cin, K = KS * KS * cin, Kpad = P.Kpad, NS = P.NS, cout = P.cout;
+    double* red = reinterpret_cast<double*>(smem);  // 16 doubles of reduction scratch
+    float* lin = reinterpret_cast<float*>(smem + P.lds_in_off);
+    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
+    int* lk = reinterpret_cast<int*>(smem + P.lds_k_off);
+
+    // 1) per-image stats of the input LayerNorm (merge of the producer's tile partials)
+    if (P.in_stats != nullptr && wave == 0) {
+        double n, m, M2;
+        merge_stats(P.in_stats, img, P.in_nparts, lane, n, m, M2);
+        if (lane == 0) {
+            red[8] = m;
+            red[9] = 1.0 / sqrt(M2 / n + (double)LN_EPS);
+        }
+    }
+    // 2) weights B[k][n] (zero padded to Kpad x NS)
+    for (int idx = tid; idx < Kpad * NS; idx += 256) {
+        int k = idx / NS, n = idx - k * NS;
+        lw[idx] = (k < K && n < cout) ? P.wt[(size_t)k * cout + n] : 0.f;
+    }
+    // 3) per-k LDS offsets of the A operand (tap, channel)
+    for (int k = tid; k < Kpad; k += 256) {
+        int off = 0;
+        if (k < K) {
+            if (KS == 3) {
+                int tap = k / cin, ci = k - tap * cin;
+                int kh = tap / 3, kw = tap - kh * 3;
+                off = (kh * d * WP + kw * d) * S + ci;
+            } else {
+                off = k;
+            }
+        }
+        lk[k] = off;
+    }
+    __syncthreads();
+    float mu = 0.f, rstd = 1.f;
+    const bool has_ln = P.in_stats != nullptr;
+    if (has_ln) {
+        mu = (float)red[8];
+        rstd = (float)red[9];
+    }
+    // 4) stage the (normalised) input tile (+halo) into LDS
+    const float* __restrict__ inb = P.in + (size_t)img * HW * P.in_cs + P.in_off;
+    const float* __restrict__ gb = P.gamma ? P.gamma + P.in_off : nullptr;
+    const float* __restrict__ bb = P.beta ? P.beta + P.in_off : nullptr;
+    const int act = P.act;
+    if (KS == 3) {
+        const int SR = TH + 2 * d;
+        const int total = SR * WP * cin;
+        const uint32_t cmag = P.cin_mag, wmag = P.wp_mag;
+        for (int base = 0; base < total; base += 256 * 4) {
+            float xv[4], gv[4], bv[4];
+            int li[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int idx = base + u * 256 + tid;
+                const int pix = (cin == 1) ? idx : (int)__umulhi((uint32_t)idx, cmag);
+                const int c = idx - pix * cin;
+                const int rr = (int)__umulhi((uint32_t)pix, wmag);
+                const int cc = pix - rr * WP;
+                const int row = r0 - d + rr, col = cc - d;
+                li[u] = (idx < total) ? pix * S + c : -1;
+                ok[u] = idx < total && row >= 0 && row < H && col >= 0 && col < W;
+                const size_t e = ok[u] ? (size_t)(row * W + col) * P.in_cs + c : 0;
+                xv[u] = ok[u] ? inb[e] : 0.f;
+                if (has_ln) {
+                    gv[u] = ok[u] ? gb[e] : 0.f;
+                    bv[u] = ok[u] ? bb[e] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (li[u] < 0) continue;
+                float x = xv[u];
+                if (act) x = lrelu(x);
+                if (has_ln) x = (x - mu) * rstd * gv[u] + bv[u];
+                lin[li[u]] = ok[u] ? x : 0.f;
+            }
+        }
+    }
+    __syncthreads();
+
+    // 5) implicit GEMM on v_mfma_f32_16x16x4_f32. Wave w owns 16-pixel subtiles w, w+4, ...
+    //    A[i][k] = lin[abase(i) + lk[k]], lane holds A[lane&15][lane>>4], B[lane>>4][lane&15].
+    const int nsub = (PT + 15) >> 4;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int nr = P.nr;
+    int abase[MR];
+    bool sact[MR];
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        int s = wave + 4 * m;
+        sact[m] = s < nsub;
+        int p = s * 16 + i16;
+        if (p >= PT) p = 0;
+        if (KS == 3) {
+            int pr = p / W, pc = p - pr * W;
+            abase[m] = (pr * WP + pc) * S;
+        } else {
+            abase[m] = p * S;
+        }
+    }
+    f4 acc[MR][4];
+#pragma unroll
+    for (int m = 0; m < MR; m++)
+#pragma unroll
+        for (int n = 0; n < 4; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 2
+    for (int k0 = 0; k0 < Kpad; k0 += 4) {
+        const int kr = k0 + kq;
+        const int ko = lk[kr];
+        const float* wrow = lw + kr * NS + i16;
+        float bv[4];
+#pragma unroll
+        for (int n = 0; n < 4; n++) bv[n] = (n < nr) ? wrow[n * 16] : 0.f;
+#pragma unroll
+        for (int m = 0; m < MR; m++) {
+            if (sact[m]) {
+                float av = lin[abase[m] + ko];
+#pragma unroll
+                for (int n = 0; n < 4; n++)
+                    if (n < nr) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[n], acc[m][n], 0, 0, 0);
+            }
+        }
+    }
+
+    // 6) epilogue: bias, residual, store, LN-stat partials of LeakyReLU(out)
+    float vals[MR * 16];
+    bool valid[MR * 16];
+    const size_t obase = ((size_t)img * HW + (size_t)r0 * W);
+#pragma unroll
+    for (int m = 0; m < MR; m++) {
+        const int s = wave + 4 * m;
+#pragma unroll
+        for (int n = 0; n < 4; n++) {
+            const int ch = n * 16 + i16;
+            const bool chv = sact[m] && n < nr && ch < cout;
+            const float bias = chv ? P.bias[ch] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int p = s * 16 + kq * 4 + r;
+                const bool ok = chv && p < Pv;
+                float v = acc[m][n][r] + bias;
+                if (ok) {
+                    size_t oe = (obase + p) * P.out_cs + P.out_off + ch;
+                    if (P.res) v += P.res[oe];
+                    if (stored(P, ch)) P.out[oe] = v;
+                }
+                vals[(m * 4 + n) * 4 + r] = lrelu(v);
+                valid[(m * 4 + n) * 4 + r] = ok;
+            }
+        }
+    }
+    if (P.out_stats != nullptr)
+        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
+}
+
+// ---------------------------------------------------------------------------------------------
+// masks (conv_cINN_make_model.py:720-759, 896-1071)
+// ---------------------------------------------------------------------------------------------
+// position in u (per-image element index) of element (compressed pixel p, channel c) of the
+// compressed half selected by mask m.
+__device__ __forceinline__ int mask_pos(int m, int p, int c, int wc, int W, int D) {
+    const int pr = p / wc, pc = p - pr * wc;
+    if (m < 2) {
+        const int half = c >= D ? 1 : 0;
+        const int ch = c - half * D;
+        // mask 0: c0 -> (even, even), c1 -> (odd, odd); mask 1: c0 -> (even, odd), c1 -> (odd, even)
+        const int dr = half;
+        const int dc = (m == 0) ? half : 1 - half;
+        return ((2 * pr + dr) * W + (2 * pc + dc)) * D + ch;
+    }
+    const int ch = (m == 2) ? 2 * c : 2 * c + 1;
+    return (pr * W + pc) * D + ch;
+}
+
+__global__ __launch_bounds__(256) void k_gather_u1c(const float* __restrict__ u, float* __restrict__ u1c, int H,
+                                                    int W, int D, int mask, int hc, int wc, int dc1) {
+    const int img = blockIdx.y;
+    const int n = hc * wc * dc1;
+    const float* ub = u + (size_t)img * H * W * D;
+    float* ob = u1c + (size_t)img * n;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+        const int p = e / dc1, c = e - p * dc1;
+        ob[e] = ub[mask_pos(mask, p, c, wc, W, D)];
+    }
+}
+
+// u -> v: copy the mask half, apply the affine law to the complement half.
+// dir=+1: v2 = exp(s)*u2 + t ; dir=-1: u2 = (1/exp(s)) * (v2 - t). s = w * tanh(s_pre).
+__global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
+    const int img = blockIdx.y;
+    const int HWD = a.H * a.W * a.D;
+    const int npx = a.hc * a.wc;
+    const float* __restrict__ ub = a.u + (size_t)img * HWD;
+    float* __restrict__ vb = a.v + (size_t)img * HWD;
+    const float* __restrict__ sb = a.s_pre + (size_t)img * npx * a.dc2;
+    const float* __restrict__ tb = a.t + (size_t)img * npx * a.dc2;
+    const float w = *a.tanh_w;
+    float lsum = 0.f;
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < npx; p += gridDim.x * 256) {
+        for (int c = 0; c < a.dc1; c++) {
+            int e = mask_pos(a.mask, p, c, a.wc, a.W, a.D);
+            vb[e] = ub[e];
+        }
+        for (int c = 0; c < a.dc2; c++) {
+            int e = mask_pos(a.mask_c, p, c, a.wc, a.W, a.D);
+            float s = w * tanhf(sb[p * a.dc2 + c]);
+            float t = tb[p * a.dc2 + c];
+            float x = ub[e];
+            float y;
+            if (a.dir > 0) {
+                y = expf(s) * x + t;
+                lsum += s;
+            } else {
+                y = (1.0f / expf(s)) * (x - t);
+            }
+            vb[e] = y;
+        }
+    }
+    if (a.ld_part != nullptr) {
+        __shared__ double sred[4];
+        double ws = wave_sum((double)lsum);
+        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = ws;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            a.ld_part[(size_t)img * gridDim.x + blockIdx.x] = sred[0] + sred[1] + sred[2] + sred[3];
+    }
+}
+
+// out[img] (=|+=) sum over nl layers, np parts of part[((l*B)+img)*np + j]
+__global__ void k_ld_reduce(const double* __restrict__ part, float* __restrict__ out, int B, int nl, int np,
+                            int accumulate) {
+    const int img = blockIdx.x * blockDim.x + threadIdx.x;
+    if (img >= B) return;
+    double s = 0.0;
+    for (int l = 0; l < nl; l++)
+        for (int j = 0; j < np; j++) s += part[((size_t)l * B + img) * np + j];
+    if (accumulate)
+        out[img] = (float)((double)out[img] + s);
+    else
+        out[img] = (float)s;
+}
+
+// dst[b, i] = src[b, idx[i]]
+__global__ __launch_bounds__(256) void k_map_gather(const float* __restrict__ src, float* __restrict__ dst,
+                                                    const int* __restrict__ idx, int n, int src_stride,
+                                                    int dst_stride) {
+    const int img = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        dst[(size_t)img * dst_stride + i] = src[(size_t)img * src_stride + idx[i]];
+}
+
+// dst[b, idx[i]] = src[b, sidx ? sidx[i] : i]
+__global__ __launch_bounds__(256) void k_map_scatter(const float* __restrict__ src, float* __restrict__ dst,
+                                                     const int* __restrict__ sidx, const int* __restrict__ didx,
+                                                     int n, int src_stride, int dst_stride) {
+    const int img = blockIdx.y;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        int s = sidx ? sidx[i] : i;
+        dst[(size_t)img * dst_stride + didx[i]] = src[(size_t)img * src_stride + s];
+    }
+}
+
+// dir=+1: out[b,i,j,(di*2+dj)*C+c] = in[b,2i+di,2j+dj,c] (in: H x W x C)
+// dir=-1: inverse (in: H x W x 4C', out 2H x 2W x C')
+__global__ __launch_bounds__(256) void k_squeeze(const float* __restrict__ in, float* __restrict__ out, int H,
+                                                 int W, int C, int dir, long long total) {
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        if (dir > 0) {
+            // e indexes out: (b, i, j, q) with q in [0, 4C)
+            const int C4 = 4 * C, H2 = H / 2, W2 = W / 2;
+            long long t = e;
+            int q = (int)(t % C4);
+            t /= C4;
+            int j = (int)(t % W2);
+            t /= W2;
+            int i = (int)(t % H2);
+            long long b = t / H2;
+            int blk = q / C, c = q - blk * C;
+            int di = blk >> 1, dj = blk & 1;
+            out[e] = in[((b * H + 2 * i + di) * W + 2 * j + dj) * C + c];
+        } else {
+            // e indexes out (b, y, x, c) of shape 2H x 2W x C'  with C' = C/4
+            const int Cp = C / 4, H2 = 2 * H, W2 = 2 * W;
+            long long t = e;
+            int c = (int)(t % Cp);
+            t /= Cp;
+            int x = (int)(t % W2);
+            t /= W2;
+            int y = (int)(t % H2);
+            long long b = t / H2;
+            int i = y >> 1, di = y & 1, j = x >> 1, dj = x & 1;
+            out[e] = in[((b * H + i) * W + j) * C + (di * 2 + dj) * Cp + c];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_chcopy(const float* __restrict__ in, int in_cs, int in_off,
+                                                float* __restrict__ out, int out_cs, int out_off, int C,
+                                                long long npix) {
+    const long long total = npix * C;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        long long p = e / C;
+        int c = (int)(e - p * C);
+        out[p * out_cs + out_off + c] = in[p * in_cs + in_off + c];
+    }
+}
+
+// per-image NLL terms: llz = sum_{h,w} (-0.5|z|^2 - x_d/2 ln 2pi), lly = -lambda*sum|y-y'|, ld
+__global__ __launch_bounds__(256) void k_nll(const float* __restrict__ xy, const float* __restrict__ zy,
+                                             const float* __restrict__ ld, float* __restrict__ per_image, int HW,
+                                             int D, int x_d, float lambda_y) {
+    const int img = blockIdx.x;
+    const float* xb = xy + (size_t)img * HW * D;
+    const float* zb = zy + (size_t)img * HW * D;
+    double zz = 0.0, ya = 0.0;
+    for (int e = threadIdx.x; e < HW * D; e += 256) {
+        int c = e % D;
+        float z = zb[e];
+        if (c < x_d)
+            zz += (double)(z * z);
+        else
+            ya += (double)fabsf(z - xb[e]);
+    }
+    __shared__ double s1[4], s2[4];
+    double a = wave_sum(zz), b = wave_sum(ya);
+    if ((threadIdx.x & 63) == 0) {
+        s1[threadIdx.x >> 6] = a;
+        s2[threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double z2 = s1[0] + s1[1] + s1[2] + s1[3];
+        double ay = s2[0] + s2[1] + s2[2] + s2[3];
+        double llz = -0.5 * z2 - 0.5 * (double)x_d * LOG_2PI_D * (double)HW;
+        double lly = -(double)lambda_y * ay;
+        per_image[img * 3 + 0] = (float)llz;
+        per_image[img * 3 + 1] = (float)lly;
+        per_image[img * 3 + 2] = ld[img];
+    }
+}
+
+__global__ void k_nll_sums(const float* __restrict__ per_image, float* __restrict__ sums, int B) {
+    __shared__ double s[4][64];
+    const int t = threadIdx.x;  // 64 threads
+    double a = 0, bz = 0, by = 0, bl = 0;
+    for (int i = t; i < B; i += 64) {
+        double llz = per_image[i * 3], lly = per_image[i * 3 + 1], ld = per_image[i * 3 + 2];
+        a += -(llz + lly + ld);
+        bz += -llz;
+        by += -lly;
+        bl += -ld;
+    }
+    a = wave_sum(a);
+    bz = wave_sum(bz);
+    by = wave_sum(by);
+    bl = wave_sum(bl);
+    if (t == 0) {
+        sums[0] = (float)a;
+        sums[1] = (float)bz;
+        sums[2] = (float)by;
+        sums[3] = (float)bl;
+    }
+    (void)s;
+}
+
+// aux[i] = map[i] >= 0 ? params[map[i]] : 0
+__global__ __launch_bounds__(256) void k_pack(const float* __restrict__ params, const int64_t* __restrict__ map,
+                                              float* __restrict__ aux, long long n) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        int64_t s = map[i];
+        aux[i] = s >= 0 ? params[s] : 0.f;
+    }
+}
+
+void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
+    dim3 g(grid_x, a.nprob), b(256);
+#define CNF_CONV_CASE(MR_, R_) \
+    if (ks == 3 && mr == MR_ && role == R_) { hipLaunchKernelGGL((k_conv<3, MR_, R_>), g, b, lds, st, a); return; }
+    CNF_CONV_CASE(1, ROLE_CONV_IN)
+    CNF_CONV_CASE(1, ROLE_GC)
+    CNF_CONV_CASE(1, ROLE_CONV_OUT)
+    CNF_CONV_CASE(2, ROLE_CONV_IN)
+    CNF_CONV_CASE(2, ROLE_GC)
+    CNF_CONV_CASE(2, ROLE_CONV_OUT)
+#undef CNF_CONV_CASE
+}
+
+void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
+    dim3 g(grid_x, a.nprob), b(256);
+#define CNF_CONV1_CASE(MR_, V_, R_) \
+    if (mr == MR_ && vec == V_ && role == R_) { hipLaunchKernelGGL((k_conv1<MR_, V_, R_>), g, b, lds, st, a); return; }
+    CNF_CONV1_CASE(1, true, ROLE_CONV_A)
+    CNF_CONV1_CASE(1, true, ROLE_CONV_B)
+    CNF_CONV1_CASE(1, false, ROLE_CONV_A)
+    CNF_CONV1_CASE(1, false, ROLE_CONV_B)
+    CNF_CONV1_CASE(2, true, ROLE_CONV_A)
+    CNF_CONV1_CASE(2, true, ROLE_CONV_B)
+    CNF_CONV1_CASE(2, false, ROLE_CONV_A)
+    CNF_CONV1_CASE(2, false, ROLE_CONV_B)
+#undef CNF_CONV1_CASE
+}
+
+void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
+                       hipStream_t st) {
+    int n = hc * wc * dc1;
+    int gx = (n + 255) / 256;
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(k_gather_u1c, dim3(gx, B), dim3(256), 0, st, u, u1c, H, W, D, mask, hc, wc, dc1);
+}
+
+void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
+    hipLaunchKernelGGL(k_coupling, dim3(nparts, B), dim3(256), 0, st, a);
+}
+
+void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st) {
+    hipLaunchKernelGGL(k_ld_reduce, dim3((B + 63) / 64), dim3(64), 0, st, part, out, B, nl, np, accumulate);
+}
+
+void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st) {
+    int gx = (n + 255) / 256;
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(k_map_gather, dim3(gx, B), dim3(256), 0, st, src, dst, idx, n, ss, ds);
+}
+
+void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
+                        int B, hipStream_t st) {
+    int gx = (n + 255) / 256;
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(k_map_scatter, dim3(gx, B), dim3(256), 0, st, src, dst, sidx, didx, n, ss, ds);
+}
+
+void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st) {
+    long long total = (long long)B * H * W * C;
+    long long gx = (total + 255) / 256;
+    if (gx > 8192) gx = 8192;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(k_squeeze, dim3((unsigned)gx), dim3(256), 0, st, in, out, H, W, C, dir, total);
+}
+
+void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
+                   hipStream_t st) {
+    long long total = npix * C;
+    long long gx = (total + 255) / 256;
+    if (gx > 8192) gx = 8192;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(k_chcopy, dim3((unsigned)gx), dim3(256), 0, st, in, in_cs, in_off, out, out_cs, out_off, C,
+                       npix);
+}
+
+void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, int B, int HW,
+                int D, int x_d, float lambda_y, hipStream_t st) {
+    hipLaunchKernelGGL(k_nll, dim3(B), dim3(256), 0, st, xy, zy, ld, per_image, HW, D, x_d, lambda_y);
+    hipLaunchKernelGGL(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
+}
+
+void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st) {
+    long long gx = (n + 255) / 256;
+    if (gx > 4096) gx = 4096;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)gx), dim3(256), 0, st, params, map, aux, n);
+}
+
+}  // namespace cnf

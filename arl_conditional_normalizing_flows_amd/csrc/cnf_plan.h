@@ -1,0 +1,121 @@
+// cnf_plan.h — host-side model plan: the cFlow schedule (conv_cINN_make_model.py:1431-1695),
+// the canonical parameter table, the dense grouped-conv aux image, the squeeze/factor index maps
+// and the workspace layout. No GPU code here.
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/cnf.h"
+
+namespace cnf {
+
+struct Branch {
+    int dil = 1;              // dilation factor of the branch (base_functions.py:575-601)
+    int width = 0;            // _d = int((nk // d) // card)   (base_functions.py:397)
+    int out_off = 0;          // channel offset inside the concat
+    std::vector<int> in_offsets;  // per group: first input channel read (closure quirk aware)
+    // dense-conv view used by the kernels: 3x3 conv from channels [cin_off, cin_off+cin)
+    int cin_off = 0, cin = 0, cout = 0;
+};
+
+struct RBParams {
+    int64_t ln1g = -1, ln1b = -1, conv_a_k = -1, conv_a_b = -1, ln2g = -1, ln2b = -1;
+    std::vector<std::vector<int64_t>> gk, gb;  // [branch][group] canonical offsets
+    std::vector<int64_t> aux_w, aux_b;         // [branch] dense aux offsets
+    int64_t ln3g = -1, ln3b = -1, conv_b_k = -1, conv_b_b = -1;
+};
+
+struct NetParams {
+    int64_t conv_in_k = -1, conv_in_b = -1;
+    std::vector<RBParams> rb;
+    int64_t ln_out_g = -1, ln_out_b = -1, conv_out_k = -1, conv_out_b = -1, tanh_w = -1;
+};
+
+struct Coupling {
+    int index = 0, block = 0, H = 0, W = 0, D = 0, mask = 0, mask_c = 0;
+    int hc = 0, wc = 0, dc1 = 0, dc2 = 0, nk = 0, card = 0, R = 0;
+    std::vector<int> dils;
+    std::vector<Branch> br;
+    int gc = 0;               // concat width of the grouped stage
+    NetParams net[2];         // 0 = A (scale), 1 = b (translation)
+};
+
+struct Layer {
+    int kind = CNF_LAYER_COUPLING;
+    int ci = -1;              // coupling index
+    int npf = 0;              // num_prev_factors (factor layers)
+    int h = 0, w = 0, d = 0;  // block io shape
+    int block = 0;
+};
+
+struct ParamTensor {
+    std::string name;
+    int64_t offset = 0;
+    std::vector<int> shape;
+    int64_t size() const {
+        int64_t s = 1;
+        for (int v : shape) s *= v;
+        return s;
+    }
+};
+
+// Squeeze+factor boundary after a block, as index maps over per-image element
+// indices. keep_src[i]: index in the current block layout of element i of the next
+// block layout. fac_src[j]/fac_orig[j]: index in current layout / position in the
+// final xy-layout output of the j-th factored-out element.
+struct Boundary {
+    int after_block = 0;
+    int n_cur = 0, n_next = 0, n_fac = 0;
+    std::vector<int> keep_src, fac_src, fac_orig;
+    int dev_keep_src = -1, dev_fac_src = -1, dev_fac_orig = -1;  // offsets into the device table
+};
+
+// A recorded kernel launch (for bench measurement hooks).
+struct Recorded {
+    std::string name;
+    double flops = 0, bytes = 0;
+    std::function<void(void*)> relaunch;
+};
+
+struct WsLayout {
+    size_t total = 0;
+    size_t uv[2] = {0, 0}, u1c = 0, y[2] = {0, 0}, t1[2] = {0, 0}, t2[2] = {0, 0}, so[2] = {0, 0};
+    size_t st_y[2] = {0, 0}, st_t1[2] = {0, 0}, st_t2[2] = {0, 0};
+    size_t ld = 0;
+    int64_t n_uv = 0, n_u1c = 0, n_y = 0, n_t2 = 0, n_so = 0;
+    int st_parts = 0;   // partial slots per image per LN slab
+    int ld_parts = 0;   // log-det partial slots per image per coupling layer
+};
+
+struct Plan {
+    cnf_flow_desc desc{};
+    std::vector<int> sfbl, rbl, nkl, cl;
+    std::vector<Layer> layers;
+    std::vector<Coupling> couplings;
+    std::vector<ParamTensor> params;
+    int64_t n_params = 0;
+    int64_t n_aux = 0;
+    std::vector<int64_t> aux_map;   // aux[i] = params[aux_map[i]] (or 0 if < 0)
+    std::vector<Boundary> boundaries;
+    std::vector<int> final_orig;    // last block layout -> xy position
+    int last_n = 0;                 // elements per image of the last block layout
+    // device constant tables (int32), uploaded lazily
+    std::vector<int> host_table;
+    int* dev_table = nullptr;
+    int64_t* dev_aux_map = nullptr;
+    int dev_final_orig = -1;
+    int device = -1;
+    // launch recording
+    bool record = true;
+    std::vector<Recorded> recorded;
+
+    WsLayout layout(int B) const;
+};
+
+// builds the plan; throws std::invalid_argument with the reference's assertion text
+Plan* build_plan(const cnf_flow_desc* d);
+
+}  // namespace cnf

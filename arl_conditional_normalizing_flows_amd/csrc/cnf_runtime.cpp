@@ -1,0 +1,778 @@
+// cnf_runtime.cpp — plan execution and the C ABI of libcnf_hip.so (include/cnf.h).
+//
+// Executes the layer schedule of cFlow.call (conv_cINN_make_model.py:1723-1798) as a fixed
+// sequence of k_conv / k_coupling / map launches on the caller's stream. All memory is the
+// caller's (params, aux, workspace); the plan owns only its index tables.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/cnf.h"
+#include "cnf_kernels.h"
+#include "cnf_plan.h"
+
+struct cnf_plan {
+    cnf::Plan* p;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define CNF_TRY try {
+#define CNF_CATCH                                                   \
+    }                                                               \
+    catch (const std::invalid_argument& e) {                        \
+        return fail(CNF_E_INVALID, e.what());                       \
+    }                                                               \
+    catch (const HipError& e) {                                     \
+        return fail(CNF_E_HIP, e.what());                           \
+    }                                                               \
+    catch (const std::exception& e) {                               \
+        return fail(CNF_E_STATE, e.what());                         \
+    }                                                               \
+    catch (...) {                                                   \
+        return fail(CNF_E_STATE, "unknown error");                  \
+    }
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+namespace cnf {
+
+// ----------------------------------------------------------------------------------------------
+// geometry
+// ----------------------------------------------------------------------------------------------
+struct Geo {
+    int TH, tiles, MR;
+};
+
+static Geo conv_geo(int h, int w) {
+    Geo g;
+    g.MR = (h * w >= 1024) ? 2 : 1;
+    const int pt = 64 * g.MR;
+    if (w > pt) throw std::invalid_argument("image width too large for the row-band tiling (w > 128)");
+    g.TH = std::min(h, std::max(1, pt / w));
+    g.tiles = (h + g.TH - 1) / g.TH;
+    return g;
+}
+
+static int lds_stride(int cin) {  // pixel stride in floats, == 2 (mod 4): conflict-free A reads
+    int s = std::max(cin, 2);
+    while (s % 4 != 2) s++;
+    return s;
+}
+
+struct ConvGeom1 {
+    int MR, P, tiles;
+};
+static ConvGeom1 conv1_geo(int h, int w) {
+    ConvGeom1 g;
+    const int hw = h * w;
+    g.MR = (hw >= 1024) ? 2 : 1;
+    g.P = 64 * g.MR;
+    g.tiles = (hw + g.P - 1) / g.P;
+    return g;
+}
+
+static int ld_parts_for(int npx) { return std::max(1, std::min(16, (npx + 255) / 256)); }
+
+WsLayout Plan::layout(int B) const {
+    WsLayout L;
+    int64_t n_uv = (int64_t)desc.io_h * desc.io_w * desc.io_d;
+    int64_t n_u1c = 0, n_y = 0, n_t2 = 0, n_so = 0;
+    int parts = 1, ldp = 1;
+    for (const auto& c : couplings) {
+        int64_t npx = (int64_t)c.hc * c.wc;
+        n_u1c = std::max<int64_t>(n_u1c, npx * c.dc1);
+        n_y = std::max<int64_t>(n_y, npx * c.nk);
+        n_t2 = std::max<int64_t>(n_t2, npx * c.gc);
+        n_so = std::max<int64_t>(n_so, npx * c.dc2);
+        Geo g = conv_geo(c.hc, c.wc);
+        parts = std::max(parts, g.tiles * (int)c.br.size());
+        parts = std::max(parts, conv1_geo(c.hc, c.wc).tiles);
+        ldp = std::max(ldp, ld_parts_for((int)npx));
+    }
+    L.n_uv = n_uv;
+    L.n_u1c = n_u1c;
+    L.n_y = n_y;
+    L.n_t2 = n_t2;
+    L.n_so = n_so;
+    L.st_parts = parts;
+    L.ld_parts = ldp;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes, 256);
+        return o;
+    };
+    const size_t Bz = (size_t)B;
+    L.uv[0] = take(Bz * n_uv * 4);
+    L.uv[1] = take(Bz * n_uv * 4);
+    L.u1c = take(Bz * n_u1c * 4);
+    for (int n = 0; n < 2; n++) {
+        L.y[n] = take(Bz * n_y * 4);
+        L.t1[n] = take(Bz * n_y * 4);
+        L.t2[n] = take(Bz * n_t2 * 4);
+        L.so[n] = take(Bz * n_so * 4);
+        L.st_y[n] = take(Bz * parts * 3 * 8);
+        L.st_t1[n] = take(Bz * parts * 3 * 8);
+        L.st_t2[n] = take(Bz * parts * 3 * 8);
+    }
+    L.ld = take(std::max<size_t>(1, couplings.size()) * Bz * ldp * 8);
+    L.total = off;
+    return L;
+}
+
+// ----------------------------------------------------------------------------------------------
+// launch helpers
+// ----------------------------------------------------------------------------------------------
+struct Exec {
+    Plan& p;
+    const float* params;
+    const float* aux;
+    char* ws;
+    WsLayout L;
+    int B;
+    hipStream_t st;
+
+    template <class T>
+    T* at(size_t off) const {
+        return reinterpret_cast<T*>(ws + off);
+    }
+
+    void record(const std::string& name, double flops, double bytes, std::function<void(void*)> fn) {
+        fn(st);
+        if (p.record) {
+            Recorded r;
+            r.name = name;
+            r.flops = flops;
+            r.bytes = bytes;
+            r.relaunch = std::move(fn);
+            p.recorded.push_back(std::move(r));
+        }
+    }
+};
+
+struct ProbSpec {
+    const float* in;
+    int in_cs, in_off, cin;
+    const double* in_stats;
+    int in_nparts;
+    const float* gamma;
+    const float* beta;
+    int act;
+    const float* wt;
+    const float* bias;
+    float* out;
+    int out_cs, out_off, cout;
+    const float* res;
+    double* out_stats;
+    int out_nparts, out_part_base;
+    int dil;
+};
+
+static const char* role_name(int r) {
+    switch (r) {
+        case ROLE_CONV_IN: return "conv_in";
+        case ROLE_CONV_A: return "conv_a";
+        case ROLE_GC: return "gc";
+        case ROLE_CONV_B: return "conv_b";
+        default: return "conv_out";
+    }
+}
+
+static uint32_t magic_for(int d, int64_t xmax) {
+    // x / d == umulhi(x, ceil(2^32 / d)) exactly while x * d * d < 2^32 (error term x*e/2^32 < 1/d)
+    if (d <= 1) return 0;
+    if ((double)xmax * d * d >= 4294967296.0) throw std::invalid_argument("magic division out of range");
+    return (uint32_t)((((uint64_t)1 << 32) + (uint64_t)d - 1) / (uint64_t)d);
+}
+
+static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
+                        uint64_t store_mask = ~0ull) {
+    if (probs.empty()) return;
+    if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.H = h;
+    a.W = w;
+    a.nprob = (int)probs.size();
+    a.B = E.B;
+    Geo g{0, 0, 0};
+    ConvGeom1 g1{0, 0, 0};
+    if (ks == 3) {
+        g = conv_geo(h, w);
+        a.TH = g.TH;
+        a.tiles_per_img = g.tiles;
+    } else {
+        g1 = conv1_geo(h, w);
+        a.P = g1.P;
+        a.tiles_per_img = g1.tiles;
+    }
+    size_t lds = 0;
+    double flops = 0, bytes = 0;
+    const double HWB = (double)h * w * E.B;
+    bool vec = true;
+    for (size_t i = 0; i < probs.size(); i++) {
+        const ProbSpec& s = probs[i];
+        ConvProb& q = a.p[i];
+        q.in = s.in;
+        q.in_stats = s.in_stats;
+        q.gamma = s.gamma;
+        q.beta = s.beta;
+        q.wt = s.wt;
+        q.bias = s.bias;
+        q.res = s.res;
+        q.out = s.out;
+        q.out_stats = s.out_stats;
+        q.in_cs = s.in_cs;
+        q.in_off = s.in_off;
+        q.cin = s.cin;
+        q.in_nparts = s.in_nparts;
+        q.out_cs = s.out_cs;
+        q.out_off = s.out_off;
+        q.cout = s.cout;
+        q.out_nparts = s.out_nparts;
+        q.out_part_base = s.out_part_base;
+        q.dil = s.dil;
+        q.act = s.act;
+        q.st_mask_lo = (uint32_t)(store_mask & 0xffffffffull);
+        q.st_mask_hi = (uint32_t)(store_mask >> 32);
+        if (s.cout > 64) throw std::invalid_argument("conv with more than 64 output channels");
+        const int K = ks * ks * s.cin;
+        q.nr = (s.cout + 15) / 16;
+        size_t off = 128;
+        if (ks == 3) {
+            q.S = lds_stride(s.cin);
+            q.Kpad = (K + 3) / 4 * 4;
+            q.NS = 16 * q.nr;
+            if (q.NS % 32 == 0) q.NS += 16;
+            const int d = s.dil;
+            const int WP = w + 2 * d;
+            const int SR = g.TH + 2 * d;
+            const int64_t total = (int64_t)SR * WP * s.cin;
+            q.cin_mag = magic_for(s.cin, total + 256 * 4);
+            q.wp_mag = magic_for(WP, (int64_t)SR * WP + 256 * 4);
+            if (WP == 1) throw std::invalid_argument("degenerate width");
+            size_t lin_f = (size_t)SR * WP * q.S;
+            q.lds_in_off = (int)off;
+            off = align_up(off + lin_f * 4, 16);
+            q.lds_w_off = (int)off;
+            off = align_up(off + (size_t)q.Kpad * q.NS * 4, 16);
+            q.lds_k_off = (int)off;
+            off = align_up(off + (size_t)q.Kpad * 4, 16);
+        } else {
+            const int G = (s.cin + 15) / 16;
+            q.lds_w_off = (int)off;
+            off = align_up(off + (size_t)G * 16 * 16 * q.nr * 4, 16);
+            if (s.cin % 4 || s.in_cs % 4 || s.in_off % 4) vec = false;
+        }
+        lds = std::max(lds, off);
+        flops += 2.0 * HWB * K * s.cout;
+        bytes += 4.0 * (HWB * s.cin + HWB * s.cout * (s.res ? 2 : 1) + (s.in_stats ? 2.0 * h * w * s.cin : 0.0) +
+                        (double)K * s.cout + s.cout);
+    }
+    if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
+    const int ilds = (int)lds;
+    if (ks == 3) {
+        const int grid_x = E.B * g.tiles;
+        const int mr = g.MR;
+        std::string name = std::string("k_conv3<") + std::to_string(mr) + "," + role_name(role) + ">";
+        E.record(name, flops, bytes, [mr, role, a, grid_x, ilds](void* st) {
+            launch_conv(3, mr, role, a, grid_x, ilds, (hipStream_t)st);
+        });
+    } else {
+        const int grid_x = E.B * g1.tiles;
+        const int mr = g1.MR;
+        std::string name = std::string("k_conv1<") + std::to_string(mr) + "," + (vec ? "vec" : "scalar") + "," +
+                           role_name(role) + ">";
+        E.record(name, flops, bytes, [mr, vec, role, a, grid_x, ilds](void* st) {
+            launch_conv1(mr, vec, role, a, grid_x, ilds, (hipStream_t)st);
+        });
+    }
+}
+
+// One coupling layer: u -> v. dir=+1 forward (ld_part may collect Σs), dir=-1 inverse.
+static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir) {
+    const int B = E.B;
+    const WsLayout& L = E.L;
+    const float* P = E.params;
+    const float* X = E.aux;
+    const int nt3 = conv_geo(c.hc, c.wc).tiles;     // LN partials written by a 3x3 launch (per problem)
+    const int nt1 = conv1_geo(c.hc, c.wc).tiles;    // ... by a 1x1 launch
+    const int nbr = (int)c.br.size();
+    const bool ln = E.p.desc.layer_norm != 0;
+    float* u1c = E.at<float>(L.u1c);
+    {
+        const float* uu = u;
+        E.record("k_gather_u1c", 0, 4.0 * B * c.hc * c.wc * c.dc1 * 2,
+                 [=](void* st) { launch_gather_u1c(uu, u1c, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, (hipStream_t)st); });
+    }
+    float* y[2] = {E.at<float>(L.y[0]), E.at<float>(L.y[1])};
+    float* t1[2] = {E.at<float>(L.t1[0]), E.at<float>(L.t1[1])};
+    float* t2[2] = {E.at<float>(L.t2[0]), E.at<float>(L.t2[1])};
+    float* so[2] = {E.at<float>(L.so[0]), E.at<float>(L.so[1])};
+    double* sy[2] = {E.at<double>(L.st_y[0]), E.at<double>(L.st_y[1])};
+    double* s1[2] = {E.at<double>(L.st_t1[0]), E.at<double>(L.st_t1[1])};
+    double* s2[2] = {E.at<double>(L.st_t2[0]), E.at<double>(L.st_t2[1])};
+
+    // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
+    {
+        std::vector<ProbSpec> pr;
+        for (int n = 0; n < 2; n++) {
+            const NetParams& np = c.net[n];
+            pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, nullptr, 0, nullptr, nullptr, 0, P + np.conv_in_k,
+                                  P + np.conv_in_b, y[n], c.nk, 0, c.nk, nullptr, ln ? sy[n] : nullptr, nt3, 0, 1});
+        }
+        conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr);
+    }
+    int ny_parts = nt3;
+    for (int r = 0; r < c.R; r++) {
+        // conv_a: LN1(LReLU(y)) -> 1x1 -> t1
+        {
+            std::vector<ProbSpec> pr;
+            for (int n = 0; n < 2; n++) {
+                const RBParams& rb = c.net[n].rb[r];
+                pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + rb.ln1g : nullptr,
+                                      ln ? P + rb.ln1b : nullptr, 1, P + rb.conv_a_k, P + rb.conv_a_b, t1[n], c.nk, 0,
+                                      c.nk, nullptr, ln ? s1[n] : nullptr, nt1, 0, 1});
+            }
+            uint64_t used = 0;
+            for (const Branch& b : c.br)
+                for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) used |= 1ull << ch;
+            conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used);
+        }
+        // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]
+        {
+            std::vector<ProbSpec> pr;
+            for (int n = 0; n < 2; n++) {
+                const RBParams& rb = c.net[n].rb[r];
+                for (int bi = 0; bi < nbr; bi++) {
+                    const Branch& b = c.br[bi];
+                    pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, ln ? s1[n] : nullptr, nt1,
+                                          ln ? P + rb.ln2g : nullptr, ln ? P + rb.ln2b : nullptr, 1, X + rb.aux_w[bi],
+                                          X + rb.aux_b[bi], t2[n], c.gc, b.out_off, b.cout, nullptr,
+                                          ln ? s2[n] : nullptr, nbr * nt3, bi * nt3, b.dil});
+                }
+            }
+            conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
+        }
+        // conv_b: LN3(LReLU(t2)) -> 1x1 -> + shortcut -> y (in place)
+        {
+            std::vector<ProbSpec> pr;
+            for (int n = 0; n < 2; n++) {
+                const RBParams& rb = c.net[n].rb[r];
+                pr.push_back(ProbSpec{t2[n], c.gc, 0, c.gc, ln ? s2[n] : nullptr, nbr * nt3,
+                                      ln ? P + rb.ln3g : nullptr, ln ? P + rb.ln3b : nullptr, 1, P + rb.conv_b_k,
+                                      P + rb.conv_b_b, y[n], c.nk, 0, c.nk, y[n], ln ? sy[n] : nullptr, nt1, 0, 1});
+            }
+            conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr);
+        }
+        ny_parts = nt1;
+    }
+    // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b)
+    {
+        std::vector<ProbSpec> pr;
+        for (int n = 0; n < 2; n++) {
+            const NetParams& np = c.net[n];
+            pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + np.ln_out_g : nullptr,
+                                  ln ? P + np.ln_out_b : nullptr, 1, P + np.conv_out_k, P + np.conv_out_b, so[n],
+                                  c.dc2, 0, c.dc2, nullptr, nullptr, 0, 0, 1});
+        }
+        conv_launch(E, 3, ROLE_CONV_OUT, c.hc, c.wc, pr);
+    }
+    // affine coupling law + decompress + log-det partials
+    {
+        CoupArgs ca;
+        ca.u = u;
+        ca.v = v;
+        ca.s_pre = so[0];
+        ca.t = so[1];
+        ca.tanh_w = P + c.net[0].tanh_w;
+        ca.ld_part = ld_part;
+        ca.H = c.H;
+        ca.W = c.W;
+        ca.D = c.D;
+        ca.mask = c.mask;
+        ca.mask_c = c.mask_c;
+        ca.hc = c.hc;
+        ca.wc = c.wc;
+        ca.dc1 = c.dc1;
+        ca.dc2 = c.dc2;
+        ca.dir = dir;
+        const int np = E.L.ld_parts;
+        E.record("k_coupling", 0, 4.0 * B * c.H * c.W * c.D * 2 + 8.0 * B * c.hc * c.wc * c.dc2,
+                 [ca, B, np](void* st) { launch_coupling(ca, B, np, (hipStream_t)st); });
+    }
+}
+
+static void ensure_tables(Plan& p) {
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (p.dev_table != nullptr && p.device == dev) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    // uploading is not capturable: the first call on a device must run eagerly
+    if (hipStreamIsCapturing(nullptr, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        throw std::runtime_error("plan tables not uploaded yet (call cnf_pack_params before graph capture)");
+    size_t nb = std::max<size_t>(1, p.host_table.size()) * sizeof(int);
+    hip_check(hipMalloc(&p.dev_table, nb), "hipMalloc(table)");
+    if (!p.host_table.empty())
+        hip_check(hipMemcpy(p.dev_table, p.host_table.data(), p.host_table.size() * sizeof(int), hipMemcpyHostToDevice),
+                  "hipMemcpy(table)");
+    size_t na = std::max<size_t>(1, p.aux_map.size()) * sizeof(int64_t);
+    hip_check(hipMalloc(&p.dev_aux_map, na), "hipMalloc(aux map)");
+    if (!p.aux_map.empty())
+        hip_check(hipMemcpy(p.dev_aux_map, p.aux_map.data(), p.aux_map.size() * sizeof(int64_t), hipMemcpyHostToDevice),
+                  "hipMemcpy(aux map)");
+    p.device = dev;
+}
+
+static void check_launch() { hip_check(hipGetLastError(), "kernel launch"); }
+
+}  // namespace cnf
+
+using namespace cnf;
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+const char* cnf_last_error(void) { return g_err.c_str(); }
+const char* cnf_version(void) { return "cnf-mi355x 0.1 (gfx950)"; }
+
+int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
+    if (!out) return fail(CNF_E_INVALID, "null out");
+    *out = nullptr;
+    CNF_TRY
+    Plan* p = build_plan(desc);
+    // validate tiling / LDS budget for every layer up-front
+    for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
+    *out = new cnf_plan{p};
+    return CNF_OK;
+    CNF_CATCH
+}
+
+void cnf_plan_destroy(cnf_plan* plan) {
+    if (!plan) return;
+    if (plan->p) {
+        if (plan->p->dev_table) (void)hipFree(plan->p->dev_table);
+        if (plan->p->dev_aux_map) (void)hipFree(plan->p->dev_aux_map);
+        delete plan->p;
+    }
+    delete plan;
+}
+
+int cnf_plan_num_layers(const cnf_plan* plan) { return plan ? (int)plan->p->layers.size() : -1; }
+
+int cnf_plan_layer_info(const cnf_plan* plan, int layer, cnf_layer_info* out) {
+    if (!plan || !out) return fail(CNF_E_INVALID, "null argument");
+    const Plan& p = *plan->p;
+    if (layer < 0 || layer >= (int)p.layers.size()) return fail(CNF_E_INVALID, "layer index out of range");
+    std::memset(out, 0, sizeof(*out));
+    const Layer& L = p.layers[layer];
+    out->kind = L.kind;
+    out->coupling_index = L.ci;
+    out->block = L.block;
+    out->h = L.h;
+    out->w = L.w;
+    out->d = L.d;
+    out->num_prev_factors = L.npf;
+    if (L.kind == CNF_LAYER_COUPLING) {
+        const Coupling& c = p.couplings[L.ci];
+        out->mask = c.mask;
+        out->hc = c.hc;
+        out->wc = c.wc;
+        out->dc1 = c.dc1;
+        out->dc2 = c.dc2;
+        out->num_kernels = c.nk;
+        out->cardinality = c.card;
+        out->num_res_blocks = c.R;
+        out->num_dilations = (int)c.dils.size();
+        for (int i = 0; i < (int)c.dils.size() && i < 8; i++) out->dilations[i] = c.dils[i];
+    }
+    return CNF_OK;
+}
+
+int64_t cnf_plan_num_params(const cnf_plan* plan) { return plan ? plan->p->n_params : -1; }
+int cnf_plan_num_param_tensors(const cnf_plan* plan) { return plan ? (int)plan->p->params.size() : -1; }
+
+int cnf_plan_param_tensor(const cnf_plan* plan, int index, char* name, int name_cap, int64_t* offset, int* ndim,
+                          int shape[4]) {
+    if (!plan) return fail(CNF_E_INVALID, "null plan");
+    const Plan& p = *plan->p;
+    if (index < 0 || index >= (int)p.params.size()) return fail(CNF_E_INVALID, "param index out of range");
+    const ParamTensor& t = p.params[index];
+    if (name && name_cap > 0) {
+        std::snprintf(name, (size_t)name_cap, "%s", t.name.c_str());
+    }
+    if (offset) *offset = t.offset;
+    if (ndim) *ndim = (int)t.shape.size();
+    if (shape)
+        for (int i = 0; i < 4; i++) shape[i] = i < (int)t.shape.size() ? t.shape[i] : 0;
+    return CNF_OK;
+}
+
+int64_t cnf_plan_aux_floats(const cnf_plan* plan) { return plan ? std::max<int64_t>(1, plan->p->n_aux) : -1; }
+
+int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* stream) {
+    if (!plan || !params || !aux) return fail(CNF_E_INVALID, "null argument");
+    CNF_TRY
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    if (p.n_aux > 0) launch_pack(params, p.dev_aux_map, aux, (long long)p.n_aux, (hipStream_t)stream);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
+    if (!plan || B <= 0) return 0;
+    return plan->p->layout(B).total;
+}
+
+int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
+                     float* logdet_per_image, void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !workspace || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    p.recorded.clear();
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    const WsLayout& L = E.L;
+    double* ld = E.at<double>(L.ld);
+    float* buf[2] = {E.at<float>(L.uv[0]), E.at<float>(L.uv[1])};
+    const float* cur = xy;
+    int which = 0;
+    size_t bi = 0;
+    const int nuv = (int)L.n_uv;
+    for (const Layer& ly : p.layers) {
+        if (ly.kind == CNF_LAYER_COUPLING) {
+            const Coupling& c = p.couplings[ly.ci];
+            float* nxt = buf[which];
+            run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1);
+            cur = nxt;
+            which ^= 1;
+        } else if (ly.kind == CNF_LAYER_FACTOR) {
+            // squeeze (:179) + factor (:276-286) at a block boundary: kept half -> next buffer,
+            // factored half -> its final xy-layout position in zy (:1762-1770 restoration).
+            const Boundary& b = p.boundaries[bi++];
+            float* nxt = buf[which];
+            const int* T = p.dev_table;
+            const float* src = cur;
+            const int ncur = b.n_cur, nnext = b.n_next, nfac = b.n_fac;
+            const int* ks = T + b.dev_keep_src;
+            const int* fs = T + b.dev_fac_src;
+            const int* fo = T + b.dev_fac_orig;
+            E.record("k_map_gather", 0, 8.0 * B * nnext, [=](void* st) {
+                launch_map_gather(src, nxt, ks, nnext, ncur, nnext, B, (hipStream_t)st);
+            });
+            E.record("k_map_scatter", 0, 8.0 * B * nfac, [=](void* st) {
+                launch_map_scatter(src, zy, fs, fo, nfac, ncur, nuv, B, (hipStream_t)st);
+            });
+            cur = nxt;
+            which ^= 1;
+        }
+    }
+    {
+        const int* T = p.dev_table;
+        const int off = p.dev_final_orig, n = p.last_n;
+        const float* src = cur;
+        E.record("k_map_scatter", 0, 8.0 * B * n, [=](void* st) {
+            launch_map_scatter(src, zy, nullptr, T + off, n, n, nuv, B, (hipStream_t)st);
+        });
+    }
+    {
+        const int nl = (int)p.couplings.size(), np = L.ld_parts;
+        E.record("k_ld_reduce", 0, 0, [=](void* st) { launch_ld_reduce(ld, logdet_per_image, B, nl, np, 0, (hipStream_t)st); });
+    }
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, const float* zy, float* xy,
+                     void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !xy || !zy || !workspace || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    p.recorded.clear();
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    const WsLayout& L = E.L;
+    float* buf[2] = {E.at<float>(L.uv[0]), E.at<float>(L.uv[1])};
+    const int nuv = (int)L.n_uv;
+    const int* T = p.dev_table;
+    // squeeze/factor forward on zy (:1784-1788) == gather of the last block layout from xy positions
+    int which = 0;
+    {
+        float* dst = buf[which];
+        const int off = p.dev_final_orig, n = p.last_n;
+        E.record("k_map_gather", 0, 8.0 * B * n,
+                 [=](void* st) { launch_map_gather(zy, dst, T + off, n, nuv, n, B, (hipStream_t)st); });
+    }
+    float* cur = buf[which];
+    which ^= 1;
+    int bi = (int)p.boundaries.size() - 1;
+    for (int li = (int)p.layers.size() - 1; li >= 0; li--) {
+        const Layer& ly = p.layers[li];
+        if (ly.kind == CNF_LAYER_COUPLING) {
+            const Coupling& c = p.couplings[ly.ci];
+            float* nxt = buf[which];
+            run_coupling(E, c, cur, nxt, nullptr, -1);
+            cur = nxt;
+            which ^= 1;
+        } else if (ly.kind == CNF_LAYER_FACTOR) {
+            // factor.backward (:294-329) + squeeze.backward (:191-217): rebuild the previous block
+            // layout from the kept part (cur) and the factored part (read from zy at xy positions).
+            const Boundary& b = p.boundaries[bi--];
+            float* prev = buf[which];
+            const float* src = cur;
+            const int ncur = b.n_cur, nnext = b.n_next, nfac = b.n_fac;
+            const int* ks = T + b.dev_keep_src;
+            const int* fs = T + b.dev_fac_src;
+            const int* fo = T + b.dev_fac_orig;
+            E.record("k_map_scatter", 0, 8.0 * B * nnext, [=](void* st) {
+                launch_map_scatter(src, prev, nullptr, ks, nnext, nnext, ncur, B, (hipStream_t)st);
+            });
+            E.record("k_map_scatter", 0, 8.0 * B * nfac, [=](void* st) {
+                launch_map_scatter(zy, prev, fo, fs, nfac, nuv, ncur, B, (hipStream_t)st);
+            });
+            cur = prev;
+            which ^= 1;
+        }
+    }
+    {
+        const float* src = cur;
+        const size_t bytes = (size_t)B * nuv * 4;
+        E.record("copy", 0, 2.0 * bytes, [=](void* st) {
+            (void)hipMemcpyAsync(xy, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)st);
+        });
+    }
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_coupling_forward(cnf_plan* plan, int layer, const float* params, const float* aux, const float* u, float* v,
+                         float* logdet_accum, void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !u || !v || !workspace || B <= 0) return fail(CNF_E_INVALID, "null argument");
+    CNF_TRY
+    Plan& p = *plan->p;
+    if (layer < 0 || layer >= (int)p.layers.size() || p.layers[layer].kind != CNF_LAYER_COUPLING)
+        return fail(CNF_E_INVALID, "layer is not a coupling layer");
+    if (u == v) return fail(CNF_E_INVALID, "u and v must not alias");
+    ensure_tables(p);
+    p.recorded.clear();
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    double* ld = E.at<double>(E.L.ld);
+    const Coupling& c = p.couplings[p.layers[layer].ci];
+    run_coupling(E, c, u, v, logdet_accum ? ld : nullptr, +1);
+    if (logdet_accum) {
+        const int np = E.L.ld_parts;
+        E.record("k_ld_reduce", 0, 0, [=](void* st) { launch_ld_reduce(ld, logdet_accum, B, 1, np, 1, (hipStream_t)st); });
+    }
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_coupling_inverse(cnf_plan* plan, int layer, const float* params, const float* aux, const float* v, float* u,
+                         void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !u || !v || !workspace || B <= 0) return fail(CNF_E_INVALID, "null argument");
+    CNF_TRY
+    Plan& p = *plan->p;
+    if (layer < 0 || layer >= (int)p.layers.size() || p.layers[layer].kind != CNF_LAYER_COUPLING)
+        return fail(CNF_E_INVALID, "layer is not a coupling layer");
+    if (u == v) return fail(CNF_E_INVALID, "u and v must not alias");
+    ensure_tables(p);
+    p.recorded.clear();
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    run_coupling(E, p.couplings[p.layers[layer].ci], v, u, nullptr, -1);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, void* stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0) return fail(CNF_E_INVALID, "bad argument");
+    if (dir > 0 && ((H % 2) || (W % 2))) return fail(CNF_E_INVALID, "u must have spatial dimensions divisible by 2.");
+    if (dir < 0 && (C % 4)) return fail(CNF_E_INVALID, "v must have channel dimensions divisible by 4.");
+    CNF_TRY
+    launch_squeeze(in, out, B, H, W, C, dir > 0 ? 1 : -1, (hipStream_t)stream);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, int B, int HW,
+                     void* stream) {
+    if (!in || !out || C < 0 || B <= 0 || HW <= 0 || in_off + C > in_cs || out_off + C > out_cs)
+        return fail(CNF_E_INVALID, "bad channel window");
+    if (C == 0) return CNF_OK;
+    CNF_TRY
+    launch_chcopy(in, in_cs, in_off, out, out_cs, out_off, C, (long long)B * HW, (hipStream_t)stream);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image, float* per_image,
+            float* sums, int B, void* stream) {
+    if (!plan || !xy || !zy || !logdet_per_image || !per_image || !sums || B <= 0)
+        return fail(CNF_E_INVALID, "null argument");
+    CNF_TRY
+    const cnf_flow_desc& d = plan->p->desc;
+    launch_nll(xy, zy, logdet_per_image, per_image, sums, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y,
+               (hipStream_t)stream);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)plan->p->recorded.size() : -1; }
+
+int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int name_cap, double* flops,
+                                  double* bytes) {
+    if (!plan) return fail(CNF_E_INVALID, "null plan");
+    const Plan& p = *plan->p;
+    if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");
+    if (name && name_cap > 0) std::snprintf(name, (size_t)name_cap, "%s", p.recorded[i].name.c_str());
+    if (flops) *flops = p.recorded[i].flops;
+    if (bytes) *bytes = p.recorded[i].bytes;
+    return CNF_OK;
+}
+
+int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream) {
+    if (!plan) return fail(CNF_E_INVALID, "null plan");
+    Plan& p = *plan->p;
+    if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");
+    CNF_TRY
+    p.recorded[i].relaunch(stream);
+    check_launch();
+    return CNF_OK;
+    CNF_CATCH
+}
+
+}  // extern "C"

@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark: images/sec of fwd + log-det (+ NLL sums) of the conditional RealNVP hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one cFlow.call(xy, +1) (zy + per-image log-det) + the NLL 4-sum over one batch of
+synthetic inputs already resident in HBM; with N>1 every rank processes its own batch
+(weak scaling, BASELINE configs[1] batch 64 per GPU) and the 4 NLL sums are all-reduced
+(the path's only exchange step, one RCCL all-reduce of 4 fp32). value = images processed by
+all ranks / max-over-ranks wall time of the K timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
+from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_16x16x4_f32) dense peak
+
+
+def synth(cfg, B, seed):
+    from arl_conditional_normalizing_flows_amd.synthetic import class_batch, sr_batch
+    H, W, D = cfg.io_shape
+    if cfg.data == 'class':
+        return class_batch(B, H, W, cfg.x_d, seed=seed)
+    return sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=seed)
+
+
+def measure_dominant_kernel(flow, stream, reps=50):
+    """Re-launch every recorded launch of the last forward with HIP events on the launch
+    stream; aggregate per kernel symbol; return the symbol with the largest total time."""
+    lib = _lib.load()
+    plan = flow._plan
+    n = lib.cnf_plan_num_recorded_launches(plan)
+    import ctypes as C
+    name = C.create_string_buffer(256)
+    fl = C.c_double()
+    by = C.c_double()
+    per = {}
+    s = torch.cuda.current_stream()
+    for i in range(n):
+        _lib.check(lib.cnf_plan_recorded_launch_info(plan, i, name, 256, C.byref(fl), C.byref(by)), 'info')
+        nm = name.value.decode()
+        if not nm.startswith('k_'):
+            continue
+        # warm
+        for _ in range(3):
+            _lib.check(lib.cnf_plan_relaunch(plan, i, stream), 'relaunch')
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            _lib.check(lib.cnf_plan_relaunch(plan, i, stream), 'relaunch')
+        e1.record(s)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        d = per.setdefault(nm, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'launches': 0})
+        d['ms'] += ms
+        d['flops'] += fl.value
+        d['bytes'] += by.value
+        d['launches'] += 1
+    return per
+
+
+def roofline_for(per):
+    name, d = max(per.items(), key=lambda kv: kv[1]['ms'])
+    t = d['ms'] / 1e3
+    tflops = d['flops'] / t / 1e12
+    gbs = d['bytes'] / t / 1e9
+    # bound = the roof the kernel's algorithmic intensity runs into first
+    ai = d['flops'] / max(d['bytes'], 1.0)
+    ridge = FP32_MFMA_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if ai >= ridge:
+        rf = {'bound': 'mfma', 'achieved': round(tflops, 3), 'peak': FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
+              'frac': round(tflops / FP32_MFMA_TFLOPS, 4)}
+    else:
+        rf = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+              'frac': round(gbs / HBM_PEAK_GBS, 4)}
+    rf.update({'kernel': name, 'launches_per_step': d['launches'],
+               'avg_launch_us': round(d['ms'] * 1e3 / d['launches'], 3),
+               'alg_flops_per_launch': d['flops'] / d['launches'],
+               'alg_bytes_per_launch': d['bytes'] / d['launches'], 'traffic': None})
+    return rf
+
+
+def cpu_baseline(cfg, budget_s=20.0):
+    """The oracle's torch-CPU fp32 op-for-op restatement of the reference graph, timed on this
+    host on a bounded sample of the same workload (rank 0, N=1 only)."""
+    try:
+        from oracle.cflow_torch_cpu import TorchCPUFlow
+    except Exception as e:  # pragma: no cover
+        return {'value': None, 'unit': 'images/s', 'cores': 0, 'kind': 'port', 'sample': f'unavailable: {e}'}
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    flow = TorchCPUFlow(**cfg.kwargs())
+    P = flow.init_params(0)
+    B = 8
+    xy = torch.from_numpy(synth(cfg, B, 123))
+    with torch.no_grad():
+        flow.log_loss(xy, P)          # warm-up
+        n_img, t0 = 0, time.perf_counter()
+        while True:
+            flow.log_loss(xy, P)
+            n_img += B
+            el = time.perf_counter() - t0
+            if el > budget_s or n_img >= 10 * B:
+                break
+    model = platform.processor() or platform.machine()
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'value': round(n_img / el, 3), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n_img} images ({n_img // B} batches of {B}) of {cfg.name} fwd+logdet+NLL, '
+                      f'{el:.1f}s, torch-CPU fp32 restatement (oracle/cflow_torch_cpu.py), {model}'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--config', default='cfg2')
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config batch)')
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    cfg = PRESETS[args.config]
+    B = args.batch or cfg.batch
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    flow = cFlow(**cfg.kwargs(), device=dev, seed=0)
+    xy = torch.from_numpy(synth(cfg, B, 1000 + rank)).to(dev)
+    zy = torch.empty_like(xy)
+    ld = torch.empty(B, device=dev)
+    per = torch.empty((B, 3), device=dev)
+    sums = torch.empty(4, device=dev)
+    ws = flow._workspace(B)
+    lib = _lib.load()
+
+    def step():
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(), xy.data_ptr(),
+                                        zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
+        _lib.check(lib.cnf_nll(flow._plan, xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
+                               sums.data_ptr(), B, st), 'nll')
+        if dist is not None:
+            dist.all_reduce(sums)
+
+    step()
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            torch.cuda.synchronize()
+        except Exception as e:  # pragma: no cover
+            print(f'# graph capture failed, eager: {e}', file=sys.stderr)
+            graph = None
+    run = graph.replay if graph is not None else step
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms = el / args.steps * 1e3
+    total_imgs = B * world * args.steps
+    value = total_imgs / el
+
+    out = None
+    if rank == 0:
+        roof = None
+        if not args.no_roofline:
+            step()   # eager forward records its launches for the measurement hooks
+            torch.cuda.synchronize()
+            per_k = measure_dominant_kernel(flow, torch.cuda.current_stream().cuda_stream)
+            roof = roofline_for(per_k)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(cfg)
+        ld_mean = ld.mean().item()
+        out = {
+            'metric': 'images/sec fwd+logdet, 32x32x3 3-scale flow @1/2/4/8 GPU; bits/dim vs ref'
+            if args.config == 'cfg2' else f'images/sec fwd+logdet ({args.config})',
+            'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(ms, 4), 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded class-conditional batch, 2% noise), '
+                                                        'seeded orthogonal-init weights',
+            'config': {'workload': f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, '
+                                   f'{B} images per GPU', 'model': f'cFlow {cfg.name}', 'global_batch': B * world,
+                       'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world} (batch shards, '
+                                                                          f'1 all-reduce of 4 fp32)',
+                       'graph': graph is not None},
+            'bits_per_dim': round(float(sums[0].item() / (B * world) / (np.log(2) * cfg.io_shape[0] * cfg.io_shape[1] * cfg.x_d)), 6),
+            'logdet_mean': ld_mean,
+            'roofline': roof,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,161 @@
+/*
+ * cnf.h — C ABI of libcnf_hip.so, the MI355X (gfx950) implementation of the
+ * conditional-RealNVP forward / inverse + Jacobian log-det hot path of
+ * USArmyResearchLab/ARL_Conditional_Normalizing_Flows.
+ *
+ * The reference is pure TensorFlow/Keras Python and has no FFI of its own; the
+ * interfaces replaced are its Python layer/model protocol, and every entry point
+ * below cites the reference function it stands in for
+ * (file:line into conv_cINN_make_model.py unless stated).
+ *
+ * Conventions
+ *   - All tensors are device pointers, NHWC, fp32, batch-first, contiguous.
+ *   - The caller allocates ALL device memory (params, activations, workspace);
+ *     the library never frees caller pointers. A plan owns only small constant
+ *     tables (index maps) that it uploads once, lazily, on first use.
+ *   - Every compute call is asynchronous on the given stream (a hipStream_t passed
+ *     as void*; NULL = default stream) and may be captured into a hipGraph.
+ *   - Return value: 0 = OK, negative = error class (CNF_E_*); the message is
+ *     available from cnf_last_error() (thread-local). No C++ exception crosses
+ *     the ABI. A plan is not thread-safe: one host thread per plan, one process
+ *     per GPU.
+ *   - Reductions are deterministic (no float atomics): repeated runs are bitwise
+ *     identical.
+ */
+#ifndef CNF_H_
+#define CNF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNF_OK 0
+#define CNF_E_INVALID (-1)   /* bad argument / shape: the reference's AssertionError */
+#define CNF_E_HIP (-2)       /* HIP runtime error */
+#define CNF_E_STATE (-3)     /* call out of order / unsupported configuration */
+
+#define CNF_GROUP_REFERENCE 0 /* late-bound Lambda closure: every group reads the last slice
+                                 (conv_cINN_base_functions.py:402) — the reference's behaviour */
+#define CNF_GROUP_INTENDED 1  /* textbook grouped conv: group j reads slice j */
+
+#define CNF_LAYER_COUPLING 0
+#define CNF_LAYER_SQUEEZE 1
+#define CNF_LAYER_FACTOR 2
+
+typedef struct cnf_plan cnf_plan;
+
+/* Constructor arguments of cFlow.__init__ (conv_cINN_make_model.py:1431-1442). */
+typedef struct cnf_flow_desc {
+    int io_h, io_w, io_d;                 /* io_shape */
+    int x_d;                              /* depth of x inside xy */
+    int num_blocks;                       /* len(squeeze_factor_block_list) */
+    const int* squeeze_factor_block_list; /* [num_blocks], entries 0/1 */
+    const int* resnext_block_list;        /* [num_blocks] */
+    const int* num_kernels_list;          /* [num_blocks] */
+    const int* cardinality_list;          /* [num_blocks] */
+    float lambda_y;                       /* default 100 */
+    int ksize;                            /* default 3 (only 3 is implemented on GPU) */
+    int layer_norm;                       /* LAYER_NORM, default 1 */
+    int dilations;                        /* DILATIONS, default 1 */
+    int group_mode;                       /* CNF_GROUP_* (default REFERENCE) */
+} cnf_flow_desc;
+
+/* One entry of cFlow.layers_list (conv_cINN_make_model.py:1630-1689). */
+typedef struct cnf_layer_info {
+    int kind;              /* CNF_LAYER_* */
+    int coupling_index;    /* ordinal among coupling layers, -1 otherwise */
+    int block;             /* coupling block */
+    int h, w, d;           /* io shape of the block (in_shape of the layer) */
+    int mask;              /* which_mask 0..3 (coupling) */
+    int hc, wc, dc1, dc2;  /* compressed u1c shape / uv2_d (coupling) */
+    int num_kernels;       /* halved for checkerboard masks (:420-423) */
+    int cardinality;
+    int num_res_blocks;
+    int num_dilations;
+    int dilations[8];
+    int num_prev_factors;  /* factor layers (:230-240) */
+} cnf_layer_info;
+
+/* Plan = cFlow.__init__ (:1431-1695): asserts, scale schedule, dilation
+ * schedule, layer list, canonical parameter table. Host-only, no GPU work. */
+int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out);
+void cnf_plan_destroy(cnf_plan* plan);
+
+int cnf_plan_num_layers(const cnf_plan* plan);
+int cnf_plan_layer_info(const cnf_plan* plan, int layer, cnf_layer_info* out);
+
+/* Canonical parameters: one flat fp32 vector, tensors in Keras order (net A,
+ * then net b, per coupling layer; Conv2D kernels HWIO, LayerNormalization
+ * gamma/beta over the flattened H*W*C axis). */
+int64_t cnf_plan_num_params(const cnf_plan* plan);
+int cnf_plan_num_param_tensors(const cnf_plan* plan);
+int cnf_plan_param_tensor(const cnf_plan* plan, int index, char* name, int name_cap,
+                          int64_t* offset, int* ndim, int shape[4]);
+
+/* Device-side auxiliary parameter image (dense grouped-conv weights built from
+ * the per-group Conv2D kernels). Size in floats; filled by cnf_pack_params,
+ * which must run again whenever the canonical params change. */
+int64_t cnf_plan_aux_floats(const cnf_plan* plan);
+int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* stream);
+
+/* Workspace bytes for a batch of B images (all activations, LN-stat partials,
+ * log-det partials). */
+size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B);
+
+/* cFlow.call(xy, direction=+1) (:1743-1772): xy[B,H,W,D] -> zy[B,H,W,D] in xy
+ * layout, logdet_per_image[B] = sum over coupling layers of sum_{h,w,c} A(u1)
+ * (the reference returns its batch mean, :1323-1326). */
+int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux,
+                     const float* xy, float* zy, float* logdet_per_image,
+                     void* workspace, int B, void* stream);
+
+/* cFlow.call(zy, direction=-1) (:1774-1798): zy -> xy. */
+int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux,
+                     const float* zy, float* xy, void* workspace, int B, void* stream);
+
+/* coupling_layer.forward_and_Jacobian (:1258-1328) for layer `layer` of
+ * layers_list: u -> v (shape of the layer's in_shape); logdet_accum[B] +=
+ * per-image sum of A(u1) (pass NULL to skip). u and v must not alias. */
+int cnf_coupling_forward(cnf_plan* plan, int layer, const float* params, const float* aux,
+                         const float* u, float* v, float* logdet_accum,
+                         void* workspace, int B, void* stream);
+
+/* coupling_layer.backward (:1333-1394): v -> u. */
+int cnf_coupling_inverse(cnf_plan* plan, int layer, const float* params, const float* aux,
+                         const float* v, float* u, void* workspace, int B, void* stream);
+
+/* squeeze_layer (:155-217): dir=+1 space_to_depth(2) in TF channel order,
+ * dir=-1 depth_to_space(2). in: [B,H,W,C] (dir=+1) or [B,H,W,4C'] (dir=-1). */
+int cnf_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, void* stream);
+
+/* Channel-window copy used by factor_out_zy_layer (:256-329):
+ * out[b,p,out_off + c] = in[b,p,in_off + c] for c < C, p < HW. */
+int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off,
+                     int C, int B, int HW, void* stream);
+
+/* cFlow.log_loss terms (:1815-1848). per_image[B*3] = (llz, lly, logdet) with
+ * llz = sum_{h,w} log N(z; 0, I_{x_d}), lly = -lambda_y * sum |y - y'|;
+ * sums[4] = (sum_i loss_i, sum_i -llz_i, sum_i -lly_i, sum_i -logdet_i),
+ * loss_i = -(llz_i + lly_i + logdet_i). Dividing sums by the (global) batch
+ * gives the reference's (loss, z_loss, y_loss, detJ_loss). */
+int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image,
+            float* per_image, float* sums, int B, void* stream);
+
+/* Measurement hooks (bench.py): number of kernel launches recorded by the last
+ * forward/inverse call on this plan, their kernel symbol names, and a re-launch
+ * of one recorded launch with identical arguments (same buffers). */
+int cnf_plan_num_recorded_launches(const cnf_plan* plan);
+int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int name_cap,
+                                  double* flops, double* bytes);
+int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream);
+
+const char* cnf_last_error(void);
+const char* cnf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CNF_H_ */

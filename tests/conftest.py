@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (ROCm GPU); run with -m gpu')
+    config.addinivalue_line('markers', 'slow: long-running CPU test')
+
+
+@pytest.fixture(scope='session')
+def lib():
+    from arl_conditional_normalizing_flows_amd import _build, _lib
+    if not _lib.LIB_PATH.exists():
+        _build.build()
+    return _lib.load()
+
+
+@pytest.fixture(scope='session')
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    from arl_conditional_normalizing_flows_amd import _build, _lib
+    if not _lib.LIB_PATH.exists():
+        _build.build()
+    return torch.device('cuda', 0)
