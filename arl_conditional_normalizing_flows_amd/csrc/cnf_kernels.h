@@ -52,8 +52,27 @@ struct CoupArgs {
     int H, W, D, mask, mask_c, hc, wc, dc1, dc2, dir;
 };
 
+// Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).
+constexpr int NETLDS_MAXBR = 8;
+struct NetLdsArgs {
+    const float* u;           // layer input [B][H][W][D]
+    float* so[2];             // outputs: raw conv_out of net A (pre-tanh) / net b, [B][hc][wc][dc2]
+    const float* params;      // canonical parameters
+    const float* aux;         // dense grouped-conv image
+    const int* offs;          // [2][offs_per_net] parameter offsets (see k_net_lds)
+    int offs_per_net;
+    int H, W, D, mask, hc, wc, dc1, dc2, nk, gc, R, nbr, ln;
+    int br_cin_off[NETLDS_MAXBR], br_cin[NETLDS_MAXBR], br_cout[NETLDS_MAXBR], br_out_off[NETLDS_MAXBR],
+        br_dil[NETLDS_MAXBR];
+    int nwin, win_off[NETLDS_MAXBR], win_len[NETLDS_MAXBR];  // disjoint union of the branch input windows
+    int sy, s1, s2;                              // LDS pixel strides (floats)
+    int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
+};
+void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
+
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st);

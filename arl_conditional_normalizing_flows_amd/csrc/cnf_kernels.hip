@@ -125,30 +125,13 @@ __device__ __forceinline__ void tile_stats(const float (&vals)[N], const bool (&
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_conv1: 1x1 convolution (conv_a / conv_b of dilated_residual_block,
-// conv_cINN_base_functions.py:561-565, 609-613) with the A operand streamed from HBM straight
-// into registers. The K (input-channel) axis is permuted so that lane (i, q) of the
-// 16x16x4 MFMA holds channels 16g + 4q + s at k-steps s = 0..3 of channel group g: one float4
-// load of x, gamma, beta per lane per group, normalised in registers (LeakyReLU -> LN), and
-// one ds_read_b128 of B per N-subtile per group (B stored [g][q][j][s] in LDS).
+// shared pieces of the convolution kernels
 // ---------------------------------------------------------------------------------------------
-template <int MR, bool VEC, int ROLE>
-__global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const ConvProb& P = a.p[blockIdx.y];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int HW = a.H * a.W;
-    const int tile = blockIdx.x;
-    const int img = tile / a.tiles_per_img;
-    const int tr = tile - img * a.tiles_per_img;
-    const int px0 = tr * a.P;
-    const int Pv = min(a.P, HW - px0);
-    const int cin = P.cin, cout = P.cout, nr = P.nr;
-    const int G = (cin + 15) >> 4;
-    const int NSJ = 16 * nr;
-    double* red = reinterpret_cast<double*>(smem);
-    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
 
+// Input-LN statistics of image `img`: wave 0 merges the producer's tile partials; (mu, rstd)
+// land in red[8], red[9]. Caller must __syncthreads() before reading them.
+__device__ __forceinline__ void stats_prologue(const ConvProb& P, int img, double* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (P.in_stats != nullptr && wave == 0) {
         double n, m, M2;
         merge_stats(P.in_stats, img, P.in_nparts, lane, n, m, M2);
@@ -157,64 +140,141 @@ __global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
             red[9] = 1.0 / sqrt(M2 / n + (double)LN_EPS);
         }
     }
-    // B image [g][q][j][s]: element (c = 16g+4q+s, j)
-    {
-        const int total = G * 16 * NSJ;
-        for (int base = 0; base < total; base += 256 * 4) {
-            float wv[4];
-            int li[4];
+}
+
+// Epilogue shared by all conv kernels. Lane (i, q) of wave w holds, for subtile s = w + 4m,
+// out[pixel pix0 + 16s + 4q + r][channel 16n + i] in acc[m][n][r]. Adds bias and the residual
+// (ALL residual loads are issued before any store: res may alias out), stores the channels of
+// the store mask, and writes the tile's LN-stat partial of LeakyReLU(out).
+template <int MR, int NR>
+__device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][NR], int img, int HW, int pix0,
+                                              int Pv, int tr, double* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int cout = P.cout;
+    float* __restrict__ out = P.out;
+    const float* res = P.res;
+    bool chv[NR], st[NR];
+    float bias[NR];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int idx = base + u * 256 + tid;
-                const int sidx = idx & 3;
-                const int rest = idx >> 2;
-                const int gq = rest / NSJ;
-                const int j = rest - gq * NSJ;
-                const int c = (gq >> 2) * 16 + (gq & 3) * 4 + sidx;
-                li[u] = idx < total ? idx : -1;
-                wv[u] = (idx < total && c < cin && j < cout) ? P.wt[(size_t)c * cout + j] : 0.f;
+    for (int n = 0; n < NR; n++) {
+        const int ch = n * 16 + i16;
+        chv[n] = ch < cout;
+        bias[n] = chv[n] ? P.bias[ch] : 0.f;
+        st[n] = chv[n] && stored(P, ch);
+    }
+    size_t oe[MR][4];
+    bool pv[MR][4];
+#pragma unroll
+    for (int m = 0; m < MR; m++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int p = (wave + 4 * m) * 16 + kq * 4 + r;
+            pv[m][r] = p < Pv;
+            oe[m][r] = ((size_t)img * HW + pix0 + (pv[m][r] ? p : 0)) * P.out_cs + P.out_off;
+        }
+    if (res != nullptr) {
+        float rv[MR][NR][4];
+#pragma unroll
+        for (int m = 0; m < MR; m++)
+#pragma unroll
+            for (int n = 0; n < NR; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) rv[m][n][r] = res[oe[m][r] + (chv[n] ? n * 16 + i16 : 0)];
+#pragma unroll
+        for (int m = 0; m < MR; m++)
+#pragma unroll
+            for (int n = 0; n < NR; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) acc[m][n][r] += rv[m][n][r];
+    }
+#pragma unroll
+    for (int m = 0; m < MR; m++)
+#pragma unroll
+        for (int n = 0; n < NR; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                acc[m][n][r] += bias[n];
+                if (pv[m][r] && st[n]) out[oe[m][r] + n * 16 + i16] = acc[m][n][r];
             }
+    if (P.out_stats != nullptr) {
+        float vals[MR * NR * 4];
+        bool valid[MR * NR * 4];
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (li[u] >= 0) lw[li[u]] = wv[u];
+        for (int m = 0; m < MR; m++)
+#pragma unroll
+            for (int n = 0; n < NR; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    vals[(m * NR + n) * 4 + r] = lrelu(acc[m][n][r]);
+                    valid[(m * NR + n) * 4 + r] = pv[m][r] && chv[n];
+                }
+        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
+    }
+}
+
+// B image [g][q][j][s] (element (c = 16g + 4q + s, column j)) of a [cin][ncol] weight matrix,
+// column j read from wt[colsrc(j) + c * ldw]; zero padded; batched loads.
+template <class ColSrc>
+__device__ __forceinline__ void stage_b_image(const float* __restrict__ wt, int ldw, int cin, int ncol, int G,
+                                              int NSJ, float* lw, ColSrc colsrc) {
+    const int tid = threadIdx.x;
+    const int total = G * 16 * NSJ;
+    for (int base = 0; base < total; base += 256 * 8) {
+        float wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int idx = base + u * 256 + tid;
+            const int sidx = idx & 3;
+            const int rest = idx >> 2;
+            const int gq = rest / NSJ;
+            const int j = rest - gq * NSJ;
+            const int c = (gq >> 2) * 16 + (gq & 3) * 4 + sidx;
+            wv[u] = (idx < total && c < cin && j < ncol) ? wt[(size_t)colsrc(j) + (size_t)c * ldw] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int idx = base + u * 256 + tid;
+            if (idx < total) lw[idx] = wv[u];
         }
     }
-    __syncthreads();
-    const bool has_ln = P.in_stats != nullptr;
-    float mu = 0.f, rstd = 1.f;
-    if (has_ln) {
-        mu = (float)red[8];
-        rstd = (float)red[9];
-    }
-    const int act = P.act;
+}
+
+// Register-streamed GEMM over the run of `npx` pixels starting at pixel p0 of image img:
+// acc[m][n] += A * B with A[p][c] = LN(LeakyReLU(in[p][c])) loaded as float4 per lane (K
+// permuted: lane (i, q) holds channels 16g + 4q + s at k-step s of channel group g) and B from
+// the LDS image lw ([g][q][j][s]). Wave w owns 16-pixel subtiles w, w+4, ... Branch-free MFMA
+// loop; pixels/channels beyond the valid range feed zeros.
+template <int MR, int NR, bool VEC>
+__device__ __forceinline__ void gemm_stream(const ConvProb& P, int img, int HW, int p0, int npx, const float* lw,
+                                            int G, float mu, float rstd, bool has_ln, f4 (&acc)[MR][NR]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
-    bool sact[MR], pval[MR];
+    const int cin = P.cin;
+    const bool act = P.act != 0;
+    constexpr int NSJ = 16 * NR;
+    bool pval[MR];
     size_t xoff[MR];
 #pragma unroll
     for (int m = 0; m < MR; m++) {
-        const int s = wave + 4 * m;
-        sact[m] = s * 16 < Pv;
-        const int p = s * 16 + i16;
-        pval[m] = p < Pv;
-        xoff[m] = (size_t)(px0 + (pval[m] ? p : 0)) * P.in_cs + P.in_off;
+        const int p = (wave + 4 * m) * 16 + i16;
+        pval[m] = p < npx;
+        xoff[m] = (size_t)(p0 + (pval[m] ? p : 0)) * P.in_cs + P.in_off;
     }
     const float* __restrict__ xb = P.in + (size_t)img * HW * P.in_cs;
     const float* __restrict__ gp = P.gamma;
     const float* __restrict__ bp = P.beta;
-
-    f4 acc[MR][4];
 #pragma unroll
     for (int m = 0; m < MR; m++)
 #pragma unroll
-        for (int n = 0; n < 4; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NR; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
 
     auto load_group = [&](int g, f4 (&xr)[MR], f4 (&gr)[MR], f4 (&br)[MR]) {
         const int c0 = 16 * g + 4 * kq;
 #pragma unroll
         for (int m = 0; m < MR; m++) {
             if (VEC) {
-                const bool ok = c0 < cin;
-                const size_t e = xoff[m] + (ok ? c0 : 0);
+                const size_t e = xoff[m] + (c0 < cin ? c0 : 0);
                 xr[m] = *reinterpret_cast<const f4*>(xb + e);
                 if (has_ln) {
                     gr[m] = *reinterpret_cast<const f4*>(gp + e);
@@ -223,8 +283,7 @@ __global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
             } else {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const bool ok = c0 + j < cin;
-                    const size_t e = xoff[m] + (ok ? c0 + j : 0);
+                    const size_t e = xoff[m] + (c0 + j < cin ? c0 + j : 0);
                     xr[m][j] = xb[e];
                     if (has_ln) {
                         gr[m][j] = gp[e];
@@ -238,6 +297,7 @@ __global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
     f4 xr[MR], gr[MR], br[MR];
 #pragma unroll
     for (int m = 0; m < MR; m++) {
+        xr[m] = f4{0.f, 0.f, 0.f, 0.f};
         gr[m] = f4{1.f, 1.f, 1.f, 1.f};
         br[m] = f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -262,20 +322,17 @@ __global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
                 if (has_ln) x = (x - mu) * rstd * gr[m][j] + br[m][j];
                 av[m][j] = (pval[m] && c0 + j < cin) ? x : 0.f;
             }
-        f4 bq[4];
+        f4 bq[NR];
         const float* brow = lw + ((size_t)(g * 4 + kq) * NSJ + i16) * 4;
 #pragma unroll
-        for (int n = 0; n < 4; n++)
-            bq[n] = (n < nr) ? *reinterpret_cast<const f4*>(brow + n * 64) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
 #pragma unroll
         for (int s = 0; s < 4; s++)
 #pragma unroll
-            for (int m = 0; m < MR; m++) {
-                if (!sact[m]) continue;
+            for (int m = 0; m < MR; m++)
 #pragma unroll
-                for (int n = 0; n < 4; n++)
-                    if (n < nr) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][s], bq[n][s], acc[m][n], 0, 0, 0);
-            }
+                for (int n = 0; n < NR; n++)
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][s], bq[n][s], acc[m][n], 0, 0, 0);
 #pragma unroll
         for (int m = 0; m < MR; m++) {
             xr[m] = xn[m];
@@ -283,108 +340,116 @@ __global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
             br[m] = bn[m];
         }
     }
-
-    // epilogue: lane holds out[pixel = 16s + 4q + r][ch = 16n + i]
-    float vals[MR * 16];
-    bool valid[MR * 16];
-    const size_t obase = (size_t)img * HW + px0;
-#pragma unroll
-    for (int m = 0; m < MR; m++) {
-        const int s = wave + 4 * m;
-#pragma unroll
-        for (int n = 0; n < 4; n++) {
-            const int ch = n * 16 + i16;
-            const bool chv = sact[m] && n < nr && ch < cout;
-            const float bias = chv ? P.bias[ch] : 0.f;
-            const bool st = chv && stored(P, ch);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int p = s * 16 + kq * 4 + r;
-                const bool ok = chv && p < Pv;
-                float v = acc[m][n][r] + bias;
-                if (ok) {
-                    const size_t oe = (obase + p) * P.out_cs + P.out_off + ch;
-                    if (P.res) v += P.res[oe];
-                    if (st) P.out[oe] = v;
-                }
-                vals[(m * 4 + n) * 4 + r] = lrelu(v);
-                valid[(m * 4 + n) * 4 + r] = ok;
-            }
-        }
-    }
-    if (P.out_stats != nullptr)
-        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_conv
+// k_conv1: 1x1 convolution (conv_a / conv_b of dilated_residual_block,
+// conv_cINN_base_functions.py:561-565, 609-613) with the A operand streamed from HBM straight
+// into registers (gemm_stream) and LN-on-load; tiles are runs of P pixels inside one image.
 // ---------------------------------------------------------------------------------------------
-template <int KS, int MR, int ROLE>
-__global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
+template <int MR, int NR, bool VEC>
+__device__ __forceinline__ void conv1_body(const ConvArgs& a, const ConvProb& P, unsigned char* smem) {
+    const int HW = a.H * a.W;
+    const int img = blockIdx.x / a.tiles_per_img;
+    const int tr = blockIdx.x - img * a.tiles_per_img;
+    const int px0 = tr * a.P;
+    const int Pv = min(a.P, HW - px0);
+    const int G = (P.cin + 15) >> 4;
+    double* red = reinterpret_cast<double*>(smem);
+    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
+    stats_prologue(P, img, red);
+    const int cout = P.cout;
+    stage_b_image(P.wt, cout, P.cin, cout, G, 16 * NR, lw, [](int j) { return j; });
+    __syncthreads();
+    const bool has_ln = P.in_stats != nullptr;
+    const float mu = has_ln ? (float)red[8] : 0.f;
+    const float rstd = has_ln ? (float)red[9] : 1.f;
+    f4 acc[MR][NR];
+    gemm_stream<MR, NR, VEC>(P, img, HW, px0, Pv, lw, G, mu, rstd, has_ln, acc);
+    conv_epilogue<MR, NR>(P, acc, img, HW, px0, Pv, tr, red);
+}
+
+template <int MR, bool VEC, int ROLE>
+__global__ __launch_bounds__(256) void k_conv1(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const ConvProb& P = a.p[blockIdx.y];
+    const ConvProb P = a.p[blockIdx.y];
+    switch (P.nr) {
+        case 1: conv1_body<MR, 1, VEC>(a, P, smem); break;
+        case 2: conv1_body<MR, 2, VEC>(a, P, smem); break;
+        case 3: conv1_body<MR, 3, VEC>(a, P, smem); break;
+        default: conv1_body<MR, 4, VEC>(a, P, smem); break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_conv: 3x3 dilated convolution as an implicit GEMM from an LDS-staged, normalised input band
+// (conv_in :1114-1119, the grouped dilated branches conv_cINN_base_functions.py:389-411, and
+// conv_out when cout > 7). Tile = TH image rows; the band (+d halo rows/cols, zero padded) is
+// staged once; A[p][k=(tap,c)] = lin[abase(p) + koff(k)], B[k][n] from LDS.
+// ---------------------------------------------------------------------------------------------
+template <int MR, int NR>
+__device__ __forceinline__ void conv3_body(const ConvArgs& a, const ConvProb& P, unsigned char* smem) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tile = blockIdx.x;
-    const int img = tile / a.tiles_per_img;
-    const int tr = tile - img * a.tiles_per_img;
+    const int img = blockIdx.x / a.tiles_per_img;
+    const int tr = blockIdx.x - img * a.tiles_per_img;
     const int H = a.H, W = a.W, TH = a.TH;
     const int HW = H * W;
     const int r0 = tr * TH;
     const int rows = min(TH, H - r0);
     const int Pv = rows * W;      // valid output pixels of this tile
     const int PT = TH * W;        // staged (padded) pixels
-    const int d = (KS == 3) ? P.dil : 0;
+    const int d = P.dil;
     const int WP = W + 2 * d;
-    const int S = P.S, cin = P.cin, K = KS * KS * cin, Kpad = P.Kpad, NS = P.NS, cout = P.cout;
-    double* red = reinterpret_cast<double*>(smem);  // 16 doubles of reduction scratch
+    const int S = P.S, cin = P.cin, K = 9 * cin, Kpad = P.Kpad, NS = P.NS, cout = P.cout;
+    double* red = reinterpret_cast<double*>(smem);
     float* lin = reinterpret_cast<float*>(smem + P.lds_in_off);
     float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
     int* lk = reinterpret_cast<int*>(smem + P.lds_k_off);
 
-    // 1) per-image stats of the input LayerNorm (merge of the producer's tile partials)
-    if (P.in_stats != nullptr && wave == 0) {
-        double n, m, M2;
-        merge_stats(P.in_stats, img, P.in_nparts, lane, n, m, M2);
-        if (lane == 0) {
-            red[8] = m;
-            red[9] = 1.0 / sqrt(M2 / n + (double)LN_EPS);
+    stats_prologue(P, img, red);
+    // weights B[k][n] (zero padded to Kpad x NS); batched loads
+    {
+        const float* __restrict__ wt = P.wt;
+        const int total = Kpad * NS;
+        for (int base = 0; base < total; base += 256 * 8) {
+            float wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int idx = base + u * 256 + tid;
+                const int k = idx / NS, n = idx - k * NS;
+                wv[u] = (idx < total && k < K && n < cout) ? wt[(size_t)k * cout + n] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int idx = base + u * 256 + tid;
+                if (idx < total) lw[idx] = wv[u];
+            }
         }
     }
-    // 2) weights B[k][n] (zero padded to Kpad x NS)
-    for (int idx = tid; idx < Kpad * NS; idx += 256) {
-        int k = idx / NS, n = idx - k * NS;
-        lw[idx] = (k < K && n < cout) ? P.wt[(size_t)k * cout + n] : 0.f;
-    }
-    // 3) per-k LDS offsets of the A operand (tap, channel)
+    // per-k LDS offsets of the A operand (tap, channel)
     for (int k = tid; k < Kpad; k += 256) {
         int off = 0;
         if (k < K) {
-            if (KS == 3) {
-                int tap = k / cin, ci = k - tap * cin;
-                int kh = tap / 3, kw = tap - kh * 3;
-                off = (kh * d * WP + kw * d) * S + ci;
-            } else {
-                off = k;
-            }
+            const int tap = k / cin, ci = k - tap * cin;
+            const int kh = tap / 3, kw = tap - kh * 3;
+            off = (kh * d * WP + kw * d) * S + ci;
         }
         lk[k] = off;
     }
     __syncthreads();
-    float mu = 0.f, rstd = 1.f;
     const bool has_ln = P.in_stats != nullptr;
-    if (has_ln) {
-        mu = (float)red[8];
-        rstd = (float)red[9];
-    }
-    // 4) stage the (normalised) input tile (+halo) into LDS
-    const float* __restrict__ inb = P.in + (size_t)img * HW * P.in_cs + P.in_off;
-    const float* __restrict__ gb = P.gamma ? P.gamma + P.in_off : nullptr;
-    const float* __restrict__ bb = P.beta ? P.beta + P.in_off : nullptr;
-    const int act = P.act;
-    if (KS == 3) {
+    const float mu = has_ln ? (float)red[8] : 0.f;
+    const float rstd = has_ln ? (float)red[9] : 1.f;
+    // stage the (normalised) input band (+halo) into LDS; magic-number divisions, batched loads
+    {
+        const float* __restrict__ inb = P.in + (size_t)img * HW * P.in_cs + P.in_off;
+        const float* __restrict__ gb = has_ln ? P.gamma + P.in_off : nullptr;
+        const float* __restrict__ bb = has_ln ? P.beta + P.in_off : nullptr;
+        const bool act = P.act != 0;
         const int SR = TH + 2 * d;
         const int total = SR * WP * cin;
         const uint32_t cmag = P.cin_mag, wmag = P.wp_mag;
+        const int in_cs = P.in_cs;
         for (int base = 0; base < total; base += 256 * 4) {
             float xv[4], gv[4], bv[4];
             int li[4];
@@ -399,11 +464,11 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
                 const int row = r0 - d + rr, col = cc - d;
                 li[u] = (idx < total) ? pix * S + c : -1;
                 ok[u] = idx < total && row >= 0 && row < H && col >= 0 && col < W;
-                const size_t e = ok[u] ? (size_t)(row * W + col) * P.in_cs + c : 0;
-                xv[u] = ok[u] ? inb[e] : 0.f;
+                const size_t e = ok[u] ? (size_t)(row * W + col) * in_cs + c : 0;
+                xv[u] = inb[e];
                 if (has_ln) {
-                    gv[u] = ok[u] ? gb[e] : 0.f;
-                    bv[u] = ok[u] ? bb[e] : 0.f;
+                    gv[u] = gb[e];
+                    bv[u] = bb[e];
                 }
             }
 #pragma unroll
@@ -418,80 +483,131 @@ __global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
     }
     __syncthreads();
 
-    // 5) implicit GEMM on v_mfma_f32_16x16x4_f32. Wave w owns 16-pixel subtiles w, w+4, ...
-    //    A[i][k] = lin[abase(i) + lk[k]], lane holds A[lane&15][lane>>4], B[lane>>4][lane&15].
-    const int nsub = (PT + 15) >> 4;
     const int i16 = lane & 15, kq = lane >> 4;
-    const int nr = P.nr;
     int abase[MR];
-    bool sact[MR];
 #pragma unroll
     for (int m = 0; m < MR; m++) {
-        int s = wave + 4 * m;
-        sact[m] = s < nsub;
-        int p = s * 16 + i16;
+        int p = (wave + 4 * m) * 16 + i16;
         if (p >= PT) p = 0;
-        if (KS == 3) {
-            int pr = p / W, pc = p - pr * W;
-            abase[m] = (pr * WP + pc) * S;
-        } else {
-            abase[m] = p * S;
-        }
+        const int pr = p / W, pc = p - pr * W;
+        abase[m] = (pr * WP + pc) * S;
     }
-    f4 acc[MR][4];
+    f4 acc[MR][NR];
 #pragma unroll
     for (int m = 0; m < MR; m++)
 #pragma unroll
-        for (int n = 0; n < 4; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll 2
+        for (int n = 0; n < NR; n++) acc[m][n] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
     for (int k0 = 0; k0 < Kpad; k0 += 4) {
         const int kr = k0 + kq;
         const int ko = lk[kr];
         const float* wrow = lw + kr * NS + i16;
-        float bv[4];
+        float bv[NR];
 #pragma unroll
-        for (int n = 0; n < 4; n++) bv[n] = (n < nr) ? wrow[n * 16] : 0.f;
+        for (int n = 0; n < NR; n++) bv[n] = wrow[n * 16];
 #pragma unroll
         for (int m = 0; m < MR; m++) {
-            if (sact[m]) {
-                float av = lin[abase[m] + ko];
+            const float av = lin[abase[m] + ko];
 #pragma unroll
-                for (int n = 0; n < 4; n++)
-                    if (n < nr) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[n], acc[m][n], 0, 0, 0);
-            }
+            for (int n = 0; n < NR; n++)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[n], acc[m][n], 0, 0, 0);
         }
     }
+    conv_epilogue<MR, NR>(P, acc, img, HW, r0 * W, Pv, tr, red);
+}
 
-    // 6) epilogue: bias, residual, store, LN-stat partials of LeakyReLU(out)
-    float vals[MR * 16];
-    bool valid[MR * 16];
-    const size_t obase = ((size_t)img * HW + (size_t)r0 * W);
+template <int KS, int MR, int ROLE>
+__global__ __launch_bounds__(256) void k_conv(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ConvProb P = a.p[blockIdx.y];
+    switch (P.nr) {
+        case 1: conv3_body<MR, 1>(a, P, smem); break;
+        case 2: conv3_body<MR, 2>(a, P, smem); break;
+        case 3: conv3_body<MR, 3>(a, P, smem); break;
+        default: conv3_body<MR, 4>(a, P, smem); break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_convtap: 3x3 (dilation 1) convolution with few output channels (conv_out, cout <= 7;
+// conv_cINN_make_model.py:1150-1155, 1190-1195) as a tap-decomposed GEMM: over the halo'd band of
+// rows [r0-1, r0+rows+1) compute C[p][(tap, o)] = sum_c LN(LeakyReLU(y))[p][c] * W[tap][c][o]
+// (K = cin, N = 9*cout, register-streamed A), then out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]
+// from LDS. 3x fewer MFMAs than the implicit GEMM at cout=2 and no per-k address table.
+// ---------------------------------------------------------------------------------------------
+template <int MT, int NR, bool VEC>
+__device__ __forceinline__ void convtap_body(const ConvArgs& a, const ConvProb& P, unsigned char* smem) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int H = a.H, W = a.W, HW = H * W, TH = a.TH;
+    const int img = blockIdx.x / a.tiles_per_img;
+    const int tr = blockIdx.x - img * a.tiles_per_img;
+    const int r0 = tr * TH;
+    const int rows = min(TH, H - r0);
+    const int rb0 = max(r0 - 1, 0), rb1 = min(r0 + rows + 1, H);
+    const int nband = (rb1 - rb0) * W;
+    const int cin = P.cin, cout = P.cout;
+    const int G = (cin + 15) >> 4;
+    constexpr int NSJ = 16 * NR;
+    constexpr int CS = NSJ + 1;   // LDS row stride of the C tile
+    double* red = reinterpret_cast<double*>(smem);
+    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
+    float* lc = reinterpret_cast<float*>(smem + P.lds_in_off);
+
+    stats_prologue(P, img, red);
+    // column j = tap*cout + o of the tap GEMM reads HWIO weight (tap, c, o) = wt[(tap*cin + c)*cout + o]
+    stage_b_image(P.wt, cout, cin, 9 * cout, G, NSJ, lw, [cin, cout](int j) {
+        const int tap = j / cout, o = j - tap * cout;
+        return tap * cin * cout + o;
+    });
+    __syncthreads();
+    const bool has_ln = P.in_stats != nullptr;
+    const float mu = has_ln ? (float)red[8] : 0.f;
+    const float rstd = has_ln ? (float)red[9] : 1.f;
+    f4 acc[MT][NR];
+    gemm_stream<MT, NR, VEC>(P, img, HW, rb0 * W, nband, lw, G, mu, rstd, has_ln, acc);
+    const int i16 = lane & 15, kq = lane >> 4;
 #pragma unroll
-    for (int m = 0; m < MR; m++) {
-        const int s = wave + 4 * m;
+    for (int m = 0; m < MT; m++)
 #pragma unroll
-        for (int n = 0; n < 4; n++) {
-            const int ch = n * 16 + i16;
-            const bool chv = sact[m] && n < nr && ch < cout;
-            const float bias = chv ? P.bias[ch] : 0.f;
+        for (int n = 0; n < NR; n++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int p = s * 16 + kq * 4 + r;
-                const bool ok = chv && p < Pv;
-                float v = acc[m][n][r] + bias;
-                if (ok) {
-                    size_t oe = (obase + p) * P.out_cs + P.out_off + ch;
-                    if (P.res) v += P.res[oe];
-                    if (stored(P, ch)) P.out[oe] = v;
-                }
-                vals[(m * 4 + n) * 4 + r] = lrelu(v);
-                valid[(m * 4 + n) * 4 + r] = ok;
+                const int p = (wave + 4 * m) * 16 + kq * 4 + r;
+                if (p < nband) lc[p * CS + n * 16 + i16] = acc[m][n][r];
+            }
+    __syncthreads();
+    const int nout = rows * W * cout;
+    float* __restrict__ out = P.out;
+    for (int e = tid; e < nout; e += 256) {
+        const int p = e / cout, o = e - p * cout;
+        const int pr = p / W, pc = p - pr * W;
+        const int row = r0 + pr;
+        float s1 = P.bias[o];
+#pragma unroll
+        for (int kh = 0; kh < 3; kh++) {
+            const int sr = row + kh - 1;
+            if (sr < 0 || sr >= H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; kw++) {
+                const int sc = pc + kw - 1;
+                if (sc < 0 || sc >= W) continue;
+                s1 += lc[((sr - rb0) * W + sc) * CS + (kh * 3 + kw) * cout + o];
             }
         }
+        out[((size_t)img * HW + (size_t)row * W + pc) * P.out_cs + P.out_off + o] = s1;
     }
-    if (P.out_stats != nullptr)
-        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
+}
+
+template <int MT, bool VEC>
+__global__ __launch_bounds__(256) void k_convtap(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ConvProb P = a.p[blockIdx.y];
+    switch (P.nr) {
+        case 1: convtap_body<MT, 1, VEC>(a, P, smem); break;
+        case 2: convtap_body<MT, 2, VEC>(a, P, smem); break;
+        case 3: convtap_body<MT, 3, VEC>(a, P, smem); break;
+        default: convtap_body<MT, 4, VEC>(a, P, smem); break;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -739,6 +855,15 @@ void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int
     CNF_CONV1_CASE(2, false, ROLE_CONV_A)
     CNF_CONV1_CASE(2, false, ROLE_CONV_B)
 #undef CNF_CONV1_CASE
+}
+
+void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
+    dim3 g(grid_x, a.nprob), b(256);
+#define CNF_TAP_CASE(MT_, V_) \
+    if (mt == MT_ && vec == V_) { hipLaunchKernelGGL((k_convtap<MT_, V_>), g, b, lds, st, a); return; }
+    CNF_TAP_CASE(1, true) CNF_TAP_CASE(2, true) CNF_TAP_CASE(3, true) CNF_TAP_CASE(4, true) CNF_TAP_CASE(6, true)
+    CNF_TAP_CASE(1, false) CNF_TAP_CASE(2, false) CNF_TAP_CASE(3, false) CNF_TAP_CASE(4, false) CNF_TAP_CASE(6, false)
+#undef CNF_TAP_CASE
 }
 
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,

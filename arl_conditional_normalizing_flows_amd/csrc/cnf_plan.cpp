@@ -293,6 +293,28 @@ Plan* build_plan(const cnf_flow_desc* d) {
             }
         }
 
+        // k_net_lds offset tables
+        require(p.n_params < (1ll << 31) && p.n_aux < (1ll << 31), "parameter image exceeds 2^31 floats");
+        for (auto& c : p.couplings) {
+            for (int net = 0; net < 2; net++) {
+                const NetParams& np = c.net[net];
+                std::vector<int> o = {(int)np.conv_in_k, (int)np.conv_in_b};
+                for (const auto& rb : np.rb) {
+                    for (int64_t v : {rb.ln1g, rb.ln1b, rb.conv_a_k, rb.conv_a_b, rb.ln2g, rb.ln2b, rb.ln3g, rb.ln3b,
+                                      rb.conv_b_k, rb.conv_b_b})
+                        o.push_back((int)std::max<int64_t>(v, 0));
+                    for (size_t bi = 0; bi < c.br.size(); bi++) {
+                        o.push_back((int)rb.aux_w[bi]);
+                        o.push_back((int)rb.aux_b[bi]);
+                    }
+                }
+                for (int64_t v : {np.ln_out_g, np.ln_out_b, np.conv_out_k, np.conv_out_b})
+                    o.push_back((int)std::max<int64_t>(v, 0));
+                c.lds_offs_per_net = (int)o.size();
+                c.lds_offs.insert(c.lds_offs.end(), o.begin(), o.end());
+            }
+        }
+
         // squeeze/factor boundary maps. orig[i] = position in the xy layout of element i of
         // the current block layout: the forward's final restoration (:1762-1770) is the exact
         // inverse of the squeeze/factor chain, so every element returns to where it started.
@@ -341,6 +363,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
             p.host_table.insert(p.host_table.end(), b.fac_src.begin(), b.fac_src.end());
             b.dev_fac_orig = (int)p.host_table.size();
             p.host_table.insert(p.host_table.end(), b.fac_orig.begin(), b.fac_orig.end());
+        }
+        for (auto& c : p.couplings) {
+            c.dev_lds_offs = (int)p.host_table.size();
+            p.host_table.insert(p.host_table.end(), c.lds_offs.begin(), c.lds_offs.end());
         }
         p.dev_final_orig = (int)p.host_table.size();
         p.host_table.insert(p.host_table.end(), p.final_orig.begin(), p.final_orig.end());

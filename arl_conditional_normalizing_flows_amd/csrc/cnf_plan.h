@@ -41,6 +41,12 @@ struct Coupling {
     std::vector<Branch> br;
     int gc = 0;               // concat width of the grouped stage
     NetParams net[2];         // 0 = A (scale), 1 = b (translation)
+    // k_net_lds parameter-offset table: [net][conv_in_k, conv_in_b, per rb (ln1g, ln1b, conv_a_k,
+    // conv_a_b, ln2g, ln2b, ln3g, ln3b, conv_b_k, conv_b_b, aux_w/aux_b per branch), ln_out_g,
+    // ln_out_b, conv_out_k, conv_out_b]; offsets into params (aux offsets into the aux image)
+    std::vector<int> lds_offs;
+    int lds_offs_per_net = 0;
+    int dev_lds_offs = -1;    // offset into the device table
 };
 
 struct Layer {
@@ -110,6 +116,7 @@ struct Plan {
     int device = -1;
     // launch recording
     bool record = true;
+    bool use_netlds = true;   // whole-net-in-LDS kernel for layers that fit (CNF_NETLDS=0 disables)
     std::vector<Recorded> recorded;
 
     WsLayout layout(int B) const;

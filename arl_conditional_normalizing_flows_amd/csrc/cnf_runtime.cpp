@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -311,6 +312,156 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
     }
 }
 
+// tap-decomposed 3x3 (dilation 1, cout <= 7): see k_convtap
+static void convtap_launch(Exec& E, int h, int w, const std::vector<ProbSpec>& probs) {
+    ConvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    Geo g = conv_geo(h, w);
+    a.H = h;
+    a.W = w;
+    a.TH = g.TH;
+    a.tiles_per_img = g.tiles;
+    a.nprob = (int)probs.size();
+    a.B = E.B;
+    const int nband = (g.TH + 2) * w;
+    int mt = (nband + 63) / 64;
+    if (mt == 5) mt = 6;
+    if (mt > 6) throw std::invalid_argument("tap conv band too large");
+    size_t lds = 0;
+    double flops = 0, bytes = 0;
+    const double HWB = (double)h * w * E.B;
+    bool vec = true;
+    for (size_t i = 0; i < probs.size(); i++) {
+        const ProbSpec& s = probs[i];
+        ConvProb& q = a.p[i];
+        q.in = s.in;
+        q.in_stats = s.in_stats;
+        q.gamma = s.gamma;
+        q.beta = s.beta;
+        q.wt = s.wt;
+        q.bias = s.bias;
+        q.out = s.out;
+        q.in_cs = s.in_cs;
+        q.in_off = s.in_off;
+        q.cin = s.cin;
+        q.in_nparts = s.in_nparts;
+        q.out_cs = s.out_cs;
+        q.out_off = s.out_off;
+        q.cout = s.cout;
+        q.act = s.act;
+        q.dil = 1;
+        q.st_mask_lo = q.st_mask_hi = 0xffffffffu;
+        if (9 * s.cout > 64) throw std::invalid_argument("tap conv needs 9*cout <= 64");
+        q.nr = (9 * s.cout + 15) / 16;
+        const int NSJ = 16 * q.nr;
+        const int G = (s.cin + 15) / 16;
+        size_t off = 128;
+        q.lds_w_off = (int)off;
+        off = align_up(off + (size_t)G * 16 * NSJ * 4, 16);
+        q.lds_in_off = (int)off;
+        off = align_up(off + (size_t)nband * (NSJ + 1) * 4, 16);
+        q.lds_k_off = (int)off;
+        off = align_up(off + (size_t)NSJ * 4, 16);
+        lds = std::max(lds, off);
+        if (s.cin % 4 || s.in_cs % 4 || s.in_off % 4) vec = false;
+        flops += 2.0 * HWB * 9 * s.cin * s.cout;
+        bytes += 4.0 * (HWB * s.cin + HWB * s.cout + (s.in_stats ? 2.0 * h * w * s.cin : 0.0) + 9.0 * s.cin * s.cout);
+    }
+    if (lds > 160 * 1024) throw std::invalid_argument("tap conv exceeds the LDS budget");
+    const int ilds = (int)lds, grid_x = E.B * g.tiles;
+    std::string name = std::string("k_convtap<") + std::to_string(mt) + (vec ? ",vec" : ",scalar") + ",conv_out>";
+    E.record(name, flops, bytes, [mt, vec, a, grid_x, ilds](void* st) {
+        launch_convtap(mt, vec, a, grid_x, ilds, (hipStream_t)st);
+    });
+}
+
+// k_net_lds geometry for coupling c; returns the LDS bytes (0 if the layer cannot use it)
+static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
+    std::memset(&a, 0, sizeof(a));
+    if ((int)c.br.size() > NETLDS_MAXBR) return 0;
+    for (const Branch& b : c.br)
+        if (b.dil > 16) return 0;
+    const int HW = c.hc * c.wc;
+    a.H = c.H;
+    a.W = c.W;
+    a.D = c.D;
+    a.mask = c.mask;
+    a.hc = c.hc;
+    a.wc = c.wc;
+    a.dc1 = c.dc1;
+    a.dc2 = c.dc2;
+    a.nk = c.nk;
+    a.gc = c.gc;
+    a.R = c.R;
+    a.nbr = (int)c.br.size();
+    a.ln = p.desc.layer_norm;
+    for (int i = 0; i < a.nbr; i++) {
+        a.br_cin_off[i] = c.br[i].cin_off;
+        a.br_cin[i] = c.br[i].cin;
+        a.br_cout[i] = c.br[i].cout;
+        a.br_out_off[i] = c.br[i].out_off;
+        a.br_dil[i] = c.br[i].dil;
+    }
+    {   // disjoint union of the grouped branches' input channel windows (normalised once, in place)
+        std::vector<std::pair<int, int>> iv;
+        for (const Branch& b : c.br) iv.push_back({b.cin_off, b.cin_off + b.cin});
+        std::sort(iv.begin(), iv.end());
+        std::vector<std::pair<int, int>> mg;
+        for (auto& x : iv) {
+            if (!mg.empty() && x.first <= mg.back().second)
+                mg.back().second = std::max(mg.back().second, x.second);
+            else
+                mg.push_back(x);
+        }
+        if ((int)mg.size() > NETLDS_MAXBR) return 0;
+        a.nwin = (int)mg.size();
+        for (int i = 0; i < a.nwin; i++) {
+            a.win_off[i] = mg[i].first;
+            a.win_len[i] = mg[i].second - mg[i].first;
+        }
+    }
+    a.offs_per_net = c.lds_offs_per_net;
+    a.sy = lds_stride(c.nk);
+    a.s1 = lds_stride(c.nk);
+    a.s2 = lds_stride(std::max(std::max(c.gc, c.nk), std::max(c.dc1, c.dc2)));
+    auto ns_of = [](int cout) {
+        int ns = (cout + 15) / 16 * 16;
+        if (ns % 32 == 0) ns += 16;
+        return ns;
+    };
+    auto kp = [](int k) { return (k + 3) / 4 * 4; };
+    size_t wmax = (size_t)kp(9 * c.dc1) * ns_of(c.nk);
+    wmax = std::max(wmax, (size_t)kp(c.nk) * ns_of(c.nk));
+    wmax = std::max(wmax, (size_t)kp(c.gc) * ns_of(c.nk));
+    wmax = std::max(wmax, (size_t)kp(9 * c.nk) * ns_of(c.dc2));
+    int kmax = std::max(kp(9 * c.dc1), kp(9 * c.nk));
+    for (const Branch& b : c.br) {
+        wmax = std::max(wmax, (size_t)kp(9 * b.cin) * ns_of(b.cout));
+        kmax = std::max(kmax, kp(9 * b.cin));
+    }
+    if (c.dc2 > 64 || c.nk > 64) return 0;
+    size_t off = 128;
+    a.off_y = (int)off;
+    off = align_up(off + (size_t)HW * a.sy * 4, 16);
+    a.off_t1 = (int)off;
+    off = align_up(off + (size_t)HW * a.s1 * 4, 16);
+    a.off_t2 = (int)off;
+    off = align_up(off + (size_t)HW * a.s2 * 4, 16);
+    a.off_w = (int)off;
+    off = align_up(off + wmax * 4, 16);
+    a.off_k = (int)off;
+    off = align_up(off + (size_t)kmax * 4, 16);
+    return off <= 160 * 1024 ? off : 0;
+}
+
+static double net_flops(const Coupling& c) {
+    const double HW = (double)c.hc * c.wc;
+    double f = 9.0 * c.dc1 * c.nk + 9.0 * c.nk * c.dc2;
+    double rb = (double)c.nk * c.nk + (double)c.gc * c.nk;
+    for (const Branch& b : c.br) rb += 9.0 * b.cin * b.cout;
+    return 2.0 * HW * (f + c.R * rb);
+}
+
 // One coupling layer: u -> v. dir=+1 forward (ld_part may collect Σs), dir=-1 inverse.
 static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir) {
     const int B = E.B;
@@ -321,6 +472,22 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     const int nt1 = conv1_geo(c.hc, c.wc).tiles;    // ... by a 1x1 launch
     const int nbr = (int)c.br.size();
     const bool ln = E.p.desc.layer_norm != 0;
+    float* so0 = E.at<float>(L.so[0]);
+    float* so1 = E.at<float>(L.so[1]);
+    NetLdsArgs na;
+    const size_t nlds = E.p.use_netlds ? netlds_setup(E.p, c, na) : 0;
+    if (nlds > 0) {
+        na.u = u;
+        na.so[0] = so0;
+        na.so[1] = so1;
+        na.params = P;
+        na.aux = X;
+        na.offs = E.p.dev_table + c.dev_lds_offs;
+        const int ilds = (int)nlds;
+        const double fl = 2.0 * B * net_flops(c);
+        const double by = 4.0 * B * (double)c.hc * c.wc * (c.dc1 + c.dc2) * 2;
+        E.record("k_net_lds", fl, by, [na, B, ilds](void* st) { launch_net_lds(na, B, ilds, (hipStream_t)st); });
+    } else {
     float* u1c = E.at<float>(L.u1c);
     {
         const float* uu = u;
@@ -398,15 +565,19 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                   ln ? P + np.ln_out_b : nullptr, 1, P + np.conv_out_k, P + np.conv_out_b, so[n],
                                   c.dc2, 0, c.dc2, nullptr, nullptr, 0, 0, 1});
         }
-        conv_launch(E, 3, ROLE_CONV_OUT, c.hc, c.wc, pr);
+        if (9 * c.dc2 <= 64)
+            convtap_launch(E, c.hc, c.wc, pr);
+        else
+            conv_launch(E, 3, ROLE_CONV_OUT, c.hc, c.wc, pr);
     }
+    }  // streamed path
     // affine coupling law + decompress + log-det partials
     {
         CoupArgs ca;
         ca.u = u;
         ca.v = v;
-        ca.s_pre = so[0];
-        ca.t = so[1];
+        ca.s_pre = so0;
+        ca.t = so1;
         ca.tanh_w = P + c.net[0].tanh_w;
         ca.ld_part = ld_part;
         ca.H = c.H;
@@ -465,6 +636,7 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     *out = nullptr;
     CNF_TRY
     Plan* p = build_plan(desc);
+    if (const char* e = std::getenv("CNF_NETLDS")) p->use_netlds = std::atoi(e) != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     *out = new cnf_plan{p};

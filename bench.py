@@ -227,6 +227,12 @@ def main():
             torch.cuda.synchronize()
             per_k = measure_dominant_kernel(flow, torch.cuda.current_stream().cuda_stream)
             roof = roofline_for(per_k)
+            tot = sum(d['ms'] for d in per_k.values())
+            print(f'# per-kernel (re-launched in isolation): total {tot:.3f} ms/step', file=sys.stderr)
+            for nm, d in sorted(per_k.items(), key=lambda kv: -kv[1]['ms']):
+                t = d['ms'] / 1e3
+                print(f'#  {nm:34s} {d["ms"]:8.3f} ms  x{d["launches"]:3d}  {d["flops"] / t / 1e12:7.2f} TF/s '
+                      f'{d["bytes"] / t / 1e9:8.1f} GB/s', file=sys.stderr)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg)

@@ -13,12 +13,15 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 
-def _setup(name, B, group_mode='reference', seed=0):
+def _setup(name, B, group_mode='reference', seed=0, netlds=True):
+    import os
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    os.environ['CNF_NETLDS'] = '1' if netlds else '0'
     cfg = PRESETS[name]
     kw = cfg.kwargs()
     kw['group_mode'] = group_mode
     flow = cFlow(**kw)
+    os.environ.pop('CNF_NETLDS', None)
     ora = OracleCFlow(**kw)
     P = ora.init_params(seed)
     flow.set_weights(P)
@@ -42,33 +45,35 @@ def _err(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
 
 
-CASES = [('tiny', 2, 'reference'), ('small', 3, 'reference'), ('small', 2, 'intended'),
-         ('cfg2', 2, 'reference'), ('cfg3', 2, 'reference'), ('ref_default', 2, 'reference')]
+CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('small', 2, 'intended', True),
+         ('cfg2', 2, 'reference', True), ('cfg3', 2, 'reference', True), ('ref_default', 2, 'reference', True),
+         # the streamed (multi-kernel) path for every layer
+         ('small', 3, 'reference', False), ('cfg2', 2, 'reference', False), ('ref_default', 2, 'reference', False)]
 
 
-@pytest.mark.parametrize('name,B,gm', CASES)
-def test_forward_logdet_matches_oracle(gpu, name, B, gm):
-    flow, ora, P, xy = _setup(name, B, gm)
+@pytest.mark.parametrize('name,B,gm,netlds', CASES)
+def test_forward_logdet_matches_oracle(gpu, name, B, gm, netlds):
+    flow, ora, P, xy = _setup(name, B, gm, netlds=netlds)
     zy_ref, ld_ref = ora.forward(xy, P)
     zy, ld = flow(torch.from_numpy(xy).to(gpu), 1, per_image_logdet=True)
     torch.cuda.synchronize()
     e_zy = _err(zy.cpu().numpy(), zy_ref)
     ld_g = ld.cpu().numpy().astype(np.float64)
     e_ld = np.max(np.abs(ld_g - ld_ref))
-    print(f'{name} {gm}: zy rel err {e_zy:.3e}, logdet abs err {e_ld:.3e} (|ref| {np.abs(ld_ref).max():.3e})')
+    print(f'{name} {gm} lds={netlds}: zy rel err {e_zy:.3e}, logdet abs err {e_ld:.3e} (|ref| {np.abs(ld_ref).max():.3e})')
     assert e_zy < RTOL
     assert e_ld <= RTOL * max(np.abs(ld_ref).max(), 1.0) * 10
 
 
-@pytest.mark.parametrize('name,B,gm', CASES)
-def test_inverse_matches_oracle(gpu, name, B, gm):
-    flow, ora, P, xy = _setup(name, B, gm)
+@pytest.mark.parametrize('name,B,gm,netlds', CASES)
+def test_inverse_matches_oracle(gpu, name, B, gm, netlds):
+    flow, ora, P, xy = _setup(name, B, gm, netlds=netlds)
     zy_ref, _ = ora.forward(xy, P)
     x_ref = ora.inverse(zy_ref, P)
     x = flow(torch.from_numpy(zy_ref.astype(np.float32)).to(gpu), -1)
     torch.cuda.synchronize()
     e = _err(x.cpu().numpy(), x_ref)
-    print(f'{name} {gm}: inverse rel err {e:.3e}')
+    print(f'{name} {gm} lds={netlds}: inverse rel err {e:.3e}')
     assert e < RTOL
 
 
