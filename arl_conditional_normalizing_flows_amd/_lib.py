@@ -30,7 +30,8 @@ class cnf_layer_info(C.Structure):
                 ('h', C.c_int), ('w', C.c_int), ('d', C.c_int), ('mask', C.c_int),
                 ('hc', C.c_int), ('wc', C.c_int), ('dc1', C.c_int), ('dc2', C.c_int),
                 ('num_kernels', C.c_int), ('cardinality', C.c_int), ('num_res_blocks', C.c_int),
-                ('num_dilations', C.c_int), ('dilations', C.c_int * 8), ('num_prev_factors', C.c_int)]
+                ('num_dilations', C.c_int), ('dilations', C.c_int * 8), ('num_prev_factors', C.c_int),
+                ('fused_net', C.c_int)]
 
 
 # (name, restype, argtypes)

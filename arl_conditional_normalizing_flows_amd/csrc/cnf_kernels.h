@@ -65,10 +65,14 @@ struct NetLdsArgs {
     int br_cin_off[NETLDS_MAXBR], br_cin[NETLDS_MAXBR], br_cout[NETLDS_MAXBR], br_out_off[NETLDS_MAXBR],
         br_dil[NETLDS_MAXBR];
     int nwin, win_off[NETLDS_MAXBR], win_len[NETLDS_MAXBR];  // disjoint union of the branch input windows
-    int sy, s1, s2;                              // LDS pixel strides (floats)
+    int sy, s1, s2, su;                          // LDS pixel strides (floats)
+    int co_tap, co_t9, ci_t9;                    // packed formats of conv_out / conv_in (else PK_KN)
+    int br_t9[NETLDS_MAXBR];                     // grouped branch packed as PK_T9 (else PK_KN)
+    const float* zero_bias;                      // >= 64 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
 };
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
+int read_stamps(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);

@@ -213,29 +213,23 @@ __device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][N
     }
 }
 
-// B image [g][q][j][s] (element (c = 16g + 4q + s, column j)) of a [cin][ncol] weight matrix,
-// column j read from wt[colsrc(j) + c * ldw]; zero padded; batched loads.
-template <class ColSrc>
-__device__ __forceinline__ void stage_b_image(const float* __restrict__ wt, int ldw, int cin, int ncol, int G,
-                                              int NSJ, float* lw, ColSrc colsrc) {
-    const int tid = threadIdx.x;
-    const int total = G * 16 * NSJ;
-    for (int base = 0; base < total; base += 256 * 8) {
-        float wv[8];
+// Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.
+template <int NTH>
+__device__ __forceinline__ void copy_to_lds(const float* __restrict__ src, float* dst, int n) {
+    const int n4 = n >> 2;
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+    f4* d4 = reinterpret_cast<f4*>(dst);
+    for (int base = 0; base < n4; base += NTH * 8) {
+        f4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const int idx = base + u * 256 + tid;
-            const int sidx = idx & 3;
-            const int rest = idx >> 2;
-            const int gq = rest / NSJ;
-            const int j = rest - gq * NSJ;
-            const int c = (gq >> 2) * 16 + (gq & 3) * 4 + sidx;
-            wv[u] = (idx < total && c < cin && j < ncol) ? wt[(size_t)colsrc(j) + (size_t)c * ldw] : 0.f;
+            const int i = base + u * NTH + (int)threadIdx.x;
+            v[u] = i < n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const int idx = base + u * 256 + tid;
-            if (idx < total) lw[idx] = wv[u];
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n4) d4[i] = v[u];
         }
     }
 }
@@ -359,7 +353,8 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, const ConvProb& P,
     float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
     stats_prologue(P, img, red);
     const int cout = P.cout;
-    stage_b_image(P.wt, cout, P.cin, cout, G, 16 * NR, lw, [](int j) { return j; });
+    copy_to_lds<256>(P.wt, lw, G * 16 * 16 * NR);   // pre-packed B image (PK_1X1)
+    (void)cout;
     __syncthreads();
     const bool has_ln = P.in_stats != nullptr;
     const float mu = has_ln ? (float)red[8] : 0.f;
@@ -407,25 +402,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a, const ConvProb& P,
     int* lk = reinterpret_cast<int*>(smem + P.lds_k_off);
 
     stats_prologue(P, img, red);
-    // weights B[k][n] (zero padded to Kpad x NS); batched loads
-    {
-        const float* __restrict__ wt = P.wt;
-        const int total = Kpad * NS;
-        for (int base = 0; base < total; base += 256 * 8) {
-            float wv[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int idx = base + u * 256 + tid;
-                const int k = idx / NS, n = idx - k * NS;
-                wv[u] = (idx < total && k < K && n < cout) ? wt[(size_t)k * cout + n] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int idx = base + u * 256 + tid;
-                if (idx < total) lw[idx] = wv[u];
-            }
-        }
-    }
+    copy_to_lds<256>(P.wt, lw, Kpad * NS);   // pre-packed [Kpad][NS] (PK_KN)
     // per-k LDS offsets of the A operand (tap, channel)
     for (int k = tid; k < Kpad; k += 256) {
         int off = 0;
@@ -554,11 +531,7 @@ __device__ __forceinline__ void convtap_body(const ConvArgs& a, const ConvProb& 
     float* lc = reinterpret_cast<float*>(smem + P.lds_in_off);
 
     stats_prologue(P, img, red);
-    // column j = tap*cout + o of the tap GEMM reads HWIO weight (tap, c, o) = wt[(tap*cin + c)*cout + o]
-    stage_b_image(P.wt, cout, cin, 9 * cout, G, NSJ, lw, [cin, cout](int j) {
-        const int tap = j / cout, o = j - tap * cout;
-        return tap * cin * cout + o;
-    });
+    copy_to_lds<256>(P.wt, lw, G * 16 * NSJ);   // pre-packed tap B image (PK_TAP)
     __syncthreads();
     const bool has_ln = P.in_stats != nullptr;
     const float mu = has_ln ? (float)red[8] : 0.f;

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "cnf_kernels.h"
 
@@ -44,42 +45,103 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
     return t;
 }
 
-// exact two-pass per-image LN statistics of LeakyReLU(buf[p][c]) for p < HW, c < C
+// Per-image LN statistics of LeakyReLU(buf[p][c]) (p < HW, c < C) in one pass of shifted sums
+// (shift K = the first element, so sum (x-K)^2 does not cancel catastrophically), fp32 per
+// thread, fp64 across the block.
 __device__ __forceinline__ void ln_stats(const float* buf, int stride, int HW, int C, double* red, float& mu,
                                          float& rstd) {
     const int n = HW * C;
-    float s = 0.f;
-    for (int e = threadIdx.x; e < n; e += NT) {
-        const int p = e / C, c = e - p * C;
-        s += lrelu_(buf[p * stride + c]);
+    const float K = lrelu_(buf[0]);
+    float s1 = 0.f, s2 = 0.f;
+    if (((stride | C) & 3) == 0) {
+        const int C4 = C >> 2;
+        for (int e = threadIdx.x; e < (n >> 2); e += NT) {
+            const int p = e / C4, c = (e - p * C4) << 2;
+            const f4 v = *reinterpret_cast<const f4*>(buf + p * stride + c);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float d = lrelu_(v[j]) - K;
+                s1 += d;
+                s2 += d * d;
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += NT) {
+            const int p = e / C, c = e - p * C;
+            const float d = lrelu_(buf[p * stride + c]) - K;
+            s1 += d;
+            s2 += d * d;
+        }
     }
-    const double mean = block_sum((double)s, red) / n;
-    const float mf = (float)mean;
-    float q = 0.f;
-    for (int e = threadIdx.x; e < n; e += NT) {
-        const int p = e / C, c = e - p * C;
-        const float dl = lrelu_(buf[p * stride + c]) - mf;
-        q += dl * dl;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double d1 = wsum((double)s1), d2 = wsum((double)s2);
+    __syncthreads();
+    if (lane == 0) {
+        red[wave] = d1;
+        red[NW + wave] = d2;
     }
-    double m2 = block_sum((double)q, red);
-    const double dm = mean - (double)mf;
-    m2 -= (double)n * dm * dm;
-    if (m2 < 0.0) m2 = 0.0;
-    mu = mf;
-    rstd = (float)(1.0 / sqrt(m2 / n + (double)LN_EPS));
+    __syncthreads();
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        t1 += red[w];
+        t2 += red[NW + w];
+    }
+    const double m = t1 / n;                 // mean of (x - K)
+    double var = t2 / n - m * m;
+    if (var < 0.0) var = 0.0;
+    mu = (float)((double)K + m);
+    rstd = (float)(1.0 / sqrt(var + (double)LN_EPS));
 }
 
 // dst[p][c] = LN(LeakyReLU(src[p][c])) for channels [c0, c0+nc) of a C_ln-channel LN tensor;
 // gamma/beta are per (p, c) over C_ln channels (global, L2-resident). dst may alias src.
+// Full-width tensors take a float4 path with up to 8 gamma + 8 beta float4 loads in flight.
 __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* dst, int dstride, int HW, int c0,
                                          int nc, int C_ln, float mu, float rstd, const float* __restrict__ g,
                                          const float* __restrict__ b, bool ln) {
     const int n = HW * nc;
-    for (int base = 0; base < n; base += NT * 4) {
-        float xv[4], gv[4], bv[4];
-        int pp[4], cc[4];
+    if (((sstride | dstride | nc | c0 | C_ln) & 3) == 0) {
+        const int n4 = n >> 2, C4 = nc >> 2;
+        const bool full = (c0 == 0 && nc == C_ln);   // gamma/beta contiguous over the whole image
+        const f4* g4 = reinterpret_cast<const f4*>(g);
+        const f4* b4 = reinterpret_cast<const f4*>(b);
+        constexpr int UV = 8;
+        for (int base = 0; base < n4; base += NT * UV) {
+            f4 gv[UV], bv[UV];
+            if (ln) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < UV; u++) {
+                    const int i = base + u * NT + (int)threadIdx.x;
+                    const int p = i / C4, c = (i - p * C4) << 2;
+                    const int gi = full ? i : (p * C_ln + c0 + c) >> 2;
+                    gv[u] = i < n4 ? g4[gi] : f4{0.f, 0.f, 0.f, 0.f};
+                    bv[u] = i < n4 ? b4[gi] : f4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UV; u++) {
+                const int i = base + u * NT + (int)threadIdx.x;
+                if (i >= n4) continue;
+                const int p = i / C4, c = c0 + ((i - p * C4) << 2);
+                f4 x = *reinterpret_cast<const f4*>(src + p * sstride + c);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    float t = lrelu_(x[j]);
+                    if (ln) t = (t - mu) * rstd * gv[u][j] + bv[u][j];
+                    x[j] = t;
+                }
+                *reinterpret_cast<f4*>(dst + p * dstride + c) = x;
+            }
+        }
+        return;
+    }
+    constexpr int US = 8;
+    for (int base = 0; base < n; base += NT * US) {
+        float xv[US], gv[US], bv[US];
+        int pp[US], cc[US];
+#pragma unroll
+        for (int u = 0; u < US; u++) {
             const int e = base + u * NT + threadIdx.x;
             const int p = e / nc, c = e - p * nc;
             pp[u] = p;
@@ -93,7 +155,7 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < US; u++) {
             const int e = base + u * NT + threadIdx.x;
             if (e >= n) continue;
             float x = lrelu_(xv[u]);
@@ -103,23 +165,52 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
     }
 }
 
-// Stage B[k][n] = wt[k*cout + n] (k < K, n < cout; zero padded to Kpad x NS) into LDS.
-__device__ __forceinline__ void stage_w(const float* __restrict__ wt, int K, int cout, int Kpad, int NS, float* wl) {
-    const int total = Kpad * NS;
-    for (int base = 0; base < total; base += NT * 4) {
-        float v[4];
+// Copy a pre-packed weight image (n floats, n % 4 == 0) global -> LDS, 4 float4 in flight per thread.
+__device__ __forceinline__ void stage_w(const float* __restrict__ src, int n, float* dst) {
+    const int n4 = n >> 2;
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+    f4* d4 = reinterpret_cast<f4*>(dst);
+    for (int base = 0; base < n4; base += NT * 4) {
+        f4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int idx = base + u * NT + threadIdx.x;
-            const int k = idx / NS, n = idx - k * NS;
-            v[u] = (idx < total && k < K && n < cout) ? wt[(size_t)k * cout + n] : 0.f;
+            const int i = base + u * NT + (int)threadIdx.x;
+            v[u] = i < n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const int idx = base + u * NT + threadIdx.x;
-            if (idx < total) wl[idx] = v[u];
+            const int i = base + u * NT + (int)threadIdx.x;
+            if (i < n4) d4[i] = v[u];
         }
     }
+}
+
+// Register prefetch of the next conv's pre-packed weight image: loaded before the current conv's
+// MFMA loop, written to LDS after the barrier that retires the current conv.
+constexpr int WPF = 4;   // float4 per thread -> up to WPF*NT*4 floats
+struct WPre {
+    f4 v[WPF];
+    int n4;
+};
+__device__ __forceinline__ void wpf_load(WPre& w, const float* __restrict__ src, int n) {
+    w.n4 = n >> 2;
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+#pragma unroll
+    for (int u = 0; u < WPF; u++) {
+        const int i = u * NT + (int)threadIdx.x;
+        w.v[u] = i < w.n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+__device__ __forceinline__ void wpf_store(const WPre& w, float* dst, const float* __restrict__ src) {
+    f4* d4 = reinterpret_cast<f4*>(dst);
+#pragma unroll
+    for (int u = 0; u < WPF; u++) {
+        const int i = u * NT + (int)threadIdx.x;
+        if (i < w.n4) d4[i] = w.v[u];
+    }
+    // images larger than the prefetch window are finished directly
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+    for (int i = WPF * NT + (int)threadIdx.x; i < w.n4; i += NT) d4[i] = s4[i];
 }
 
 __device__ __forceinline__ int ns_of(int cout) {
@@ -153,6 +244,7 @@ __device__ __forceinline__ void conv_lds(const float* in, int istride, int ic0, 
         f4 acc[NR];
 #pragma unroll
         for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
         for (int k0 = 0; k0 < Kpad; k0 += 4) {
             const int k = k0 + kq;
             float av;
@@ -203,6 +295,188 @@ __device__ __forceinline__ void conv_lds_any(const float* in, int istride, int i
         conv_lds<KS, 4>(in, istride, ic0, cin, d, H, W, wl, Kpad, NS, ktab, out, ostride, oc0, cout, bias, residual);
 }
 
+// 1x1 conv from an LDS buffer with pixel stride S == 8 (mod 16) (conflict-free ds_read_b128 of
+// 4 channels per lane) against the pre-packed PK_1X1 image wl ([g][q][j][s]); K permuted so lane
+// (i, q) holds channels 16g + 4q + s at k-step s. out[p][oc0 + n] = bias + (+= if residual) A.B
+template <int NR>
+__device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl,
+                                          float* out, int ostride, int cout, const float* __restrict__ bias,
+                                          bool residual) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int nsub = (HW + 15) >> 4;
+    const int G = (cin + 15) >> 4;
+    constexpr int NSJ = 16 * NR;
+    float bz[NR];
+#pragma unroll
+    for (int n = 0; n < NR; n++) {
+        const int ch = n * 16 + i16;
+        bz[n] = ch < cout ? bias[ch] : 0.f;
+    }
+    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+        // two subtiles per pass (s0, s0 + NW) share the B reads
+        const int s1 = s0 + NW;
+        const bool v1 = s1 < nsub;
+        const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
+        const bool pva = pa < HW, pvb = v1 && pb < HW;
+        f4 acc0[NR], acc1[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) {
+            acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
+            acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+        for (int g = 0; g < G; g++) {
+            const int c0 = 16 * g + 4 * kq;
+            const bool cv = c0 < cin;
+            f4 a0 = (pva && cv) ? *reinterpret_cast<const f4*>(in + pa * istride + c0) : f4{0.f, 0.f, 0.f, 0.f};
+            f4 a1 = (pvb && cv) ? *reinterpret_cast<const f4*>(in + pb * istride + c0) : f4{0.f, 0.f, 0.f, 0.f};
+            if (c0 + 4 > cin) {   // ragged channel tail (cin % 4 != 0)
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (c0 + j >= cin) {
+                        a0[j] = 0.f;
+                        a1[j] = 0.f;
+                    }
+            }
+            const float* brow = wl + ((g * 4 + kq) * NSJ + i16) * 4;
+            f4 bq[NR];
+#pragma unroll
+            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+#pragma unroll
+            for (int st = 0; st < 4; st++)
+#pragma unroll
+                for (int n = 0; n < NR; n++) {
+                    acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], bq[n][st], acc0[n], 0, 0, 0);
+                    acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], bq[n][st], acc1[n], 0, 0, 0);
+                }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int sb = h ? s1 : s0;
+            if (h && !v1) break;
+#pragma unroll
+            for (int n = 0; n < NR; n++) {
+                const int ch = n * 16 + i16;
+                if (ch >= cout) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int q = sb * 16 + kq * 4 + r;
+                    if (q >= HW) continue;
+                    float v = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
+                    float* o = out + q * ostride + ch;
+                    if (residual) v += *o;
+                    *o = v;
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void conv1_lds_any(const float* in, int istride, int cin, int HW, const float* wl,
+                                              float* out, int ostride, int cout, const float* bias, bool residual) {
+    const int nr = (cout + 15) / 16;
+    if (nr == 1)
+        conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
+    else if (nr == 2)
+        conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
+    else if (nr == 3)
+        conv1_lds<3>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
+    else
+        conv1_lds<4>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
+}
+
+// 3x3 dilation-d conv from an LDS buffer (pixel stride == 8 mod 16, cin % 4 == 0) against the
+// PK_T9 image ([tap][g][q][j][s]): per tap and 16-channel group each lane reads the channel
+// quad 16g+4q.. of its shifted pixel with one ds_read_b128 (zero outside the image); no tap
+// table, 4*NR MFMAs per read. Two subtiles per pass share the B reads.
+template <int NR>
+__device__ __forceinline__ void conv3_t9_lds(const float* in, int istride, int ic0, int cin, int d, int H, int W,
+                                             const float* wl, float* out, int ostride, int oc0, int cout,
+                                             const float* __restrict__ bias) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int HW = H * W;
+    const int nsub = (HW + 15) >> 4;
+    const int G = (cin + 15) >> 4;
+    constexpr int NSJ = 16 * NR;
+    float bz[NR];
+#pragma unroll
+    for (int n = 0; n < NR; n++) {
+        const int ch = n * 16 + i16;
+        bz[n] = ch < cout ? bias[ch] : 0.f;
+    }
+    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+        const int s1 = s0 + NW;
+        const bool v1 = s1 < nsub;
+        const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
+        const bool pva = pa < HW, pvb = v1 && pb < HW;
+        const int ra = pva ? pa / W : 0, ca = pva ? pa - ra * W : 0;
+        const int rb = pvb ? pb / W : 0, cb = pvb ? pb - rb * W : 0;
+        f4 acc0[NR], acc1[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) {
+            acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
+            acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll 1
+        for (int tap = 0; tap < 9; tap++) {
+            const int dr = (tap / 3 - 1) * d, dc = (tap % 3 - 1) * d;
+            const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
+            const bool oka = pva && ya >= 0 && ya < H && xa >= 0 && xa < W;
+            const bool okb = pvb && yb >= 0 && yb < H && xb >= 0 && xb < W;
+            const float* pa_ = in + (oka ? (ya * W + xa) : 0) * istride + ic0;
+            const float* pb_ = in + (okb ? (yb * W + xb) : 0) * istride + ic0;
+            for (int g = 0; g < G; g++) {
+                const int c0 = 16 * g + 4 * kq;
+                const bool cv = c0 < cin;
+                f4 a0 = (oka && cv) ? *reinterpret_cast<const f4*>(pa_ + c0) : f4{0.f, 0.f, 0.f, 0.f};
+                f4 a1 = (okb && cv) ? *reinterpret_cast<const f4*>(pb_ + c0) : f4{0.f, 0.f, 0.f, 0.f};
+                const float* brow = wl + (((tap * G + g) * 4 + kq) * NSJ + i16) * 4;
+                f4 bq[NR];
+#pragma unroll
+                for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+#pragma unroll
+                for (int st = 0; st < 4; st++)
+#pragma unroll
+                    for (int n = 0; n < NR; n++) {
+                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], bq[n][st], acc0[n], 0, 0, 0);
+                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], bq[n][st], acc1[n], 0, 0, 0);
+                    }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int sb = h ? s1 : s0;
+            if (h && !v1) break;
+#pragma unroll
+            for (int n = 0; n < NR; n++) {
+                const int ch = n * 16 + i16;
+                if (ch >= cout) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int q = sb * 16 + kq * 4 + r;
+                    if (q >= HW) continue;
+                    out[q * ostride + oc0 + ch] = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void conv3_t9_any(const float* in, int istride, int ic0, int cin, int d, int H, int W,
+                                             const float* wl, float* out, int ostride, int oc0, int cout,
+                                             const float* bias) {
+    const int nr = (cout + 15) / 16;
+    if (nr == 1)
+        conv3_t9_lds<1>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
+    else if (nr == 2)
+        conv3_t9_lds<2>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
+    else if (nr == 3)
+        conv3_t9_lds<3>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
+    else
+        conv3_t9_lds<4>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
+}
+
 // k -> (dr, dc, c) table of a 3x3 dilation-d conv over cin channels, -1 beyond K
 __device__ __forceinline__ void build_ktab(int* ktab, int cin, int d, int Kpad) {
     for (int k = threadIdx.x; k < Kpad; k += NT) {
@@ -218,6 +492,17 @@ __device__ __forceinline__ void build_ktab(int* ktab, int cin, int d, int Kpad) 
 
 }  // namespace
 
+// Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs).
+__device__ long long g_stamps[256];
+#define STAMP(i)                                                                            \
+    do {                                                                                     \
+        if (STAMPS) {                                                                        \
+            __syncthreads();                                                                 \
+            if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0)                      \
+                g_stamps[(i)] = (long long)__builtin_amdgcn_s_memrealtime();                \
+        }                                                                                    \
+    } while (0)
+
 __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int D) {
     const int pr = p / wc, pc = p - pr * wc;
     if (m < 2) {
@@ -231,6 +516,7 @@ __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int
     return (pr * W + pc) * D + ch;
 }
 
+template <bool STAMPS>
 __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int img = blockIdx.x, net = blockIdx.y;
@@ -242,94 +528,189 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     float* T2 = reinterpret_cast<float*>(smem + a.off_t2);
     float* WL = reinterpret_cast<float*>(smem + a.off_w);
     int* KT = reinterpret_cast<int*>(smem + a.off_k);
-    double* red = reinterpret_cast<double*>(smem);
+    double* red = reinterpret_cast<double*>(smem);   // 2*NW doubles
     const float* P = a.params;
+    const float* X = a.aux;
     const int* off = a.offs + net * a.offs_per_net;   // see NetLdsArgs
     const bool ln = a.ln != 0;
     float mu = 0.f, rstd = 1.f;
 
-    // gather u1c (mask compress, :720-759) straight from u into T2 (stride S2)
+    // packed-image sizes of every conv of this net (floats)
+    const int r16 = ((nk + 15) / 16) * 16;                 // G*16 for cin = nk
+    const int sz_ci = a.ci_t9 ? 9 * ((a.dc1 + 15) / 16) * 16 * r16 : ((9 * a.dc1 + 3) / 4 * 4) * ns_of(nk);
+    const int sz_ca = r16 * r16;                           // PK_1X1 nk -> nk
+    const int sz_cb = ((gc + 15) / 16) * 16 * r16;         // PK_1X1 gc -> nk
+    const int co_nr = (9 * a.dc2 + 15) / 16;
+    const int sz_co = a.co_tap ? r16 * 16 * co_nr
+                      : a.co_t9 ? 9 * r16 * ((a.dc2 + 15) / 16) * 16 : ((9 * nk + 3) / 4 * 4) * ns_of(a.dc2);
+    auto sz_gc = [&](int bi) {
+        return a.br_t9[bi] ? 9 * ((a.br_cin[bi] + 15) / 16) * 16 * ((a.br_cout[bi] + 15) / 16) * 16
+                           : ((9 * a.br_cin[bi] + 3) / 4 * 4) * ns_of(a.br_cout[bi]);
+    };
+    const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
+    const int per_rb = 10 + 2 * a.nbr;
+    auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
+    const int* oend = off + RB0 + a.R * per_rb;
+    WPre pf;
+
+    int sti = 0;
+    STAMP(sti++);
+    // gather u1c (mask compress, :720-759) straight from u into the T2 region (stride SU)
+    wpf_load(pf, X + off[0], sz_ci);
+    const int SU = a.su;
     {
         const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
         const int n = HW * a.dc1;
         for (int e = threadIdx.x; e < n; e += NT) {
             const int p = e / a.dc1, c = e - p * a.dc1;
-            T2[p * S2 + c] = ub[mask_pos_(a.mask, p, c, W, a.W, a.D)];
+            T2[p * SU + c] = ub[mask_pos_(a.mask, p, c, W, a.W, a.D)];
         }
     }
-    // conv_in (3x3, dc1 -> nk)
+    // conv_in (3x3, dc1 -> nk), PK_KN
     {
-        const int K = 9 * a.dc1, Kpad = (K + 3) / 4 * 4, NS = ns_of(nk);
-        stage_w(P + off[0], K, nk, Kpad, NS, WL);
-        build_ktab(KT, a.dc1, 1, Kpad);
+        const int Kpad = (9 * a.dc1 + 3) / 4 * 4, NS = ns_of(nk);
+        if (!a.ci_t9) build_ktab(KT, a.dc1, 1, Kpad);
+        wpf_store(pf, WL, X + off[0]);
         __syncthreads();
-        conv_lds_any<3>(T2, S2, 0, a.dc1, 1, H, W, WL, Kpad, NS, KT, Y, SY, 0, nk, P + off[1], false);
+        if (a.R > 0)
+            wpf_load(pf, X + rbo(0)[2], sz_ca);
+        else
+            wpf_load(pf, X + oend[2], sz_co);
+        STAMP(sti++);
+        if (a.ci_t9)
+            conv3_t9_any(T2, SU, 0, a.dc1, 1, H, W, WL, Y, SY, 0, nk, X + off[1]);
+        else
+            conv_lds_any<3>(T2, SU, 0, a.dc1, 1, H, W, WL, Kpad, NS, KT, Y, SY, 0, nk, X + off[1], false);
         __syncthreads();
+        STAMP(sti++);
     }
-    const int RB0 = 2;   // offs: [conv_in_k, conv_in_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, conv_out_k, conv_out_b]
-    const int per_rb = 10 + 2 * a.nbr;
     for (int r = 0; r < a.R; r++) {
-        const int* o = off + RB0 + r * per_rb;
+        const int* o = rbo(r);
         // LN1(LReLU(y)) -> T2 (scratch), conv_a (1x1 nk->nk) -> T1
         if (ln) ln_stats(Y, SY, HW, nk, red, mu, rstd);
+        STAMP(sti++);
         ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
-        {
-            const int Kpad = (nk + 3) / 4 * 4, NS = ns_of(nk);
-            stage_w(P + o[2], nk, nk, Kpad, NS, WL);
-            __syncthreads();
-            conv_lds_any<1>(T2, S2, 0, nk, 1, H, W, WL, Kpad, NS, KT, T1, S1, 0, nk, P + o[3], false);
-            __syncthreads();
-        }
+        STAMP(sti++);
+        wpf_store(pf, WL, X + o[2]);
+        __syncthreads();
+        wpf_load(pf, X + o[10], sz_gc(0));
+        STAMP(sti++);
+        conv1_lds_any(T2, S2, nk, HW, WL, T1, S1, nk, X + o[3], false);
+        __syncthreads();
+        STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
         if (ln) ln_stats(T1, S1, HW, nk, red, mu, rstd);
         for (int wi = 0; wi < a.nwin; wi++)
             ln_apply(T1, S1, T1, S1, HW, a.win_off[wi], a.win_len[wi], nk, mu, rstd, ln ? P + o[4] : nullptr,
                      ln ? P + o[5] : nullptr, ln);
-        __syncthreads();
         // grouped dilated branches -> T2[:, out_off : out_off + cout]
         for (int bi = 0; bi < a.nbr; bi++) {
             const int cin = a.br_cin[bi], cout = a.br_cout[bi], d = a.br_dil[bi];
-            const int K = 9 * cin, Kpad = (K + 3) / 4 * 4, NS = ns_of(cout);
-            stage_w(a.aux + o[10 + 2 * bi], K, cout, Kpad, NS, WL);
-            build_ktab(KT, cin, d, Kpad);
+            const int Kpad = (9 * cin + 3) / 4 * 4, NS = ns_of(cout);
             __syncthreads();
-            conv_lds_any<3>(T1, S1, a.br_cin_off[bi], cin, d, H, W, WL, Kpad, NS, KT, T2, S2, a.br_out_off[bi], cout,
-                            a.aux + o[11 + 2 * bi], false);
+            if (!a.br_t9[bi]) build_ktab(KT, cin, d, Kpad);
+            wpf_store(pf, WL, X + o[10 + 2 * bi]);
             __syncthreads();
+            if (bi + 1 < a.nbr)
+                wpf_load(pf, X + o[10 + 2 * (bi + 1)], sz_gc(bi + 1));
+            else
+                wpf_load(pf, X + o[8], sz_cb);
+            STAMP(sti++);
+            if (a.br_t9[bi])
+                conv3_t9_any(T1, S1, a.br_cin_off[bi], cin, d, H, W, WL, T2, S2, a.br_out_off[bi], cout,
+                             X + o[11 + 2 * bi]);
+            else
+                conv_lds_any<3>(T1, S1, a.br_cin_off[bi], cin, d, H, W, WL, Kpad, NS, KT, T2, S2, a.br_out_off[bi],
+                                cout, X + o[11 + 2 * bi], false);
+            STAMP(sti++);
         }
+        __syncthreads();
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y
         if (ln) ln_stats(T2, S2, HW, gc, red, mu, rstd);
+        STAMP(sti++);
         ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
-        {
-            const int Kpad = (gc + 3) / 4 * 4, NS = ns_of(nk);
-            stage_w(P + o[8], gc, nk, Kpad, NS, WL);
-            __syncthreads();
-            conv_lds_any<1>(T2, S2, 0, gc, 1, H, W, WL, Kpad, NS, KT, Y, SY, 0, nk, P + o[9], true);
-            __syncthreads();
-        }
+        STAMP(sti++);
+        wpf_store(pf, WL, X + o[8]);
+        __syncthreads();
+        if (r + 1 < a.R)
+            wpf_load(pf, X + rbo(r + 1)[2], sz_ca);
+        else
+            wpf_load(pf, X + oend[2], sz_co);
+        STAMP(sti++);
+        conv1_lds_any(T2, S2, gc, HW, WL, Y, SY, nk, X + o[9], true);
+        __syncthreads();
+        STAMP(sti++);
     }
-    // LN_out(LReLU(y)) in place, conv_out (3x3 nk -> dc2) -> T2 -> global
+    // LN_out(LReLU(y)) in place, conv_out (3x3 nk -> dc2) -> global
     {
-        const int* o = off + RB0 + a.R * per_rb;
+        const int* o = oend;
         if (ln) ln_stats(Y, SY, HW, nk, red, mu, rstd);
         ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
-        const int K = 9 * nk, Kpad = (K + 3) / 4 * 4, NS = ns_of(a.dc2);
-        stage_w(P + o[2], K, a.dc2, Kpad, NS, WL);
-        build_ktab(KT, nk, 1, Kpad);
-        __syncthreads();
-        conv_lds_any<3>(Y, SY, 0, nk, 1, H, W, WL, Kpad, NS, KT, T2, S2, 0, a.dc2, P + o[3], false);
-        __syncthreads();
+        STAMP(sti++);
         float* dst = a.so[net] + (size_t)img * HW * a.dc2;
-        const int n = HW * a.dc2;
-        for (int e = threadIdx.x; e < n; e += NT) {
-            const int p = e / a.dc2, c = e - p * a.dc2;
-            dst[e] = T2[p * S2 + c];
+        const float* __restrict__ bias = X + o[3];
+        if (a.co_tap) {
+            // tap-decomposed: C[p][(tap, o)] = sum_c y[p][c] W[tap][c][o] (1x1 GEMM, scratch over T1..T2),
+            // out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]
+            const int ncol = 9 * a.dc2;
+            const int CS = 16 * co_nr + 1;
+            float* C = T1;
+            wpf_store(pf, WL, X + o[2]);
+            __syncthreads();
+            conv1_lds_any(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false);
+            __syncthreads();
+            const int n = HW * a.dc2;
+            for (int e = threadIdx.x; e < n; e += NT) {
+                const int p = e / a.dc2, oc = e - p * a.dc2;
+                const int pr = p / W, pc = p - pr * W;
+                float acc = bias[oc];
+#pragma unroll
+                for (int kh = 0; kh < 3; kh++) {
+                    const int sr = pr + kh - 1;
+                    if (sr < 0 || sr >= H) continue;
+#pragma unroll
+                    for (int kw = 0; kw < 3; kw++) {
+                        const int sc = pc + kw - 1;
+                        if (sc < 0 || sc >= W) continue;
+                        acc += C[(sr * W + sc) * CS + (kh * 3 + kw) * a.dc2 + oc];
+                    }
+                }
+                dst[e] = acc;
+            }
+        } else {
+            const int Kpad = (9 * nk + 3) / 4 * 4, NS = ns_of(a.dc2);
+            if (!a.co_t9) build_ktab(KT, nk, 1, Kpad);
+            wpf_store(pf, WL, X + o[2]);
+            __syncthreads();
+            if (a.co_t9)
+                conv3_t9_any(Y, SY, 0, nk, 1, H, W, WL, T2, S2, 0, a.dc2, bias);
+            else
+                conv_lds_any<3>(Y, SY, 0, nk, 1, H, W, WL, Kpad, NS, KT, T2, S2, 0, a.dc2, bias, false);
+            __syncthreads();
+            const int n = HW * a.dc2;
+            for (int e = threadIdx.x; e < n; e += NT) {
+                const int p = e / a.dc2, c = e - p * a.dc2;
+                dst[e] = T2[p * S2 + c];
+            }
         }
     }
+    STAMP(sti++);
+    if (STAMPS && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_stamps[255] = sti;
 }
 
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
-    hipLaunchKernelGGL(k_net_lds, dim3(B, 2), dim3(NT), lds, st, a);
+    static const bool stamps = [] {
+        const char* e = std::getenv("CNF_STAMPS");
+        return e && std::atoi(e) != 0;
+    }();
+    if (stamps)
+        hipLaunchKernelGGL(k_net_lds<true>, dim3(B, 2), dim3(NT), lds, st, a);
+    else
+        hipLaunchKernelGGL(k_net_lds<false>, dim3(B, 2), dim3(NT), lds, st, a);
+}
+
+int read_stamps(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(long long) * (n > 256 ? 256 : n)) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace cnf

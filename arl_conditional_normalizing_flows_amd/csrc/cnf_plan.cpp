@@ -3,6 +3,8 @@
 #include "cnf_plan.h"
 
 #include <cmath>
+#include <cstdlib>
+#include <functional>
 #include <stdexcept>
 
 namespace cnf {
@@ -49,6 +51,78 @@ std::vector<int> s2d(const std::vector<int>& in, int h, int w, int c) {
     return out;
 }
 
+
+// floats of a packed conv image and its K extent (see PackedConv); must match the pack lambda
+void packed_dims(int fmt, int ks, int cin, int cout, int64_t& size, int& kpad) {
+    if (fmt == PK_T9) {
+        const int G = (cin + 15) / 16;
+        kpad = 9 * G * 16;
+        size = 9LL * G * 16 * 16 * ((cout + 15) / 16);
+    } else if (fmt == PK_KN) {
+        int ns = 16 * ((cout + 15) / 16);
+        if (ns % 32 == 0) ns += 16;
+        kpad = (ks * ks * cin + 3) / 4 * 4;
+        size = (int64_t)kpad * ns;
+    } else {
+        const int ncol = (fmt == PK_TAP) ? 9 * cout : cout;
+        kpad = (cin + 15) / 16 * 16;
+        size = (int64_t)kpad * 16 * ((ncol + 15) / 16);
+    }
+}
+
+int align16(int64_t v) { return (int)((v + 15) / 16 * 16); }
+int stride8(int ch) {   // == 8 (mod 16) floats: conflict-free ds_read_b128 of channel quads
+    int v = std::max(ch, 8);
+    while (v % 16 != 8) v++;
+    return v;
+}
+int stride2(int ch) {   // == 2 (mod 4) floats: conflict-free b32 reads of the tap-table path
+    int v = std::max(ch, 2);
+    while (v % 4 != 2) v++;
+    return v;
+}
+
+// LDS image of k_net_lds for coupling c under the given conv formats; false if over 160 KiB.
+bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vector<int>& gc_fmt, NetLdsGeom& g) {
+    if (c.nk > 64 || c.dc2 > 64 || c.br.size() > 8) return false;
+    for (const Branch& b : c.br)
+        if (b.dil > 16) return false;
+    const int64_t HW = (int64_t)c.hc * c.wc;
+    g.sy = stride8(c.nk);
+    g.s1 = stride8(c.nk);
+    g.s2 = stride8(std::max(std::max(c.gc, c.nk), c.dc2));
+    g.su = ci_fmt == PK_T9 ? stride8(c.dc1) : stride2(c.dc1);
+    g.s2r = std::max(g.s2, g.su);
+    if (co_fmt == PK_TAP)   // tap-decomposed conv_out scratch (stride 16*nr+1) spans T1..T2
+        g.s2r = std::max(g.s2r, 16 * ((9 * c.dc2 + 15) / 16) + 1 - g.s1);
+    int64_t wmax = 0, sz;
+    int kmax = 4, kp;
+    auto acc = [&](int fmt, int ks, int cin, int cout) {
+        packed_dims(fmt, ks, cin, cout, sz, kp);
+        wmax = std::max(wmax, sz);
+        if (fmt == PK_KN) kmax = std::max(kmax, kp);
+    };
+    acc(ci_fmt, 3, c.dc1, c.nk);
+    acc(co_fmt, 3, c.nk, c.dc2);
+    if (c.R > 0) {
+        acc(PK_1X1, 1, c.nk, c.nk);
+        acc(PK_1X1, 1, c.gc, c.nk);
+        for (size_t bi = 0; bi < c.br.size(); bi++) acc(gc_fmt[bi], 3, c.br[bi].cin, c.br[bi].cout);
+    }
+    int64_t off = 128;   // block reduction scratch (2 x 8 doubles)
+    g.off_y = (int)off;
+    off = align16(off + HW * g.sy * 4);
+    g.off_t1 = (int)off;
+    off = align16(off + HW * g.s1 * 4);   // T1 and T2 contiguous (tap scratch)
+    g.off_t2 = (int)off;
+    off = align16(off + HW * g.s2r * 4);
+    g.off_w = (int)off;
+    off = align16(off + wmax * 4);
+    g.off_k = (int)off;
+    off = align16(off + (int64_t)kmax * 4);
+    g.bytes = (int)std::min<int64_t>(off, 1 << 30);
+    return off <= 160 * 1024;
+}
 }  // namespace
 
 Plan* build_plan(const cnf_flow_desc* d) {
@@ -261,55 +335,154 @@ Plan* build_plan(const cnf_flow_desc* d) {
             }
         }
 
-        // aux image: dense [9*cin][cout] weights + [cout] bias per grouped branch
-        for (auto& c : p.couplings) {
-            for (int net = 0; net < 2; net++) {
-                for (auto& rb : c.net[net].rb) {
-                    for (size_t bi = 0; bi < c.br.size(); bi++) {
-                        const Branch& b = c.br[bi];
-                        const int K = ks * ks * b.cin;
-                        int64_t wo = p.n_aux;
-                        p.aux_map.resize(p.aux_map.size() + (size_t)K * b.cout, -1);
-                        for (size_t j = 0; j < b.in_offsets.size(); j++) {
-                            const int64_t gk = rb.gk[bi][j];
-                            const int in_rel = b.in_offsets[j] - b.cin_off;  // 0 in reference mode
-                            for (int tap = 0; tap < ks * ks; tap++)
-                                for (int ci2 = 0; ci2 < b.width; ci2++)
-                                    for (int o = 0; o < b.width; o++) {
-                                        int64_t dst = wo + (int64_t)(tap * b.cin + in_rel + ci2) * b.cout +
-                                                      (int64_t)j * b.width + o;
-                                        p.aux_map[dst] = gk + ((int64_t)tap * b.width + ci2) * b.width + o;
-                                    }
-                        }
-                        p.n_aux += (int64_t)K * b.cout;
-                        rb.aux_w.push_back(wo);
-                        int64_t bo = p.n_aux;
-                        for (size_t j = 0; j < b.in_offsets.size(); j++)
-                            for (int o = 0; o < b.width; o++) p.aux_map.push_back(rb.gb[bi][j] + o);
-                        p.n_aux += b.cout;
-                        rb.aux_b.push_back(bo);
-                    }
+        // conv formats and which layers run the whole-net-in-LDS kernel (CNF_NETLDS=0 disables):
+        // prefer PK_T9 for its 3x3 convs (channel-quad reads, no tap table), fall back to PK_KN
+        // when the T9 images do not fit the 160 KiB LDS image, else stream the layer.
+        {
+            bool allow = true;
+            if (const char* e = std::getenv("CNF_NETLDS")) allow = std::atoi(e) != 0;
+            for (auto& c : p.couplings) {
+                const int tapco = 9 * c.dc2 <= 64 ? PK_TAP : PK_KN;
+                c.ci_fmt = PK_KN;
+                c.co_fmt = tapco;
+                c.gc_fmt.assign(c.br.size(), PK_KN);
+                c.use_lds = false;
+                if (!allow) continue;
+                const int ci9 = c.dc1 % 4 == 0 ? PK_T9 : PK_KN;
+                const int co9 = tapco == PK_TAP ? PK_TAP : (c.nk % 4 == 0 ? PK_T9 : PK_KN);
+                std::vector<int> gc9;
+                for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_T9 : PK_KN);
+                NetLdsGeom g;
+                if (netlds_geometry(c, ci9, co9, gc9, g)) {
+                    c.ci_fmt = ci9;
+                    c.co_fmt = co9;
+                    c.gc_fmt = gc9;
+                    c.use_lds = true;
+                } else if (netlds_geometry(c, PK_KN, tapco, c.gc_fmt, g)) {
+                    c.use_lds = true;
                 }
+                if (c.use_lds) c.lds = g;
             }
         }
 
-        // k_net_lds offset tables
+        // kernel image (aux): every conv's weights + bias packed in its kernel's LDS layout
+        auto pack = [&](PackedConv& pc, int fmt, int cin, int cout, const std::function<int64_t(int, int)>& src,
+                        const std::function<int64_t(int)>& bsrc) {
+            pc.fmt = fmt;
+            pc.cin = cin;
+            pc.cout = cout;
+            pc.w = p.n_aux;
+            if (fmt == PK_T9) {
+                pc.nr = (cout + 15) / 16;
+                pc.ns = 16 * pc.nr;
+                pc.G = (cin + 15) / 16;
+                pc.kpad = 9 * pc.G * 16;
+                pc.size = 9LL * pc.G * 16 * pc.ns;
+                for (int tap = 0; tap < 9; tap++)
+                    for (int g = 0; g < pc.G; g++)
+                        for (int q = 0; q < 4; q++)
+                            for (int j = 0; j < pc.ns; j++)
+                                for (int s4 = 0; s4 < 4; s4++) {
+                                    const int c2 = 16 * g + 4 * q + s4;
+                                    p.aux_map.push_back((c2 < cin && j < cout) ? src(tap * cin + c2, j) : -1);
+                                }
+            } else if (fmt == PK_KN) {
+                const int K = ks * ks * cin;
+                pc.nr = (cout + 15) / 16;
+                pc.ns = 16 * pc.nr;
+                if (pc.ns % 32 == 0) pc.ns += 16;
+                pc.kpad = (K + 3) / 4 * 4;
+                pc.size = (int64_t)pc.kpad * pc.ns;
+                for (int k = 0; k < pc.kpad; k++)
+                    for (int n = 0; n < pc.ns; n++) p.aux_map.push_back((k < K && n < cout) ? src(k, n) : -1);
+            } else {
+                const int ncol = (fmt == PK_TAP) ? 9 * cout : cout;
+                pc.nr = (ncol + 15) / 16;
+                pc.ns = 16 * pc.nr;
+                pc.G = (cin + 15) / 16;
+                pc.kpad = pc.G * 16;
+                pc.size = (int64_t)pc.G * 16 * pc.ns;
+                for (int g = 0; g < pc.G; g++)
+                    for (int q = 0; q < 4; q++)
+                        for (int j = 0; j < pc.ns; j++)
+                            for (int s4 = 0; s4 < 4; s4++) {
+                                const int c = 16 * g + 4 * q + s4;
+                                p.aux_map.push_back((c < cin && j < ncol) ? src(c, j) : -1);
+                            }
+            }
+            p.n_aux += pc.size;
+            pc.b = p.n_aux;
+            const int bpad = (cout + 3) / 4 * 4;
+            for (int n = 0; n < bpad; n++) p.aux_map.push_back(n < cout ? bsrc(n) : -1);
+            p.n_aux += bpad;
+        };
+        for (auto& c : p.couplings) {
+            for (int net = 0; net < 2; net++) {
+                NetParams& np = c.net[net];
+                const int64_t cik = np.conv_in_k, cib = np.conv_in_b;
+                const int nk = c.nk;
+                pack(np.ci, c.ci_fmt, c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
+                     [=](int n) { return cib + n; });
+                for (auto& rb : np.rb) {
+                    const int64_t ak = rb.conv_a_k, ab = rb.conv_a_b, bk = rb.conv_b_k, bb = rb.conv_b_b;
+                    pack(rb.ca, PK_1X1, nk, nk, [=](int ci2, int j) { return ak + (int64_t)ci2 * nk + j; },
+                         [=](int n) { return ab + n; });
+                    for (size_t bi = 0; bi < c.br.size(); bi++) {
+                        const Branch b = c.br[bi];
+                        const std::vector<int64_t> gk = rb.gk[bi], gb = rb.gb[bi];
+                        PackedConv pc;
+                        // dense [9*cin][cout] view of the card per-group Conv2D kernels (:401-411)
+                        pack(pc, c.gc_fmt[bi], b.cin, b.cout,
+                             [=](int k, int n) -> int64_t {
+                                 const int tap = k / b.cin, ci2 = k - tap * b.cin;
+                                 const int j = n / b.width, o = n - j * b.width;
+                                 const int in_rel = b.in_offsets[j] - b.cin_off;
+                                 const int cj = ci2 - in_rel;
+                                 if (cj < 0 || cj >= b.width) return -1;
+                                 return gk[j] + ((int64_t)tap * b.width + cj) * b.width + o;
+                             },
+                             [=](int n) { return gb[n / b.width] + (n % b.width); });
+                        rb.gc.push_back(pc);
+                    }
+                    pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
+                         [=](int n) { return bb + n; });
+                }
+                const int64_t ok = np.conv_out_k, ob = np.conv_out_b;
+                const int dc2 = c.dc2;
+                if (c.co_fmt == PK_TAP)
+                    pack(np.co, PK_TAP, nk, dc2,
+                         [=](int ci2, int j) {
+                             const int tap = j / dc2, o = j - tap * dc2;
+                             return ok + ((int64_t)tap * nk + ci2) * dc2 + o;
+                         },
+                         [=](int n) { return ob + n; });
+                else
+                    pack(np.co, c.co_fmt, nk, dc2,
+                         [=](int k, int n) { return ok + (int64_t)k * dc2 + n; },
+                         [=](int n) { return ob + n; });
+            }
+        }
+
+        p.aux_zero = p.n_aux;   // 64 zeros (bias of bias-free GEMM stages)
+        for (int i = 0; i < 64; i++) p.aux_map.push_back(-1);
+        p.n_aux += 64;
+
+        // k_net_lds offset table (params offsets for LN gamma/beta, kernel-image offsets for convs)
         require(p.n_params < (1ll << 31) && p.n_aux < (1ll << 31), "parameter image exceeds 2^31 floats");
         for (auto& c : p.couplings) {
             for (int net = 0; net < 2; net++) {
                 const NetParams& np = c.net[net];
-                std::vector<int> o = {(int)np.conv_in_k, (int)np.conv_in_b};
+                std::vector<int> o = {(int)np.ci.w, (int)np.ci.b};
                 for (const auto& rb : np.rb) {
-                    for (int64_t v : {rb.ln1g, rb.ln1b, rb.conv_a_k, rb.conv_a_b, rb.ln2g, rb.ln2b, rb.ln3g, rb.ln3b,
-                                      rb.conv_b_k, rb.conv_b_b})
+                    for (int64_t v : {rb.ln1g, rb.ln1b, rb.ca.w, rb.ca.b, rb.ln2g, rb.ln2b, rb.ln3g, rb.ln3b, rb.cb.w,
+                                      rb.cb.b})
                         o.push_back((int)std::max<int64_t>(v, 0));
-                    for (size_t bi = 0; bi < c.br.size(); bi++) {
-                        o.push_back((int)rb.aux_w[bi]);
-                        o.push_back((int)rb.aux_b[bi]);
+                    for (const auto& g : rb.gc) {
+                        o.push_back((int)g.w);
+                        o.push_back((int)g.b);
                     }
                 }
-                for (int64_t v : {np.ln_out_g, np.ln_out_b, np.conv_out_k, np.conv_out_b})
-                    o.push_back((int)std::max<int64_t>(v, 0));
+                for (int64_t v : {np.ln_out_g, np.ln_out_b, np.co.w, np.co.b}) o.push_back((int)std::max<int64_t>(v, 0));
                 c.lds_offs_per_net = (int)o.size();
                 c.lds_offs.insert(c.lds_offs.end(), o.begin(), o.end());
             }

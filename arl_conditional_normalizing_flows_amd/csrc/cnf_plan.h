@@ -21,17 +21,37 @@ struct Branch {
     int cin_off = 0, cin = 0, cout = 0;
 };
 
+// A convolution's weights + bias as packed into the device "kernel image" (the aux buffer) in the
+// exact LDS layout its kernel consumes, so staging is a plain float4 copy:
+//   PK_1X1  1x1 conv [cin][cout]: B image [g][q][j][s], element (c = 16g+4q+s, j), j < 16*nr
+//   PK_TAP  3x3 conv as tap GEMM: same image over c with columns j = tap*cout + o (9*cout <= 64)
+//   PK_KN   3x3 implicit GEMM: [kpad][ns], k = tap*cin + c, ns = 16*nr (+16 if ns % 32 == 0)
+//   PK_T9   3x3 with channel quads: [tap][g][q][j][s], element (tap, c = 16g+4q+s, j) (LDS kernel)
+enum { PK_1X1 = 0, PK_KN = 1, PK_TAP = 2, PK_T9 = 3 };
+struct PackedConv {
+    int fmt = PK_KN, cin = 0, cout = 0, nr = 0, ns = 0, G = 0, kpad = 0;
+    int64_t w = -1, b = -1, size = 0;   // offsets (floats) into the kernel image; size of the weight image
+};
+
 struct RBParams {
     int64_t ln1g = -1, ln1b = -1, conv_a_k = -1, conv_a_b = -1, ln2g = -1, ln2b = -1;
     std::vector<std::vector<int64_t>> gk, gb;  // [branch][group] canonical offsets
-    std::vector<int64_t> aux_w, aux_b;         // [branch] dense aux offsets
     int64_t ln3g = -1, ln3b = -1, conv_b_k = -1, conv_b_b = -1;
+    PackedConv ca, cb;                         // conv_a, conv_b (PK_1X1)
+    std::vector<PackedConv> gc;                // grouped branches as dense 3x3 convs (PK_KN)
 };
 
 struct NetParams {
     int64_t conv_in_k = -1, conv_in_b = -1;
     std::vector<RBParams> rb;
     int64_t ln_out_g = -1, ln_out_b = -1, conv_out_k = -1, conv_out_b = -1, tanh_w = -1;
+    PackedConv ci, co;                         // conv_in (PK_KN), conv_out (PK_TAP or PK_KN)
+};
+
+// LDS image of k_net_lds (cnf_netlds.hip): Y | T1 | T2 | W | K, byte offsets; pixel strides in floats
+struct NetLdsGeom {
+    int sy = 0, s1 = 0, s2 = 0, su = 0, s2r = 0;
+    int off_y = 0, off_t1 = 0, off_t2 = 0, off_w = 0, off_k = 0, bytes = 0;
 };
 
 struct Coupling {
@@ -47,6 +67,10 @@ struct Coupling {
     std::vector<int> lds_offs;
     int lds_offs_per_net = 0;
     int dev_lds_offs = -1;    // offset into the device table
+    bool use_lds = false;     // run the whole s,t net in one workgroup (k_net_lds)
+    int ci_fmt = PK_KN, co_fmt = PK_KN;   // packed formats of conv_in / conv_out
+    std::vector<int> gc_fmt;              // per grouped branch
+    NetLdsGeom lds;                       // valid when use_lds
 };
 
 struct Layer {
@@ -104,7 +128,8 @@ struct Plan {
     std::vector<ParamTensor> params;
     int64_t n_params = 0;
     int64_t n_aux = 0;
-    std::vector<int64_t> aux_map;   // aux[i] = params[aux_map[i]] (or 0 if < 0)
+    int64_t aux_zero = 0;           // offset of 64 zero floats in the kernel image
+    std::vector<int64_t> aux_map;   // kernel image: aux[i] = params[aux_map[i]] (or 0 if < 0)
     std::vector<Boundary> boundaries;
     std::vector<int> final_orig;    // last block layout -> xy position
     int last_n = 0;                 // elements per image of the last block layout
@@ -116,7 +141,6 @@ struct Plan {
     int device = -1;
     // launch recording
     bool record = true;
-    bool use_netlds = true;   // whole-net-in-LDS kernel for layers that fit (CNF_NETLDS=0 disables)
     std::vector<Recorded> recorded;
 
     WsLayout layout(int B) const;

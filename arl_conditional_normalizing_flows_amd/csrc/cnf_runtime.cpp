@@ -421,37 +421,21 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
         }
     }
     a.offs_per_net = c.lds_offs_per_net;
-    a.sy = lds_stride(c.nk);
-    a.s1 = lds_stride(c.nk);
-    a.s2 = lds_stride(std::max(std::max(c.gc, c.nk), std::max(c.dc1, c.dc2)));
-    auto ns_of = [](int cout) {
-        int ns = (cout + 15) / 16 * 16;
-        if (ns % 32 == 0) ns += 16;
-        return ns;
-    };
-    auto kp = [](int k) { return (k + 3) / 4 * 4; };
-    size_t wmax = (size_t)kp(9 * c.dc1) * ns_of(c.nk);
-    wmax = std::max(wmax, (size_t)kp(c.nk) * ns_of(c.nk));
-    wmax = std::max(wmax, (size_t)kp(c.gc) * ns_of(c.nk));
-    wmax = std::max(wmax, (size_t)kp(9 * c.nk) * ns_of(c.dc2));
-    int kmax = std::max(kp(9 * c.dc1), kp(9 * c.nk));
-    for (const Branch& b : c.br) {
-        wmax = std::max(wmax, (size_t)kp(9 * b.cin) * ns_of(b.cout));
-        kmax = std::max(kmax, kp(9 * b.cin));
-    }
-    if (c.dc2 > 64 || c.nk > 64) return 0;
-    size_t off = 128;
-    a.off_y = (int)off;
-    off = align_up(off + (size_t)HW * a.sy * 4, 16);
-    a.off_t1 = (int)off;
-    off = align_up(off + (size_t)HW * a.s1 * 4, 16);
-    a.off_t2 = (int)off;
-    off = align_up(off + (size_t)HW * a.s2 * 4, 16);
-    a.off_w = (int)off;
-    off = align_up(off + wmax * 4, 16);
-    a.off_k = (int)off;
-    off = align_up(off + (size_t)kmax * 4, 16);
-    return off <= 160 * 1024 ? off : 0;
+    const NetLdsGeom& g = c.lds;
+    a.sy = g.sy;
+    a.s1 = g.s1;
+    a.s2 = g.s2;
+    a.su = g.su;
+    a.co_tap = c.co_fmt == PK_TAP;
+    a.co_t9 = c.co_fmt == PK_T9;
+    a.ci_t9 = c.ci_fmt == PK_T9;
+    for (int i = 0; i < a.nbr; i++) a.br_t9[i] = c.gc_fmt[i] == PK_T9;
+    a.off_y = g.off_y;
+    a.off_t1 = g.off_t1;
+    a.off_t2 = g.off_t2;
+    a.off_w = g.off_w;
+    a.off_k = g.off_k;
+    return (size_t)g.bytes;
 }
 
 static double net_flops(const Coupling& c) {
@@ -475,7 +459,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     float* so0 = E.at<float>(L.so[0]);
     float* so1 = E.at<float>(L.so[1]);
     NetLdsArgs na;
-    const size_t nlds = E.p.use_netlds ? netlds_setup(E.p, c, na) : 0;
+    const size_t nlds = c.use_lds ? netlds_setup(E.p, c, na) : 0;
+    if (c.use_lds && nlds == 0) throw std::runtime_error("layer planned for k_net_lds does not fit its LDS budget");
     if (nlds > 0) {
         na.u = u;
         na.so[0] = so0;
@@ -483,6 +468,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.params = P;
         na.aux = X;
         na.offs = E.p.dev_table + c.dev_lds_offs;
+        na.zero_bias = X + E.p.aux_zero;
         const int ilds = (int)nlds;
         const double fl = 2.0 * B * net_flops(c);
         const double by = 4.0 * B * (double)c.hc * c.wc * (c.dc1 + c.dc2) * 2;
@@ -507,8 +493,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         std::vector<ProbSpec> pr;
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];
-            pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, nullptr, 0, nullptr, nullptr, 0, P + np.conv_in_k,
-                                  P + np.conv_in_b, y[n], c.nk, 0, c.nk, nullptr, ln ? sy[n] : nullptr, nt3, 0, 1});
+            pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, nullptr, 0, nullptr, nullptr, 0, X + np.ci.w,
+                                  X + np.ci.b, y[n], c.nk, 0, c.nk, nullptr, ln ? sy[n] : nullptr, nt3, 0, 1});
         }
         conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr);
     }
@@ -520,7 +506,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
                 pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + rb.ln1g : nullptr,
-                                      ln ? P + rb.ln1b : nullptr, 1, P + rb.conv_a_k, P + rb.conv_a_b, t1[n], c.nk, 0,
+                                      ln ? P + rb.ln1b : nullptr, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.nk, 0,
                                       c.nk, nullptr, ln ? s1[n] : nullptr, nt1, 0, 1});
             }
             uint64_t used = 0;
@@ -536,8 +522,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
                     pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, ln ? s1[n] : nullptr, nt1,
-                                          ln ? P + rb.ln2g : nullptr, ln ? P + rb.ln2b : nullptr, 1, X + rb.aux_w[bi],
-                                          X + rb.aux_b[bi], t2[n], c.gc, b.out_off, b.cout, nullptr,
+                                          ln ? P + rb.ln2g : nullptr, ln ? P + rb.ln2b : nullptr, 1, X + rb.gc[bi].w,
+                                          X + rb.gc[bi].b, t2[n], c.gc, b.out_off, b.cout, nullptr,
                                           ln ? s2[n] : nullptr, nbr * nt3, bi * nt3, b.dil});
                 }
             }
@@ -549,8 +535,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
                 pr.push_back(ProbSpec{t2[n], c.gc, 0, c.gc, ln ? s2[n] : nullptr, nbr * nt3,
-                                      ln ? P + rb.ln3g : nullptr, ln ? P + rb.ln3b : nullptr, 1, P + rb.conv_b_k,
-                                      P + rb.conv_b_b, y[n], c.nk, 0, c.nk, y[n], ln ? sy[n] : nullptr, nt1, 0, 1});
+                                      ln ? P + rb.ln3g : nullptr, ln ? P + rb.ln3b : nullptr, 1, X + rb.cb.w,
+                                      X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n], ln ? sy[n] : nullptr, nt1, 0, 1});
             }
             conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr);
         }
@@ -562,10 +548,10 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];
             pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + np.ln_out_g : nullptr,
-                                  ln ? P + np.ln_out_b : nullptr, 1, P + np.conv_out_k, P + np.conv_out_b, so[n],
+                                  ln ? P + np.ln_out_b : nullptr, 1, X + np.co.w, X + np.co.b, so[n],
                                   c.dc2, 0, c.dc2, nullptr, nullptr, 0, 0, 1});
         }
-        if (9 * c.dc2 <= 64)
+        if (c.net[0].co.fmt == PK_TAP)
             convtap_launch(E, c.hc, c.wc, pr);
         else
             conv_launch(E, 3, ROLE_CONV_OUT, c.hc, c.wc, pr);
@@ -636,7 +622,6 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     *out = nullptr;
     CNF_TRY
     Plan* p = build_plan(desc);
-    if (const char* e = std::getenv("CNF_NETLDS")) p->use_netlds = std::atoi(e) != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     *out = new cnf_plan{p};
@@ -670,6 +655,7 @@ int cnf_plan_layer_info(const cnf_plan* plan, int layer, cnf_layer_info* out) {
     out->d = L.d;
     out->num_prev_factors = L.npf;
     if (L.kind == CNF_LAYER_COUPLING) {
+        out->fused_net = p.couplings[L.ci].use_lds ? 1 : 0;
         const Coupling& c = p.couplings[L.ci];
         out->mask = c.mask;
         out->hc = c.hc;
@@ -922,6 +908,9 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
     return CNF_OK;
     CNF_CATCH
 }
+
+// diagnostic: phase stamps of the last CNF_STAMPS=1 k_net_lds launch (s_memrealtime, 100 MHz)
+int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 
 int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)plan->p->recorded.size() : -1; }
 

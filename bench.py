@@ -98,14 +98,19 @@ def roofline_for(per):
     return rf
 
 
-def cpu_baseline(cfg, budget_s=20.0):
+def cpu_baseline(cfg, budget_s=12.0):
     """The oracle's torch-CPU fp32 op-for-op restatement of the reference graph, timed on this
     host on a bounded sample of the same workload (rank 0, N=1 only)."""
     try:
         from oracle.cflow_torch_cpu import TorchCPUFlow
     except Exception as e:  # pragma: no cover
         return {'value': None, 'unit': 'images/s', 'cores': 0, 'kind': 'port', 'sample': f'unavailable: {e}'}
-    threads = os.cpu_count() or 1
+    # the host's CPU share, not the machine's: os.cpu_count() on the GPU box reports every core
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, int(os.environ.get('OMP_NUM_THREADS', '16') or 16), 16))
     torch.set_num_threads(threads)
     flow = TorchCPUFlow(**cfg.kwargs())
     P = flow.init_params(0)
@@ -118,7 +123,7 @@ def cpu_baseline(cfg, budget_s=20.0):
             flow.log_loss(xy, P)
             n_img += B
             el = time.perf_counter() - t0
-            if el > budget_s or n_img >= 10 * B:
+            if el > budget_s:
                 break
     model = platform.processor() or platform.machine()
     try:

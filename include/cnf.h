@@ -77,6 +77,7 @@ typedef struct cnf_layer_info {
     int num_dilations;
     int dilations[8];
     int num_prev_factors;  /* factor layers (:230-240) */
+    int fused_net;         /* 1: both s,t nets run as one workgroup per image (k_net_lds) */
 } cnf_layer_info;
 
 /* Plan = cFlow.__init__ (:1431-1695): asserts, scale schedule, dilation

@@ -103,3 +103,32 @@ def test_aux_pack_map_is_grouped_kernel_gather(lib):
 
 def test_version(lib):
     assert b'gfx950' in lib.cnf_version()
+
+
+def test_fused_net_plan(lib):
+    """k_net_lds covers every cfg2 coupling layer whose s,t net fits one CU's 160 KiB LDS image
+    (all but the four 32x32 channel-mask layers); CNF_NETLDS=0 forces the streamed path."""
+    import os
+    kw = PRESETS['cfg2'].kwargs()
+    kw.pop('group_mode')
+
+    def fused():
+        rc, p, keep = _plan(lib, kw)
+        assert rc == 0
+        out = []
+        for i in range(lib.cnf_plan_num_layers(p)):
+            li = _lib.cnf_layer_info()
+            assert lib.cnf_plan_layer_info(p, i, C.byref(li)) == 0
+            if li.kind == 0:
+                out.append((li.hc * li.wc, li.num_kernels, li.fused_net))
+        lib.cnf_plan_destroy(p)
+        return out
+
+    f = fused()
+    assert len(f) == 16
+    assert [x[2] for x in f] == [0 if (hw == 1024 and nk == 64) else 1 for hw, nk, _ in f]
+    os.environ['CNF_NETLDS'] = '0'
+    try:
+        assert all(x[2] == 0 for x in fused())
+    finally:
+        os.environ.pop('CNF_NETLDS')
