@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / 'lib' / 'libcnf_hip.so'
+# CNF_LIB: load an alternative build of the same library (kernel-variant experiments)
+LIB_PATH = Path(os.environ['CNF_LIB']) if os.environ.get('CNF_LIB') else _PKG / 'lib' / 'libcnf_hip.so'
 
 
 class cnf_flow_desc(C.Structure):

@@ -22,7 +22,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int NW = 8;            // waves per workgroup
+#ifndef CNF_NETLDS_NW
+#define CNF_NETLDS_NW 8
+#endif
+constexpr int NW = CNF_NETLDS_NW;   // waves per workgroup (one workgroup per CU: LDS-bound)
 constexpr int NT = NW * 64;      // threads
 
 __device__ __forceinline__ float lrelu_(float x) { return x >= 0.f ? x : LRELU_ALPHA * x; }
@@ -187,7 +190,7 @@ __device__ __forceinline__ void stage_w(const float* __restrict__ src, int n, fl
 
 // Register prefetch of the next conv's pre-packed weight image: loaded before the current conv's
 // MFMA loop, written to LDS after the barrier that retires the current conv.
-constexpr int WPF = 4;   // float4 per thread -> up to WPF*NT*4 floats
+constexpr int WPF = NW >= 16 ? 2 : 4;   // float4 per thread -> up to WPF*NT*4 floats
 struct WPre {
     f4 v[WPF];
     int n4;
@@ -528,7 +531,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     float* T2 = reinterpret_cast<float*>(smem + a.off_t2);
     float* WL = reinterpret_cast<float*>(smem + a.off_w);
     int* KT = reinterpret_cast<int*>(smem + a.off_k);
-    double* red = reinterpret_cast<double*>(smem);   // 2*NW doubles
+    double* red = reinterpret_cast<double*>(smem);   // 2*NW doubles (<= 256 bytes)
     const float* P = a.params;
     const float* X = a.aux;
     const int* off = a.offs + net * a.offs_per_net;   // see NetLdsArgs

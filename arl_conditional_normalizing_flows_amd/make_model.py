@@ -479,21 +479,17 @@ class cFlow:
                                   _stream()), 'cnf_nll')
         return sums, per
 
-    def log_loss(self, xy, process_group=None, global_batch=None):
+    def log_loss(self, xy, process_group=None):
         """cFlow.log_loss (:1800-1848): (loss, z_loss, y_loss, detJ_loss), batch means.
-        With torch.distributed initialised and process_group given (or the default group),
-        the 4 sums are all-reduced (one collective of 4 fp32 over RCCL) and divided by the
-        global batch."""
+        With process_group given (True = the default group) and torch.distributed initialised,
+        this rank's 4 sums and its image count are all-reduced (one collective of 5 fp32,
+        distributed.reduce_nll_sums) so the means are over the global batch; shards may be
+        ragged."""
+        from .distributed import reduce_nll_sums
         xy = _as_input(xy, 'xy')
         sums, _ = self.nll_sums(xy)
-        n = xy.shape[0]
-        if process_group is not None:
-            import torch.distributed as dist
-            grp = None if process_group is True else process_group
-            dist.all_reduce(sums, group=grp)
-            n = global_batch if global_batch is not None else n * dist.get_world_size(grp)
-        s = sums / n
-        return s[0], s[1], s[2], s[3]
+        grp = None if process_group is True else process_group
+        return reduce_nll_sums(sums, xy.shape[0], group=grp, all_reduce=process_group is not None)
 
     def train_step(self, xy):
         raise NotImplementedError('the NLL training step (backward kernels + Adam) is the next milestone; '

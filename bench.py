@@ -165,7 +165,11 @@ def main():
     B = args.batch or cfg.batch
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
     flow = cFlow(**cfg.kwargs(), device=dev, seed=0)
-    xy = torch.from_numpy(synth(cfg, B, 1000 + rank)).to(dev)
+    # one seeded global batch, sliced per rank (weak scaling: B images per rank)
+    from arl_conditional_normalizing_flows_amd.distributed import shard_range, pack_nll_sums
+    lo, hi = shard_range(B * world, rank, world)
+    xy = torch.from_numpy(synth(cfg, B * world, 1000)[lo:hi].copy()).to(dev)
+    red = torch.empty(5, device=dev)
     zy = torch.empty_like(xy)
     ld = torch.empty(B, device=dev)
     per = torch.empty((B, 3), device=dev)
@@ -180,7 +184,8 @@ def main():
         _lib.check(lib.cnf_nll(flow._plan, xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
                                sums.data_ptr(), B, st), 'nll')
         if dist is not None:
-            dist.all_reduce(sums)
+            pack_nll_sums(sums, B, red)
+            dist.all_reduce(red)
 
     step()
     torch.cuda.synchronize()

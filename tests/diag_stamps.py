@@ -23,7 +23,7 @@ buf = np.zeros(256, dtype=np.int64)
 for li, layer in enumerate(flow.layers_list):
     if not hasattr(layer, 'which_mask'):
         continue
-    if li not in (0, 8):
+    if li not in (0, 10, 12, 16, 18):
         continue
     u = torch.randn((64, layer.input_height, layer.input_width, layer.input_depth), device='cuda')
     for _ in range(3):

@@ -1,0 +1,77 @@
+"""Golden fixtures (tests/golden/make_golden.py): the oracle reproduces them (CPU) and the HIP
+path through the C ABI matches them within the north-star tolerance (GPU).
+
+Parity note: the fixtures come from the numpy restatement; the TensorFlow reference cannot run
+here and holds no vectors of its own, so parity is pinned by the oracle's
+invariant KATs (tests/test_oracle.py), not by reference outputs."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from arl_conditional_normalizing_flows_amd.config import PRESETS
+from oracle.cflow_np import OracleCFlow, flatten_params
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+FILES = sorted(glob.glob(os.path.join(HERE, '*.npz')))
+RTOL = 1e-5
+
+
+def _load(path):
+    g = dict(np.load(path, allow_pickle=False))
+    name, gm = str(g['name']), str(g['group_mode'])
+    kw = PRESETS[name].kwargs()
+    kw['group_mode'] = gm
+    ora = OracleCFlow(**kw)
+    if 'params' in g:
+        flat = g['params']
+    else:
+        P = ora.init_params(int(g['seed']))
+        flat = flatten_params({k: np.asarray(v, np.float32) for k, v in P.items()}, ora.specs).astype(np.float32)
+    assert flat.size == int(g['n_params'])
+    assert np.array_equal(flat[:16], g['params_head'])
+    assert abs(flat.astype(np.float64).sum() - float(g['params_sum'])) <= 1e-9 * max(1.0, abs(float(g['params_sum'])))
+    assert abs((flat.astype(np.float64) ** 2).sum() - float(g['params_sumsq'])) <= 1e-9 * float(g['params_sumsq'])
+    P32, o = {}, 0
+    for n, s in ora.specs:
+        size = int(np.prod(s)) if s else 1
+        P32[n] = flat[o:o + size].reshape(s)
+        o += size
+    return g, kw, ora, P32, flat
+
+
+def test_fixtures_present():
+    assert len(FILES) >= 4
+
+
+@pytest.mark.parametrize('path', FILES, ids=[os.path.basename(f) for f in FILES])
+def test_oracle_reproduces_golden(path):
+    g, kw, ora, P32, _ = _load(path)
+    zy, ld = ora.forward(g['xy'].astype(np.float64), P32)
+    assert np.allclose(zy, g['zy'], rtol=0, atol=1e-10)
+    assert np.allclose(ld, g['logdet'], rtol=0, atol=1e-9)
+    x = ora.inverse(g['zy_in'].astype(np.float64), P32)
+    assert np.allclose(x, g['x_out'], rtol=0, atol=1e-10)
+    assert np.allclose(np.array(ora.log_loss(g['xy'].astype(np.float64), P32)), g['nll'], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('path', FILES, ids=[os.path.basename(f) for f in FILES])
+def test_hip_matches_golden(gpu, path):
+    import torch
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    g, kw, ora, P32, flat = _load(path)
+    flow = cFlow(**kw)
+    flow.set_weights(flat)
+    xy = torch.from_numpy(g['xy']).to(gpu)
+    zy, ld = flow(xy, 1, per_image_logdet=True)
+    x = flow(torch.from_numpy(g['zy_in']).to(gpu), -1)
+    nll = [t.item() for t in flow.log_loss(xy)]
+    torch.cuda.synchronize()
+    zr = g['zy']
+    assert np.max(np.abs(zy.cpu().numpy() - zr)) <= RTOL * np.max(np.abs(zr))
+    assert np.max(np.abs(ld.cpu().numpy() - g['logdet'])) <= RTOL * max(1.0, np.max(np.abs(g['logdet']))) * 10
+    assert np.max(np.abs(x.cpu().numpy() - g['x_out'])) <= RTOL * np.max(np.abs(g['x_out']))
+    for r, v in zip(g['nll'], nll):
+        assert abs(r - v) <= RTOL * max(1.0, abs(r)) * 10
