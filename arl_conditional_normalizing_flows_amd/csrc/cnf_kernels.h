@@ -19,16 +19,17 @@ enum { ROLE_CONV_IN = 0, ROLE_CONV_A = 1, ROLE_GC = 2, ROLE_CONV_B = 3, ROLE_CON
 // One convolution problem of a k_conv launch (blockIdx.y selects the problem).
 struct ConvProb {
     const float* in;          // NHWC, image 0
-    const double* in_stats;   // LN partials of the input tensor [B][in_nparts][3] or null (no LN)
+    const double* in_part;    // LN partials (n, mean, M2) of the input tensor [B][part_stride][3] (first
+                              // in_nparts slots valid), or null (no LN)
     const float* gamma;       // LN gamma over the full in_cs-channel tensor (per h,w,c)
     const float* beta;
-    const float* wt;          // [K = KS*KS*cin][cout] (HWIO flattened)
+    const float* wt;          // pre-packed weight image (PK_1X1 / PK_KN / PK_TAP)
     const float* bias;        // [cout]
     const float* res;         // residual, same layout as out, or null
     float* out;
-    double* out_stats;        // LN partials of LeakyReLU(out) [B][out_nparts][3] or null
+    double* out_part;         // per-wave LN partials of LeakyReLU(out) [B][part_stride][3], or null
     int in_cs, in_off, cin, in_nparts;
-    int out_cs, out_off, cout, out_nparts, out_part_base;
+    int out_cs, out_off, cout, part_stride, out_part_base;
     int dil, act;
     int lds_in_off, lds_w_off, lds_k_off;  // byte offsets in dynamic LDS
     int S, Kpad, NS, nr;                   // LDS pixel stride, padded K, B row stride, N-subtiles

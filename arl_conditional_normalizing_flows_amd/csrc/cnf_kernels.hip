@@ -33,55 +33,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// Chan et al. pairwise merge of (n, mean, M2)
-__device__ __forceinline__ void chan_merge(double& n, double& m, double& M2, double nb, double mb, double M2b) {
-    if (nb == 0.0) return;
-    if (n == 0.0) {
-        n = nb;
-        m = mb;
-        M2 = M2b;
-        return;
-    }
-    double nn = n + nb;
-    double delta = mb - m;
-    m = m + delta * (nb / nn);
-    M2 = M2 + M2b + delta * delta * (n * nb / nn);
-    n = nn;
-}
-
-// One wave merges `nparts` LN-stat partials of image `img` (lane 0 holds the result).
-__device__ __forceinline__ void merge_stats(const double* __restrict__ st, int img, int nparts, int lane,
-                                            double& n, double& m, double& M2) {
-    n = 0.0;
-    m = 0.0;
-    M2 = 0.0;
-    for (int base = 0; base < nparts; base += 64) {
-        double pn = 0.0, pm = 0.0, pM = 0.0;
-        if (base + lane < nparts) {
-            const double* q = st + ((size_t)img * nparts + base + lane) * 3;
-            pn = q[0];
-            pm = q[1];
-            pM = q[2];
-        }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            double on = __shfl_xor(pn, o, 64), om = __shfl_xor(pm, o, 64), oM = __shfl_xor(pM, o, 64);
-            chan_merge(pn, pm, pM, on, om, oM);
-        }
-        chan_merge(n, m, M2, pn, pm, pM);
-    }
-}
-
 __device__ __forceinline__ bool stored(const ConvProb& P, int ch) {
     return ((ch < 32 ? (P.st_mask_lo >> ch) : (P.st_mask_hi >> (ch - 32))) & 1u) != 0u;
 }
 
-// Per-tile LN-stat partial (n, mean, M2) of the values a thread holds in vals[0..cnt) (already
-// LeakyReLU'd), reduced over the 256-thread block; written by thread 0. `red` = 8 doubles of LDS.
+// LN statistics of a conv output, produced in the conv's epilogue (no extra pass, no barrier):
+// each wave writes the partial (n, mean, M2) of the LeakyReLU'd values its lanes hold.
 template <int N>
-__device__ __forceinline__ void tile_stats(const float (&vals)[N], const bool (&valid)[N], double* red,
-                                           double* dst) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&valid)[N], double* __restrict__ dst) {
+    const int lane = threadIdx.x & 63;
     float lsum = 0.f;
     int lcnt = 0;
 #pragma unroll
@@ -90,56 +50,50 @@ __device__ __forceinline__ void tile_stats(const float (&vals)[N], const bool (&
             lsum += vals[i];
             lcnt++;
         }
-    double ws = wave_sum((double)lsum);
-    double wc = wave_sum((double)lcnt);
-    __syncthreads();
-    if (lane == 0) {
-        red[wave] = ws;
-        red[4 + wave] = wc;
-    }
-    __syncthreads();
-    const double tot = red[0] + red[1] + red[2] + red[3];
-    const double cnt = red[4] + red[5] + red[6] + red[7];
-    const double mean = cnt > 0 ? tot / cnt : 0.0;
+    const double wc = wave_sum((double)lcnt);
+    const double mean = wc > 0.0 ? wave_sum((double)lsum) / wc : 0.0;
     const float meanf = (float)mean;
     float lm2 = 0.f;
 #pragma unroll
     for (int i = 0; i < N; i++)
         if (valid[i]) {
-            float dl = vals[i] - meanf;
+            const float dl = vals[i] - meanf;
             lm2 += dl * dl;
         }
-    double wm2 = wave_sum((double)lm2);
-    __syncthreads();
-    if (lane == 0) red[wave] = wm2;
-    __syncthreads();
-    if (tid == 0) {
-        double m2 = red[0] + red[1] + red[2] + red[3];
-        const double dm = mean - (double)meanf;   // sum (x-m')^2 = M2 + n (m-m')^2
-        m2 -= cnt * dm * dm;
-        if (m2 < 0.0) m2 = 0.0;
-        dst[0] = cnt;
+    const double dm = mean - (double)meanf;   // sum (x-m')^2 = M2 + n (m-m')^2
+    double m2 = wave_sum((double)lm2) - wc * dm * dm;
+    if (m2 < 0.0) m2 = 0.0;
+    if (lane == 0) {
+        dst[0] = wc;
         dst[1] = mean;
         dst[2] = m2;
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// shared pieces of the convolution kernels
-// ---------------------------------------------------------------------------------------------
-
-// Input-LN statistics of image `img`: wave 0 merges the producer's tile partials; (mu, rstd)
-// land in red[8], red[9]. Caller must __syncthreads() before reading them.
-__device__ __forceinline__ void stats_prologue(const ConvProb& P, int img, double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (P.in_stats != nullptr && wave == 0) {
-        double n, m, M2;
-        merge_stats(P.in_stats, img, P.in_nparts, lane, n, m, M2);
-        if (lane == 0) {
-            red[8] = m;
-            red[9] = 1.0 / sqrt(M2 / n + (double)LN_EPS);
-        }
+// (mean, rstd) of the input LayerNorm of image img from the producer's partials, merged by every
+// wave on its own (parallel-axis form: one division, fixed order, no barrier); identity without LN.
+__device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
+    mu = 0.f;
+    rstd = 1.f;
+    if (P.in_part == nullptr) return;
+    const int lane = threadIdx.x & 63;
+    const double* __restrict__ q = P.in_part + (size_t)img * P.part_stride * 3;
+    double ln = 0.0, ls = 0.0;
+    for (int i = lane; i < P.in_nparts; i += 64) {
+        const double n = q[3 * i];
+        ln += n;
+        ls += n * q[3 * i + 1];
     }
+    const double nt = wave_sum(ln);
+    const double mt = wave_sum(ls) / nt;
+    double lm = 0.0;
+    for (int i = lane; i < P.in_nparts; i += 64) {
+        const double d = q[3 * i + 1] - mt;
+        lm += q[3 * i + 2] + q[3 * i] * d * d;
+    }
+    const double M2 = wave_sum(lm);
+    mu = (float)mt;
+    rstd = (float)(1.0 / sqrt(M2 / nt + (double)LN_EPS));
 }
 
 // Epilogue shared by all conv kernels. Lane (i, q) of wave w holds, for subtile s = w + 4m,
@@ -197,7 +151,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][N
                 acc[m][n][r] += bias[n];
                 if (pv[m][r] && st[n]) out[oe[m][r] + n * 16 + i16] = acc[m][n][r];
             }
-    if (P.out_stats != nullptr) {
+    if (P.out_part != nullptr) {
         float vals[MR * NR * 4];
         bool valid[MR * NR * 4];
 #pragma unroll
@@ -209,7 +163,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][N
                     vals[(m * NR + n) * 4 + r] = lrelu(acc[m][n][r]);
                     valid[(m * NR + n) * 4 + r] = pv[m][r] && chv[n];
                 }
-        tile_stats(vals, valid, red, P.out_stats + ((size_t)img * P.out_nparts + P.out_part_base + tr) * 3);
+        ln_partial(vals, valid,
+                   P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tr * 4 + (threadIdx.x >> 6)) * 3);
     }
 }
 
@@ -351,14 +306,11 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, const ConvProb& P,
     const int G = (P.cin + 15) >> 4;
     double* red = reinterpret_cast<double*>(smem);
     float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
-    stats_prologue(P, img, red);
-    const int cout = P.cout;
+    float mu, rstd;
+    in_ln(P, img, mu, rstd);
     copy_to_lds<256>(P.wt, lw, G * 16 * 16 * NR);   // pre-packed B image (PK_1X1)
-    (void)cout;
     __syncthreads();
-    const bool has_ln = P.in_stats != nullptr;
-    const float mu = has_ln ? (float)red[8] : 0.f;
-    const float rstd = has_ln ? (float)red[9] : 1.f;
+    const bool has_ln = P.in_part != nullptr;
     f4 acc[MR][NR];
     gemm_stream<MR, NR, VEC>(P, img, HW, px0, Pv, lw, G, mu, rstd, has_ln, acc);
     conv_epilogue<MR, NR>(P, acc, img, HW, px0, Pv, tr, red);
@@ -401,7 +353,8 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a, const ConvProb& P,
     float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
     int* lk = reinterpret_cast<int*>(smem + P.lds_k_off);
 
-    stats_prologue(P, img, red);
+    float mu, rstd;
+    in_ln(P, img, mu, rstd);
     copy_to_lds<256>(P.wt, lw, Kpad * NS);   // pre-packed [Kpad][NS] (PK_KN)
     // per-k LDS offsets of the A operand (tap, channel)
     for (int k = tid; k < Kpad; k += 256) {
@@ -414,9 +367,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a, const ConvProb& P,
         lk[k] = off;
     }
     __syncthreads();
-    const bool has_ln = P.in_stats != nullptr;
-    const float mu = has_ln ? (float)red[8] : 0.f;
-    const float rstd = has_ln ? (float)red[9] : 1.f;
+    const bool has_ln = P.in_part != nullptr;
     // stage the (normalised) input band (+halo) into LDS; magic-number divisions, batched loads
     {
         const float* __restrict__ inb = P.in + (size_t)img * HW * P.in_cs + P.in_off;
@@ -530,12 +481,11 @@ __device__ __forceinline__ void convtap_body(const ConvArgs& a, const ConvProb& 
     float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
     float* lc = reinterpret_cast<float*>(smem + P.lds_in_off);
 
-    stats_prologue(P, img, red);
+    float mu, rstd;
+    in_ln(P, img, mu, rstd);
     copy_to_lds<256>(P.wt, lw, G * 16 * NSJ);   // pre-packed tap B image (PK_TAP)
     __syncthreads();
-    const bool has_ln = P.in_stats != nullptr;
-    const float mu = has_ln ? (float)red[8] : 0.f;
-    const float rstd = has_ln ? (float)red[9] : 1.f;
+    const bool has_ln = P.in_part != nullptr;
     f4 acc[MT][NR];
     gemm_stream<MT, NR, VEC>(P, img, HW, rb0 * W, nband, lw, G, mu, rstd, has_ln, acc);
     const int i16 = lane & 15, kq = lane >> 4;

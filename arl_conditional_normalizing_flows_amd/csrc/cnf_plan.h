@@ -113,7 +113,7 @@ struct Recorded {
 struct WsLayout {
     size_t total = 0;
     size_t uv[2] = {0, 0}, u1c = 0, y[2] = {0, 0}, t1[2] = {0, 0}, t2[2] = {0, 0}, so[2] = {0, 0};
-    size_t st_y[2] = {0, 0}, st_t1[2] = {0, 0}, st_t2[2] = {0, 0};
+    size_t st_part[2][3] = {};   // LN partials [net][y, t1, t2]
     size_t ld = 0;
     int64_t n_uv = 0, n_u1c = 0, n_y = 0, n_t2 = 0, n_so = 0;
     int st_parts = 0;   // partial slots per image per LN slab

@@ -108,8 +108,8 @@ WsLayout Plan::layout(int B) const {
         n_t2 = std::max<int64_t>(n_t2, npx * c.gc);
         n_so = std::max<int64_t>(n_so, npx * c.dc2);
         Geo g = conv_geo(c.hc, c.wc);
-        parts = std::max(parts, g.tiles * (int)c.br.size());
-        parts = std::max(parts, conv1_geo(c.hc, c.wc).tiles);
+        parts = std::max(parts, 4 * g.tiles * (int)c.br.size());   // 4 waves per workgroup
+        parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
     L.n_uv = n_uv;
@@ -134,10 +134,11 @@ WsLayout Plan::layout(int B) const {
         L.t1[n] = take(Bz * n_y * 4);
         L.t2[n] = take(Bz * n_t2 * 4);
         L.so[n] = take(Bz * n_so * 4);
-        L.st_y[n] = take(Bz * parts * 3 * 8);
-        L.st_t1[n] = take(Bz * parts * 3 * 8);
-        L.st_t2[n] = take(Bz * parts * 3 * 8);
+        for (int k = 0; k < 3; k++) {   // LN slabs y, t1, t2: per-wave partials
+            L.st_part[n][k] = take(Bz * parts * 3 * 8);
+        }
     }
+
     L.ld = take(std::max<size_t>(1, couplings.size()) * Bz * ldp * 8);
     L.total = off;
     return L;
@@ -173,11 +174,17 @@ struct Exec {
     }
 };
 
+// LN statistics slab of one tensor: per-wave partials [B][st_parts][3] of which the last producer
+// wrote the first nparts (see ConvProb)
+struct Slab {
+    double* part = nullptr;
+    int nparts = 0;
+};
+
 struct ProbSpec {
     const float* in;
     int in_cs, in_off, cin;
-    const double* in_stats;
-    int in_nparts;
+    Slab in_st;               // input LN partials (.part == null: no LN)
     const float* gamma;
     const float* beta;
     int act;
@@ -186,8 +193,8 @@ struct ProbSpec {
     float* out;
     int out_cs, out_off, cout;
     const float* res;
-    double* out_stats;
-    int out_nparts, out_part_base;
+    Slab out_st;              // .part == null: no output statistics
+    int out_part_base;        // first partial slot of this problem
     int dil;
 };
 
@@ -237,22 +244,22 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
         const ProbSpec& s = probs[i];
         ConvProb& q = a.p[i];
         q.in = s.in;
-        q.in_stats = s.in_stats;
+        q.in_part = s.in_st.part;
+        q.in_nparts = s.in_st.nparts;
         q.gamma = s.gamma;
         q.beta = s.beta;
         q.wt = s.wt;
         q.bias = s.bias;
         q.res = s.res;
         q.out = s.out;
-        q.out_stats = s.out_stats;
+        q.out_part = s.out_st.part;
         q.in_cs = s.in_cs;
         q.in_off = s.in_off;
         q.cin = s.cin;
-        q.in_nparts = s.in_nparts;
         q.out_cs = s.out_cs;
         q.out_off = s.out_off;
         q.cout = s.cout;
-        q.out_nparts = s.out_nparts;
+        q.part_stride = E.L.st_parts;
         q.out_part_base = s.out_part_base;
         q.dil = s.dil;
         q.act = s.act;
@@ -289,7 +296,7 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
         }
         lds = std::max(lds, off);
         flops += 2.0 * HWB * K * s.cout;
-        bytes += 4.0 * (HWB * s.cin + HWB * s.cout * (s.res ? 2 : 1) + (s.in_stats ? 2.0 * h * w * s.cin : 0.0) +
+        bytes += 4.0 * (HWB * s.cin + HWB * s.cout * (s.res ? 2 : 1) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
                         (double)K * s.cout + s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
@@ -335,7 +342,9 @@ static void convtap_launch(Exec& E, int h, int w, const std::vector<ProbSpec>& p
         const ProbSpec& s = probs[i];
         ConvProb& q = a.p[i];
         q.in = s.in;
-        q.in_stats = s.in_stats;
+        q.in_part = s.in_st.part;
+        q.in_nparts = s.in_st.nparts;
+        q.part_stride = E.L.st_parts;
         q.gamma = s.gamma;
         q.beta = s.beta;
         q.wt = s.wt;
@@ -344,7 +353,6 @@ static void convtap_launch(Exec& E, int h, int w, const std::vector<ProbSpec>& p
         q.in_cs = s.in_cs;
         q.in_off = s.in_off;
         q.cin = s.cin;
-        q.in_nparts = s.in_nparts;
         q.out_cs = s.out_cs;
         q.out_off = s.out_off;
         q.cout = s.cout;
@@ -365,7 +373,7 @@ static void convtap_launch(Exec& E, int h, int w, const std::vector<ProbSpec>& p
         lds = std::max(lds, off);
         if (s.cin % 4 || s.in_cs % 4 || s.in_off % 4) vec = false;
         flops += 2.0 * HWB * 9 * s.cin * s.cout;
-        bytes += 4.0 * (HWB * s.cin + HWB * s.cout + (s.in_stats ? 2.0 * h * w * s.cin : 0.0) + 9.0 * s.cin * s.cout);
+        bytes += 4.0 * (HWB * s.cin + HWB * s.cout + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) + 9.0 * s.cin * s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("tap conv exceeds the LDS budget");
     const int ilds = (int)lds, grid_x = E.B * g.tiles;
@@ -484,30 +492,39 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     float* t1[2] = {E.at<float>(L.t1[0]), E.at<float>(L.t1[1])};
     float* t2[2] = {E.at<float>(L.t2[0]), E.at<float>(L.t2[1])};
     float* so[2] = {E.at<float>(L.so[0]), E.at<float>(L.so[1])};
-    double* sy[2] = {E.at<double>(L.st_y[0]), E.at<double>(L.st_y[1])};
-    double* s1[2] = {E.at<double>(L.st_t1[0]), E.at<double>(L.st_t1[1])};
-    double* s2[2] = {E.at<double>(L.st_t2[0]), E.at<double>(L.st_t2[1])};
+    Slab sl[2][3];   // [net][y, t1, t2]
+    for (int n = 0; n < 2; n++)
+        for (int k = 0; k < 3; k++) {
+            sl[n][k].part = E.at<double>(L.st_part[n][k]);
+        }
+    // out_slab records how many partial slots the producing launch writes; in_slab hands that count on
+    auto out_slab = [&](int n, int k, int nparts) {
+        if (!ln) return Slab{};
+        sl[n][k].nparts = nparts;
+        return sl[n][k];
+    };
+    auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };
+    const float* none = nullptr;
 
     // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
     {
         std::vector<ProbSpec> pr;
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];
-            pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, nullptr, 0, nullptr, nullptr, 0, X + np.ci.w,
-                                  X + np.ci.b, y[n], c.nk, 0, c.nk, nullptr, ln ? sy[n] : nullptr, nt3, 0, 1});
+            pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, Slab{}, none, none, 0, X + np.ci.w, X + np.ci.b, y[n], c.nk, 0,
+                                  c.nk, none, out_slab(n, 0, 4 * nt3), 0, 1});
         }
         conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr);
     }
-    int ny_parts = nt3;
     for (int r = 0; r < c.R; r++) {
         // conv_a: LN1(LReLU(y)) -> 1x1 -> t1
         {
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
-                pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + rb.ln1g : nullptr,
-                                      ln ? P + rb.ln1b : nullptr, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.nk, 0,
-                                      c.nk, nullptr, ln ? s1[n] : nullptr, nt1, 0, 1});
+                pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + rb.ln1g : none,
+                                      ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.nk, 0, c.nk,
+                                      none, out_slab(n, 1, 4 * nt1), 0, 1});
             }
             uint64_t used = 0;
             for (const Branch& b : c.br)
@@ -521,10 +538,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 const RBParams& rb = c.net[n].rb[r];
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
-                    pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, ln ? s1[n] : nullptr, nt1,
-                                          ln ? P + rb.ln2g : nullptr, ln ? P + rb.ln2b : nullptr, 1, X + rb.gc[bi].w,
-                                          X + rb.gc[bi].b, t2[n], c.gc, b.out_off, b.cout, nullptr,
-                                          ln ? s2[n] : nullptr, nbr * nt3, bi * nt3, b.dil});
+                    pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
+                                          ln ? P + rb.ln2b : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
+                                          b.out_off, b.cout, none, out_slab(n, 2, 4 * nt3 * nbr), bi * nt3 * 4, b.dil});
                 }
             }
             conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
@@ -534,22 +550,21 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
-                pr.push_back(ProbSpec{t2[n], c.gc, 0, c.gc, ln ? s2[n] : nullptr, nbr * nt3,
-                                      ln ? P + rb.ln3g : nullptr, ln ? P + rb.ln3b : nullptr, 1, X + rb.cb.w,
-                                      X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n], ln ? sy[n] : nullptr, nt1, 0, 1});
+                pr.push_back(ProbSpec{t2[n], c.gc, 0, c.gc, in_slab(n, 2), ln ? P + rb.ln3g : none,
+                                      ln ? P + rb.ln3b : none, 1, X + rb.cb.w, X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n],
+                                      out_slab(n, 0, 4 * nt1), 0, 1});
             }
             conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr);
         }
-        ny_parts = nt1;
     }
     // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b)
     {
         std::vector<ProbSpec> pr;
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];
-            pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, ln ? sy[n] : nullptr, ny_parts, ln ? P + np.ln_out_g : nullptr,
-                                  ln ? P + np.ln_out_b : nullptr, 1, X + np.co.w, X + np.co.b, so[n],
-                                  c.dc2, 0, c.dc2, nullptr, nullptr, 0, 0, 1});
+            pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + np.ln_out_g : none,
+                                  ln ? P + np.ln_out_b : none, 1, X + np.co.w, X + np.co.b, so[n], c.dc2, 0, c.dc2,
+                                  none, Slab{}, 0, 1});
         }
         if (c.net[0].co.fmt == PK_TAP)
             convtap_launch(E, c.hc, c.wc, pr);
