@@ -1,0 +1,126 @@
+// cnf_device.h — device helpers shared by the conv kernels (cnf_kernels.hip, cnf_stream.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cnf_kernels.h"
+
+namespace cnf {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
+__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// raw buffer resource over [base, base + bytes): loads beyond the range return 0, stores beyond it
+// are dropped — used for branch-free masking (offset BUF_OOB) and 32-bit offsets.
+constexpr uint32_t BUF_OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f4 buf_load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void buf_store1(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ bool stored(const ConvProb& P, int ch) {
+    return ((ch < 32 ? (P.st_mask_lo >> ch) : (P.st_mask_hi >> (ch - 32))) & 1u) != 0u;
+}
+
+// LN statistics of a conv output, produced in the conv's epilogue (no extra pass, no barrier):
+// each wave writes the partial (n, mean, M2) of the LeakyReLU'd values its lanes hold. Sums are
+// fp32 shifted by a wave-uniform sample value K (readfirstlane), so sum (x-K)^2 does not cancel;
+// the (n, mean, M2) conversion and every cross-wave merge are fp64.
+template <int N>
+__device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&valid)[N], double* __restrict__ dst) {
+    const float K = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, vals[0])));
+    float s1 = 0.f, s2 = 0.f, c = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const float d = valid[i] ? vals[i] - K : 0.f;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+        c += valid[i] ? 1.f : 0.f;
+    }
+    s1 = wave_sum_f(s1);
+    s2 = wave_sum_f(s2);
+    c = wave_sum_f(c);
+    if ((threadIdx.x & 63) == 0) {
+        const double n = c, S1 = s1, S2 = s2;
+        const double m = n > 0.0 ? S1 / n : 0.0;
+        double M2 = S2 - S1 * m;
+        dst[0] = n;
+        dst[1] = n > 0.0 ? (double)K + m : 0.0;
+        dst[2] = M2 > 0.0 ? M2 : 0.0;
+    }
+}
+
+// (mean, rstd) of the input LayerNorm of image img from the producer's partials, merged by every
+// wave on its own (parallel-axis form: one division, fixed order, no barrier); identity without LN.
+__device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
+    mu = 0.f;
+    rstd = 1.f;
+    if (P.in_part == nullptr) return;
+    const int lane = threadIdx.x & 63;
+    const double* __restrict__ q = P.in_part + (size_t)img * P.part_stride * 3;
+    double ln = 0.0, ls = 0.0;
+    for (int i = lane; i < P.in_nparts; i += 64) {
+        const double n = q[3 * i];
+        ln += n;
+        ls += n * q[3 * i + 1];
+    }
+    const double nt = wave_sum(ln);
+    const double mt = wave_sum(ls) / nt;
+    double lm = 0.0;
+    for (int i = lane; i < P.in_nparts; i += 64) {
+        const double d = q[3 * i + 1] - mt;
+        lm += q[3 * i + 2] + q[3 * i] * d * d;
+    }
+    const double M2 = wave_sum(lm);
+    mu = (float)mt;
+    rstd = (float)(1.0 / sqrt(M2 / nt + (double)LN_EPS));
+}
+
+
+// Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.
+template <int NTH>
+__device__ __forceinline__ void copy_to_lds(const float* __restrict__ src, float* dst, int n) {
+    const int n4 = n >> 2;
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+    f4* d4 = reinterpret_cast<f4*>(dst);
+    for (int base = 0; base < n4; base += NTH * 8) {
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            v[u] = i < n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = base + u * NTH + (int)threadIdx.x;
+            if (i < n4) d4[i] = v[u];
+        }
+    }
+}
+
+
+}  // namespace cnf

@@ -13,6 +13,9 @@ constexpr double LOG_2PI_D = 1.8378770664093453;
 
 constexpr int MAXPROB = 12;
 
+// packed weight-image formats (see cnf_plan.h PackedConv)
+enum { PK_1X1 = 0, PK_KN = 1, PK_TAP = 2, PK_Q4 = 3 };
+
 // kernel roles: distinct symbols so per-kernel profiles separate the ResNeXt stages
 enum { ROLE_CONV_IN = 0, ROLE_CONV_A = 1, ROLE_GC = 2, ROLE_CONV_B = 3, ROLE_CONV_OUT = 4 };
 
@@ -40,7 +43,7 @@ struct ConvProb {
 struct ConvArgs {
     ConvProb p[MAXPROB];
     int H, W, TH, tiles_per_img, nprob, B;
-    int P;   // 1x1 kernels: pixels per tile (tiles are runs of pixels inside one image)
+    int P;     // 1x1 kernels: pixels per tile (tiles are runs of pixels inside one image)
 };
 
 struct CoupArgs {
@@ -55,6 +58,12 @@ struct CoupArgs {
 
 // Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).
 constexpr int NETLDS_MAXBR = 8;
+// one conv of k_net_lds: packed format (PK_*), image floats, K extent (PK_KN: padded K; PK_Q4:
+// 16 * groups), B row stride (PK_KN)
+struct LdsConv {
+    int fmt, size, kpad, ns;
+};
+
 struct NetLdsArgs {
     const float* u;           // layer input [B][H][W][D]
     float* so[2];             // outputs: raw conv_out of net A (pre-tanh) / net b, [B][hc][wc][dc2]
@@ -67,9 +76,8 @@ struct NetLdsArgs {
         br_dil[NETLDS_MAXBR];
     int nwin, win_off[NETLDS_MAXBR], win_len[NETLDS_MAXBR];  // disjoint union of the branch input windows
     int sy, s1, s2, su;                          // LDS pixel strides (floats)
-    int co_tap, co_t9, ci_t9;                    // packed formats of conv_out / conv_in (else PK_KN)
-    int br_t9[NETLDS_MAXBR];                     // grouped branch packed as PK_T9 (else PK_KN)
-    const float* zero_bias;                      // >= 64 zeros (tap GEMM has no bias)
+    LdsConv ci, ca, cb, co, gcv[NETLDS_MAXBR];   // packed images of conv_in, conv_a, conv_b, conv_out, branches
+    const float* zero_bias;                      // >= 128 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
 };
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
@@ -77,6 +85,7 @@ int read_stamps(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_pw(int nr, int gm, int mi, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

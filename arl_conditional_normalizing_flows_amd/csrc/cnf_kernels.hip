@@ -19,82 +19,9 @@
 
 #include <cstdint>
 
-#include "cnf_kernels.h"
+#include "cnf_device.h"
 
 namespace cnf {
-
-typedef float f4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float lrelu(float x) { return x >= 0.f ? x : LRELU_ALPHA * x; }
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ bool stored(const ConvProb& P, int ch) {
-    return ((ch < 32 ? (P.st_mask_lo >> ch) : (P.st_mask_hi >> (ch - 32))) & 1u) != 0u;
-}
-
-// LN statistics of a conv output, produced in the conv's epilogue (no extra pass, no barrier):
-// each wave writes the partial (n, mean, M2) of the LeakyReLU'd values its lanes hold.
-template <int N>
-__device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&valid)[N], double* __restrict__ dst) {
-    const int lane = threadIdx.x & 63;
-    float lsum = 0.f;
-    int lcnt = 0;
-#pragma unroll
-    for (int i = 0; i < N; i++)
-        if (valid[i]) {
-            lsum += vals[i];
-            lcnt++;
-        }
-    const double wc = wave_sum((double)lcnt);
-    const double mean = wc > 0.0 ? wave_sum((double)lsum) / wc : 0.0;
-    const float meanf = (float)mean;
-    float lm2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < N; i++)
-        if (valid[i]) {
-            const float dl = vals[i] - meanf;
-            lm2 += dl * dl;
-        }
-    const double dm = mean - (double)meanf;   // sum (x-m')^2 = M2 + n (m-m')^2
-    double m2 = wave_sum((double)lm2) - wc * dm * dm;
-    if (m2 < 0.0) m2 = 0.0;
-    if (lane == 0) {
-        dst[0] = wc;
-        dst[1] = mean;
-        dst[2] = m2;
-    }
-}
-
-// (mean, rstd) of the input LayerNorm of image img from the producer's partials, merged by every
-// wave on its own (parallel-axis form: one division, fixed order, no barrier); identity without LN.
-__device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
-    mu = 0.f;
-    rstd = 1.f;
-    if (P.in_part == nullptr) return;
-    const int lane = threadIdx.x & 63;
-    const double* __restrict__ q = P.in_part + (size_t)img * P.part_stride * 3;
-    double ln = 0.0, ls = 0.0;
-    for (int i = lane; i < P.in_nparts; i += 64) {
-        const double n = q[3 * i];
-        ln += n;
-        ls += n * q[3 * i + 1];
-    }
-    const double nt = wave_sum(ln);
-    const double mt = wave_sum(ls) / nt;
-    double lm = 0.0;
-    for (int i = lane; i < P.in_nparts; i += 64) {
-        const double d = q[3 * i + 1] - mt;
-        lm += q[3 * i + 2] + q[3 * i] * d * d;
-    }
-    const double M2 = wave_sum(lm);
-    mu = (float)mt;
-    rstd = (float)(1.0 / sqrt(M2 / nt + (double)LN_EPS));
-}
 
 // Epilogue shared by all conv kernels. Lane (i, q) of wave w holds, for subtile s = w + 4m,
 // out[pixel pix0 + 16s + 4q + r][channel 16n + i] in acc[m][n][r]. Adds bias and the residual
@@ -165,27 +92,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][N
                 }
         ln_partial(vals, valid,
                    P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tr * 4 + (threadIdx.x >> 6)) * 3);
-    }
-}
-
-// Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.
-template <int NTH>
-__device__ __forceinline__ void copy_to_lds(const float* __restrict__ src, float* dst, int n) {
-    const int n4 = n >> 2;
-    const f4* s4 = reinterpret_cast<const f4*>(src);
-    f4* d4 = reinterpret_cast<f4*>(dst);
-    for (int base = 0; base < n4; base += NTH * 8) {
-        f4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int i = base + u * NTH + (int)threadIdx.x;
-            v[u] = i < n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int i = base + u * NTH + (int)threadIdx.x;
-            if (i < n4) d4[i] = v[u];
-        }
     }
 }
 

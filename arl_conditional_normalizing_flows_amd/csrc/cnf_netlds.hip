@@ -1,14 +1,18 @@
 // cnf_netlds.hip — one workgroup computes a whole s,t network (net A or net b of one coupling
 // layer, conv_cINN_make_model.py:1076-1213 + conv_cINN_base_functions.py:330-627) for ONE image
 // with every activation resident in LDS. Used for the layers whose activations fit the 160 KiB
-// LDS of a CU (the compressed images of 16x16 and below at cfg2); the per-image LayerNorm over
-// H*W*C becomes an exact in-workgroup two-pass reduction and the ~11 launches of the streamed
-// path collapse into one.
+// LDS of a CU (the compressed images of 16x16 and below at cfg2); the ~11 launches of the
+// streamed path collapse into one.
 //
-// LDS: Y (residual stream, nk ch) | T1 (nk ch) | T2 (concat of the grouped branches, gc ch;
-// also the normalised input of conv_a and the gathered u1c of conv_in) | W (weights of the
-// conv being run) | K (per-k tap table) | reduction scratch. Pixel strides are == 2 (mod 4) so
-// the MFMA A-operand reads (16 pixels x 1 channel per 16-lane group) are bank-conflict free.
+// LDS: reduction slots | Y (residual stream, nk ch) | T1 (nk ch) | T2 (concat of the grouped
+// branches, gc ch; also the normalised input of conv_a and the gathered u1c of conv_in) | W
+// (packed weights of the conv being run) | K (tap / quad table). Pixel strides are == 8 (mod 16)
+// floats so the channel-quad ds_read_b128 A reads are bank-conflict free.
+//
+// LayerNorm statistics (per image over H*W*C, conv_cINN_base_functions.py:357) are produced in
+// the epilogue of the conv that writes the tensor: every lane accumulates shifted fp32 sums of
+// LeakyReLU(out) (shift = a wave-uniform sample value), each wave reduces and Chan-merges into its
+// fp64 LDS slot, and after the conv's barrier every wave merges the NW slots — no extra pass.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -26,84 +30,101 @@ namespace {
 #define CNF_NETLDS_NW 8
 #endif
 constexpr int NW = CNF_NETLDS_NW;   // waves per workgroup (one workgroup per CU: LDS-bound)
-constexpr int NT = NW * 64;      // threads
+constexpr int NT = NW * 64;         // threads
 
-__device__ __forceinline__ float lrelu_(float x) { return x >= 0.f ? x : LRELU_ALPHA * x; }
+// LeakyReLU(0.3) as max(x, 0.3x) (2 VALU ops; equal to the select form for every finite x)
+__device__ __forceinline__ float lrelu_(float x) { return __builtin_fmaxf(x, LRELU_ALPHA * x); }
 
-__device__ __forceinline__ double wsum(double v) {
+__device__ __forceinline__ float wsum_f(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wsum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-__device__ __forceinline__ double block_sum(double v, double* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    v = wsum(v);
-    __syncthreads();
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) t += red[w];
-    return t;
+// ---------------------------------------------------------------------------------------------
+// LN statistics produced in conv epilogues
+// ---------------------------------------------------------------------------------------------
+struct LStat {
+    float K, s1, s2, c;
+};
+__device__ __forceinline__ void lst_reset(LStat& a) {
+    a.K = 0.f;
+    a.s1 = 0.f;
+    a.s2 = 0.f;
+    a.c = 0.f;
 }
-
-// Per-image LN statistics of LeakyReLU(buf[p][c]) (p < HW, c < C) in one pass of shifted sums
-// (shift K = the first element, so sum (x-K)^2 does not cancel catastrophically), fp32 per
-// thread, fp64 across the block.
-__device__ __forceinline__ void ln_stats(const float* buf, int stride, int HW, int C, double* red, float& mu,
-                                         float& rstd) {
-    const int n = HW * C;
-    const float K = lrelu_(buf[0]);
-    float s1 = 0.f, s2 = 0.f;
-    if (((stride | C) & 3) == 0) {
-        const int C4 = C >> 2;
-        for (int e = threadIdx.x; e < (n >> 2); e += NT) {
-            const int p = e / C4, c = (e - p * C4) << 2;
-            const f4 v = *reinterpret_cast<const f4*>(buf + p * stride + c);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float d = lrelu_(v[j]) - K;
-                s1 += d;
-                s2 += d * d;
-            }
+// shift = LeakyReLU of lane 0's value (call in wave-uniform control flow)
+__device__ __forceinline__ void lst_setk(LStat& a, float v) {
+    a.K = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lrelu_(v))));
+}
+__device__ __forceinline__ void lst_add(LStat& a, float v) {
+    const float d = lrelu_(v) - a.K;
+    a.s1 += d;
+    a.s2 = fmaf(d, d, a.s2);
+    a.c += 1.f;
+}
+// each wave zeroes its own slot before the producing conv(s) of a tensor
+__device__ __forceinline__ void lst_zero(double* slots) {
+    if ((threadIdx.x & 63) == 0) {
+        double* q = slots + 3 * (threadIdx.x >> 6);
+        q[0] = 0.0;
+        q[1] = 0.0;
+        q[2] = 0.0;
+    }
+}
+// wave-reduce the lane sums and Chan-merge (n, mean, M2) into this wave's slot
+__device__ __forceinline__ void lst_flush(const LStat& a, double* slots) {
+    const float s1 = wsum_f(a.s1), s2 = wsum_f(a.s2), c = wsum_f(a.c);
+    if ((threadIdx.x & 63) == 0 && c > 0.f) {
+        const double nb = c, S1 = s1;
+        const double mb = S1 / nb;
+        double M2b = (double)s2 - S1 * mb;
+        if (M2b < 0.0) M2b = 0.0;
+        double* q = slots + 3 * (threadIdx.x >> 6);
+        const double na = q[0], ma = q[1];
+        const double mbx = (double)a.K + mb;
+        if (na == 0.0) {
+            q[0] = nb;
+            q[1] = mbx;
+            q[2] = M2b;
+        } else {
+            const double nn = na + nb, dl = mbx - ma;
+            q[1] = ma + dl * (nb / nn);
+            q[2] = q[2] + M2b + dl * dl * (na * nb / nn);
+            q[0] = nn;
         }
-    } else {
-        for (int e = threadIdx.x; e < n; e += NT) {
-            const int p = e / C, c = e - p * C;
-            const float d = lrelu_(buf[p * stride + c]) - K;
-            s1 += d;
-            s2 += d * d;
-        }
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double d1 = wsum((double)s1), d2 = wsum((double)s2);
-    __syncthreads();
-    if (lane == 0) {
-        red[wave] = d1;
-        red[NW + wave] = d2;
+}
+// (mean, rstd) of the tensor from the NW slots (every wave, after the producer's barrier)
+__device__ __forceinline__ void lst_final(const double* slots, float& mu, float& rstd) {
+    const int lane = threadIdx.x & 63;
+    double n = 0.0, m = 0.0, M2 = 0.0;
+    if (lane < NW) {
+        n = slots[3 * lane];
+        m = slots[3 * lane + 1];
+        M2 = slots[3 * lane + 2];
     }
-    __syncthreads();
-    double t1 = 0.0, t2 = 0.0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-        t1 += red[w];
-        t2 += red[NW + w];
-    }
-    const double m = t1 / n;                 // mean of (x - K)
-    double var = t2 / n - m * m;
-    if (var < 0.0) var = 0.0;
-    mu = (float)((double)K + m);
-    rstd = (float)(1.0 / sqrt(var + (double)LN_EPS));
+    const double N = wsum_d(n);
+    const double mean = wsum_d(n * m) / N;
+    const double d = m - mean;
+    const double M2t = wsum_d(M2 + n * d * d);
+    mu = (float)mean;
+    rstd = (float)(1.0 / sqrt(M2t / N + (double)LN_EPS));
 }
 
 // dst[p][c] = LN(LeakyReLU(src[p][c])) for channels [c0, c0+nc) of a C_ln-channel LN tensor;
 // gamma/beta are per (p, c) over C_ln channels (global, L2-resident). dst may alias src.
-// Full-width tensors take a float4 path with up to 8 gamma + 8 beta float4 loads in flight.
+// Quad-aligned windows take a float4 path with up to 8 gamma + 8 beta float4 loads in flight.
 __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* dst, int dstride, int HW, int c0,
                                          int nc, int C_ln, float mu, float rstd, const float* __restrict__ g,
                                          const float* __restrict__ b, bool ln) {
     const int n = HW * nc;
+    const float nmr = -mu * rstd;
     if (((sstride | dstride | nc | c0 | C_ln) & 3) == 0) {
         const int n4 = n >> 2, C4 = nc >> 2;
         const bool full = (c0 == 0 && nc == C_ln);   // gamma/beta contiguous over the whole image
@@ -130,9 +151,8 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
                 f4 x = *reinterpret_cast<const f4*>(src + p * sstride + c);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    float t = lrelu_(x[j]);
-                    if (ln) t = (t - mu) * rstd * gv[u][j] + bv[u][j];
-                    x[j] = t;
+                    const float t = lrelu_(x[j]);
+                    x[j] = ln ? fmaf(fmaf(t, rstd, nmr), gv[u][j], bv[u][j]) : t;
                 }
                 *reinterpret_cast<f4*>(dst + p * dstride + c) = x;
             }
@@ -161,29 +181,8 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
         for (int u = 0; u < US; u++) {
             const int e = base + u * NT + threadIdx.x;
             if (e >= n) continue;
-            float x = lrelu_(xv[u]);
-            if (ln) x = (x - mu) * rstd * gv[u] + bv[u];
-            dst[pp[u] * dstride + c0 + cc[u]] = x;
-        }
-    }
-}
-
-// Copy a pre-packed weight image (n floats, n % 4 == 0) global -> LDS, 4 float4 in flight per thread.
-__device__ __forceinline__ void stage_w(const float* __restrict__ src, int n, float* dst) {
-    const int n4 = n >> 2;
-    const f4* s4 = reinterpret_cast<const f4*>(src);
-    f4* d4 = reinterpret_cast<f4*>(dst);
-    for (int base = 0; base < n4; base += NT * 4) {
-        f4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = base + u * NT + (int)threadIdx.x;
-            v[u] = i < n4 ? s4[i] : f4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = base + u * NT + (int)threadIdx.x;
-            if (i < n4) d4[i] = v[u];
+            const float t = lrelu_(xv[u]);
+            dst[pp[u] * dstride + c0 + cc[u]] = ln ? fmaf(fmaf(t, rstd, nmr), gv[u], bv[u]) : t;
         }
     }
 }
@@ -216,108 +215,62 @@ __device__ __forceinline__ void wpf_store(const WPre& w, float* dst, const float
     for (int i = WPF * NT + (int)threadIdx.x; i < w.n4; i += NT) d4[i] = s4[i];
 }
 
-__device__ __forceinline__ int ns_of(int cout) {
-    int ns = (cout + 15) / 16 * 16;
-    if (ns % 32 == 0) ns += 16;
-    return ns;
-}
-
-// out[p][oc0 + n] = bias[n] + (res ? res[p][n] : 0) + sum_k A[p][k] B[k][n], k over
-// KS*KS*cin taps x channels of `in` (LDS, channels [ic0, ic0+cin), dilation d, zero padded).
-// MFMA 16x16x4 f32; each wave takes 16-pixel subtiles wave, wave+NW, ...
-template <int KS, int NR>
-__device__ __forceinline__ void conv_lds(const float* in, int istride, int ic0, int cin, int d, int H, int W,
-                                         const float* wl, int Kpad, int NS, const int* ktab, float* out,
-                                         int ostride, int oc0, int cout, const float* __restrict__ bias,
-                                         bool residual) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i16 = lane & 15, kq = lane >> 4;
-    const int HW = H * W;
-    const int nsub = (HW + 15) >> 4;
+// ---------------------------------------------------------------------------------------------
+// convolutions from LDS (MFMA v_mfma_f32_16x16x4f32). Every conv takes two 16-pixel subtiles per
+// wave and pass (they share the B reads); the epilogue adds bias (+ residual), stores, and
+// (slots != null) accumulates the LN statistics of LeakyReLU(out).
+// ---------------------------------------------------------------------------------------------
+template <int NR>
+struct Epi {
     float bz[NR];
-#pragma unroll
-    for (int n = 0; n < NR; n++) {
-        const int ch = n * 16 + i16;
-        bz[n] = ch < cout ? bias[ch] : 0.f;
-    }
-    for (int s = wave; s < nsub; s += NW) {
-        const int p = s * 16 + i16;
-        const bool pv = p < HW;
-        const int pr = pv ? p / W : 0, pc = pv ? p - (p / W) * W : 0;
-        f4 acc[NR];
-#pragma unroll
-        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-        for (int k0 = 0; k0 < Kpad; k0 += 4) {
-            const int k = k0 + kq;
-            float av;
-            if (KS == 1) {
-                av = (pv && k < cin) ? in[p * istride + ic0 + k] : 0.f;
-            } else {
-                const int t = ktab[k];              // packed (dr+16, dc+16, c) or -1
-                const int c = t & 0xffff;
-                const int dr = ((t >> 24) & 0xff) - 16, dc = ((t >> 16) & 0xff) - 16;
-                const int rr = pr + dr, cc = pc + dc;
-                const bool ok = pv && t >= 0 && rr >= 0 && rr < H && cc >= 0 && cc < W;
-                av = ok ? in[(rr * W + cc) * istride + ic0 + c] : 0.f;
-            }
-            const float* wrow = wl + k * NS + i16;
-#pragma unroll
-            for (int n = 0; n < NR; n++)
-                acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wrow[n * 16], acc[n], 0, 0, 0);
-        }
+    bool chv[NR];
+    __device__ __forceinline__ void init(const float* __restrict__ bias, int cout) {
+        const int i16 = threadIdx.x & 15;
 #pragma unroll
         for (int n = 0; n < NR; n++) {
             const int ch = n * 16 + i16;
-            if (ch >= cout) continue;
+            chv[n] = ch < cout;
+            bz[n] = chv[n] ? bias[ch] : 0.f;
+        }
+    }
+    // write subtile sb of acc; out points at channel oc0 of pixel 0
+    __device__ __forceinline__ void store(const f4 (&acc)[NR], int sb, int HW, float* out, int ostride, bool residual,
+                                          bool stats, LStat& st) {
+        const int i16 = threadIdx.x & 15, kq = (threadIdx.x & 63) >> 4;
+#pragma unroll
+        for (int n = 0; n < NR; n++) {
+            if (!chv[n]) continue;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int q = s * 16 + kq * 4 + r;
+                const int q = sb * 16 + kq * 4 + r;
                 if (q >= HW) continue;
+                float* o = out + q * ostride + n * 16 + i16;
                 float v = acc[n][r] + bz[n];
-                float* o = out + q * ostride + oc0 + ch;
                 if (residual) v += *o;
                 *o = v;
+                if (stats) lst_add(st, v);
             }
         }
     }
-}
+};
 
-template <int KS>
-__device__ __forceinline__ void conv_lds_any(const float* in, int istride, int ic0, int cin, int d, int H, int W,
-                                             const float* wl, int Kpad, int NS, const int* ktab, float* out,
-                                             int ostride, int oc0, int cout, const float* bias, bool residual) {
-    const int nr = (cout + 15) / 16;
-    if (nr == 1)
-        conv_lds<KS, 1>(in, istride, ic0, cin, d, H, W, wl, Kpad, NS, ktab, out, ostride, oc0, cout, bias, residual);
-    else if (nr == 2)
-        conv_lds<KS, 2>(in, istride, ic0, cin, d, H, W, wl, Kpad, NS, ktab, out, ostride, oc0, cout, bias, residual);
-    else if (nr == 3)
-        conv_lds<KS, 3>(in, istride, ic0, cin, d, H, W, wl, Kpad, NS, ktab, out, ostride, oc0, cout, bias, residual);
-    else
-        conv_lds<KS, 4>(in, istride, ic0, cin, d, H, W, wl, Kpad, NS, ktab, out, ostride, oc0, cout, bias, residual);
-}
-
-// 1x1 conv from an LDS buffer with pixel stride S == 8 (mod 16) (conflict-free ds_read_b128 of
-// 4 channels per lane) against the pre-packed PK_1X1 image wl ([g][q][j][s]); K permuted so lane
-// (i, q) holds channels 16g + 4q + s at k-step s. out[p][oc0 + n] = bias + (+= if residual) A.B
+// 1x1 conv: A = in[p][0..cin) (pixel stride == 8 mod 16), PK_1X1 image wl ([g][q][j][s], lane
+// (i, q) holds channels 16g + 4q + s at k-step s); out[p][n] (+)= bias + A.B
 template <int NR>
-__device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl,
-                                          float* out, int ostride, int cout, const float* __restrict__ bias,
-                                          bool residual) {
+__device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl, float* out,
+                                          int ostride, int cout, const float* __restrict__ bias, bool residual,
+                                          double* slots) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int nsub = (HW + 15) >> 4;
     const int G = (cin + 15) >> 4;
     constexpr int NSJ = 16 * NR;
-    float bz[NR];
-#pragma unroll
-    for (int n = 0; n < NR; n++) {
-        const int ch = n * 16 + i16;
-        bz[n] = ch < cout ? bias[ch] : 0.f;
-    }
+    Epi<NR> ep;
+    ep.init(bias, cout);
+    LStat st;
+    lst_reset(st);
+    const bool stats = slots != nullptr;
     for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
-        // two subtiles per pass (s0, s0 + NW) share the B reads
         const int s1 = s0 + NW;
         const bool v1 = s1 < nsub;
         const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
@@ -346,151 +299,216 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
 #pragma unroll
             for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
 #pragma unroll
-            for (int st = 0; st < 4; st++)
+            for (int s = 0; s < 4; s++)
 #pragma unroll
                 for (int n = 0; n < NR; n++) {
-                    acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], bq[n][st], acc0[n], 0, 0, 0);
-                    acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], bq[n][st], acc1[n], 0, 0, 0);
+                    acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], bq[n][s], acc0[n], 0, 0, 0);
+                    acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bq[n][s], acc1[n], 0, 0, 0);
                 }
         }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int sb = h ? s1 : s0;
-            if (h && !v1) break;
-#pragma unroll
-            for (int n = 0; n < NR; n++) {
-                const int ch = n * 16 + i16;
-                if (ch >= cout) continue;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int q = sb * 16 + kq * 4 + r;
-                    if (q >= HW) continue;
-                    float v = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
-                    float* o = out + q * ostride + ch;
-                    if (residual) v += *o;
-                    *o = v;
-                }
-            }
-        }
+        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        ep.store(acc0, s0, HW, out, ostride, residual, stats, st);
+        if (v1) ep.store(acc1, s1, HW, out, ostride, residual, stats, st);
+    }
+    if (stats) lst_flush(st, slots);
+}
+
+__device__ __forceinline__ void conv1_any(const float* in, int istride, int cin, int HW, const float* wl, float* out,
+                                          int ostride, int cout, const float* bias, bool residual, double* slots) {
+    switch ((cout + 15) / 16) {
+        case 1: conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        case 2: conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        case 3: conv1_lds<3>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        case 4: conv1_lds<4>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        default: conv1_lds<5>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
     }
 }
 
-__device__ __forceinline__ void conv1_lds_any(const float* in, int istride, int cin, int HW, const float* wl,
-                                              float* out, int ostride, int cout, const float* bias, bool residual) {
-    const int nr = (cout + 15) / 16;
-    if (nr == 1)
-        conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
-    else if (nr == 2)
-        conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
-    else if (nr == 3)
-        conv1_lds<3>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
-    else
-        conv1_lds<4>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual);
+// quad table of a PK_Q4 conv: entry qd = tap*(cin/4) + cq -> packed (dr+32 | dc+32 << 6 | c << 12),
+// c = ic0 + 4cq; -1 for the padding quads of the last group
+__device__ __forceinline__ void build_qtab(int* qt, int cin, int ic0, int d) {
+    const int cpq = cin >> 2, nq = 9 * cpq, nq4 = (nq + 3) & ~3;
+    for (int qd = threadIdx.x; qd < nq4; qd += NT) {
+        int t = -1;
+        if (qd < nq) {
+            const int tap = qd / cpq, cq = qd - tap * cpq;
+            const int dr = (tap / 3 - 1) * d, dc = (tap % 3 - 1) * d;
+            t = (dr + 32) | ((dc + 32) << 6) | ((ic0 + 4 * cq) << 12);
+        }
+        qt[qd] = t;
+    }
 }
 
-// 3x3 dilation-d conv from an LDS buffer (pixel stride == 8 mod 16, cin % 4 == 0) against the
-// PK_T9 image ([tap][g][q][j][s]): per tap and 16-channel group each lane reads the channel
-// quad 16g+4q.. of its shifted pixel with one ds_read_b128 (zero outside the image); no tap
-// table, 4*NR MFMAs per read. Two subtiles per pass share the B reads.
+// 3x3 dilated conv, PK_Q4: per group g each lane reads one channel quad (tap, cq) of its shifted
+// pixel with a ds_read_b128 (zero outside the image) -> 4*NR MFMAs per subtile.
 template <int NR>
-__device__ __forceinline__ void conv3_t9_lds(const float* in, int istride, int ic0, int cin, int d, int H, int W,
-                                             const float* wl, float* out, int ostride, int oc0, int cout,
-                                             const float* __restrict__ bias) {
+__device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, int H, int W, const float* wl,
+                                           const int* qt, float* out, int ostride, int cout,
+                                           const float* __restrict__ bias, double* slots) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
     const int nsub = (HW + 15) >> 4;
-    const int G = (cin + 15) >> 4;
     constexpr int NSJ = 16 * NR;
-    float bz[NR];
-#pragma unroll
-    for (int n = 0; n < NR; n++) {
-        const int ch = n * 16 + i16;
-        bz[n] = ch < cout ? bias[ch] : 0.f;
-    }
+    Epi<NR> ep;
+    ep.init(bias, cout);
+    LStat st;
+    lst_reset(st);
+    const bool stats = slots != nullptr;
     for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
         const int s1 = s0 + NW;
         const bool v1 = s1 < nsub;
         const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
         const bool pva = pa < HW, pvb = v1 && pb < HW;
-        const int ra = pva ? pa / W : 0, ca = pva ? pa - ra * W : 0;
-        const int rb = pvb ? pb / W : 0, cb = pvb ? pb - rb * W : 0;
+        const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
+        const int rb = pvb ? pb / W : -4096, cb = pvb ? pb - (pb / W) * W : -4096;
         f4 acc0[NR], acc1[NR];
 #pragma unroll
         for (int n = 0; n < NR; n++) {
             acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
             acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
         }
-#pragma unroll 1
-        for (int tap = 0; tap < 9; tap++) {
-            const int dr = (tap / 3 - 1) * d, dc = (tap % 3 - 1) * d;
+        for (int g = 0; g < G; g++) {
+            const int t = qt[4 * g + kq];
+            const int dr = (t & 63) - 32, dc = ((t >> 6) & 63) - 32, c = t >> 12;
             const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
-            const bool oka = pva && ya >= 0 && ya < H && xa >= 0 && xa < W;
-            const bool okb = pvb && yb >= 0 && yb < H && xb >= 0 && xb < W;
-            const float* pa_ = in + (oka ? (ya * W + xa) : 0) * istride + ic0;
-            const float* pb_ = in + (okb ? (yb * W + xb) : 0) * istride + ic0;
-            for (int g = 0; g < G; g++) {
-                const int c0 = 16 * g + 4 * kq;
-                const bool cv = c0 < cin;
-                f4 a0 = (oka && cv) ? *reinterpret_cast<const f4*>(pa_ + c0) : f4{0.f, 0.f, 0.f, 0.f};
-                f4 a1 = (okb && cv) ? *reinterpret_cast<const f4*>(pb_ + c0) : f4{0.f, 0.f, 0.f, 0.f};
-                const float* brow = wl + (((tap * G + g) * 4 + kq) * NSJ + i16) * 4;
-                f4 bq[NR];
+            const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
+            const bool okb = t >= 0 && (unsigned)yb < (unsigned)H && (unsigned)xb < (unsigned)W;
+            const f4 a0 = oka ? *reinterpret_cast<const f4*>(in + (ya * W + xa) * istride + c) : f4{0.f, 0.f, 0.f, 0.f};
+            const f4 a1 = okb ? *reinterpret_cast<const f4*>(in + (yb * W + xb) * istride + c) : f4{0.f, 0.f, 0.f, 0.f};
+            const float* brow = wl + ((g * 4 + kq) * NSJ + i16) * 4;
+            f4 bq[NR];
 #pragma unroll
-                for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
 #pragma unroll
-                for (int st = 0; st < 4; st++)
+            for (int s = 0; s < 4; s++)
 #pragma unroll
-                    for (int n = 0; n < NR; n++) {
-                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[st], bq[n][st], acc0[n], 0, 0, 0);
-                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], bq[n][st], acc1[n], 0, 0, 0);
-                    }
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int sb = h ? s1 : s0;
-            if (h && !v1) break;
-#pragma unroll
-            for (int n = 0; n < NR; n++) {
-                const int ch = n * 16 + i16;
-                if (ch >= cout) continue;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int q = sb * 16 + kq * 4 + r;
-                    if (q >= HW) continue;
-                    out[q * ostride + oc0 + ch] = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
+                for (int n = 0; n < NR; n++) {
+                    acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], bq[n][s], acc0[n], 0, 0, 0);
+                    acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bq[n][s], acc1[n], 0, 0, 0);
                 }
-            }
         }
+        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        ep.store(acc0, s0, HW, out, ostride, false, stats, st);
+        if (v1) ep.store(acc1, s1, HW, out, ostride, false, stats, st);
+    }
+    if (stats) lst_flush(st, slots);
+}
+
+__device__ __forceinline__ void conv3q_any(const float* in, int istride, int G, int H, int W, const float* wl,
+                                           const int* qt, float* out, int ostride, int cout, const float* bias,
+                                           double* slots) {
+    switch ((cout + 15) / 16) {
+        case 1: conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
+        case 2: conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
+        case 3: conv3q_lds<3>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
+        default: conv3q_lds<4>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
     }
 }
 
-__device__ __forceinline__ void conv3_t9_any(const float* in, int istride, int ic0, int cin, int d, int H, int W,
-                                             const float* wl, float* out, int ostride, int oc0, int cout,
-                                             const float* bias) {
-    const int nr = (cout + 15) / 16;
-    if (nr == 1)
-        conv3_t9_lds<1>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
-    else if (nr == 2)
-        conv3_t9_lds<2>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
-    else if (nr == 3)
-        conv3_t9_lds<3>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
-    else
-        conv3_t9_lds<4>(in, istride, ic0, cin, d, H, W, wl, out, ostride, oc0, cout, bias);
-}
-
-// k -> (dr, dc, c) table of a 3x3 dilation-d conv over cin channels, -1 beyond K
-__device__ __forceinline__ void build_ktab(int* ktab, int cin, int d, int Kpad) {
+// k -> (dr, dc, c) table of a PK_KN conv over cin channels from channel ic0; -1 beyond K
+__device__ __forceinline__ void build_ktab(int* ktab, int cin, int ic0, int d, int Kpad) {
     for (int k = threadIdx.x; k < Kpad; k += NT) {
         int t = -1;
         if (k < 9 * cin) {
             const int tap = k / cin, c = k - tap * cin;
-            const int kh = tap / 3, kw = tap - kh * 3;
-            t = (((kh - 1) * d + 16) << 24) | (((kw - 1) * d + 16) << 16) | c;
+            t = (((tap / 3 - 1) * d + 32) << 24) | (((tap % 3 - 1) * d + 32) << 16) | (ic0 + c);
         }
         ktab[k] = t;
     }
+}
+
+// 3x3 dilated conv, PK_KN (any cin): scalar A reads through the tap table, K = 9*cin padded to 4
+template <int NR>
+__device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, int W, const float* wl, int Kpad,
+                                           int NS, const int* ktab, float* out, int ostride, int cout,
+                                           const float* __restrict__ bias, double* slots) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    const int HW = H * W;
+    const int nsub = (HW + 15) >> 4;
+    Epi<NR> ep;
+    ep.init(bias, cout);
+    LStat st;
+    lst_reset(st);
+    const bool stats = slots != nullptr;
+    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+        const int s1 = s0 + NW;
+        const bool v1 = s1 < nsub;
+        const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
+        const bool pva = pa < HW, pvb = v1 && pb < HW;
+        const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
+        const int rb = pvb ? pb / W : -4096, cb = pvb ? pb - (pb / W) * W : -4096;
+        f4 acc0[NR], acc1[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) {
+            acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
+            acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll 2
+        for (int k0 = 0; k0 < Kpad; k0 += 4) {
+            const int t = ktab[k0 + kq];
+            const int c = t & 0xffff;
+            const int dr = ((t >> 24) & 0xff) - 32, dc = ((t >> 16) & 0xff) - 32;
+            const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
+            const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
+            const bool okb = t >= 0 && (unsigned)yb < (unsigned)H && (unsigned)xb < (unsigned)W;
+            const float a0 = oka ? in[(ya * W + xa) * istride + c] : 0.f;
+            const float a1 = okb ? in[(yb * W + xb) * istride + c] : 0.f;
+            const float* wrow = wl + (k0 + kq) * NS + i16;
+#pragma unroll
+            for (int n = 0; n < NR; n++) {
+                const float b = wrow[n * 16];
+                acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc0[n], 0, 0, 0);
+                acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc1[n], 0, 0, 0);
+            }
+        }
+        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        ep.store(acc0, s0, HW, out, ostride, false, stats, st);
+        if (v1) ep.store(acc1, s1, HW, out, ostride, false, stats, st);
+    }
+    if (stats) lst_flush(st, slots);
+}
+
+__device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, int W, const float* wl, int Kpad,
+                                           int NS, const int* ktab, float* out, int ostride, int cout,
+                                           const float* bias, double* slots) {
+    switch ((cout + 15) / 16) {
+        case 1: conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
+        case 2: conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
+        case 3: conv3k_lds<3>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
+        default: conv3k_lds<4>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
+    }
+}
+
+// build the table a 3x3 conv of format fmt needs (caller barriers before the conv)
+__device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin, int ic0, int d) {
+    if (cv.fmt == PK_Q4)
+        build_qtab(tab, cin, ic0, d);
+    else
+        build_ktab(tab, cin, ic0, d, cv.kpad);
+}
+__device__ __forceinline__ void conv3_run(const LdsConv& cv, const float* in, int istride, int H, int W,
+                                          const float* wl, const int* tab, float* out, int ostride, int cout,
+                                          const float* bias, double* slots) {
+    if (cv.fmt == PK_Q4)
+        conv3q_any(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, slots);
+    else
+        conv3k_any(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, slots);
+}
+
+// position in u of element (pixel p, channel c) of the compressed u1c (mask compress, :720-759)
+__device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int D) {
+    const int pr = p / wc, pc = p - pr * wc;
+    if (m < 2) {
+        const int half = c >= D ? 1 : 0;
+        const int ch = c - half * D;
+        const int dr = half;
+        const int dcol = (m == 0) ? half : 1 - half;
+        return ((2 * pr + dr) * W + (2 * pc + dcol)) * D + ch;
+    }
+    const int ch = (m == 2) ? 2 * c : 2 * c + 1;
+    return (pr * W + pc) * D + ch;
 }
 
 }  // namespace
@@ -506,50 +524,25 @@ __device__ long long g_stamps[256];
         }                                                                                    \
     } while (0)
 
-__device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int D) {
-    const int pr = p / wc, pc = p - pr * wc;
-    if (m < 2) {
-        const int half = c >= D ? 1 : 0;
-        const int ch = c - half * D;
-        const int dr = half;
-        const int dcol = (m == 0) ? half : 1 - half;
-        return ((2 * pr + dr) * W + (2 * pc + dcol)) * D + ch;
-    }
-    const int ch = (m == 2) ? 2 * c : 2 * c + 1;
-    return (pr * W + pc) * D + ch;
-}
-
 template <bool STAMPS>
 __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int img = blockIdx.x, net = blockIdx.y;
     const int H = a.hc, W = a.wc, HW = H * W;
     const int nk = a.nk, gc = a.gc;
-    const int SY = a.sy, S1 = a.s1, S2 = a.s2;   // S2 covers max(gc, nk, dc1, dc2) channels
+    const int SY = a.sy, S1 = a.s1, S2 = a.s2, SU = a.su;   // S2 covers max(gc, nk, dc2) channels
+    double* slots = reinterpret_cast<double*>(smem);         // NW x (n, mean, M2)
     float* Y = reinterpret_cast<float*>(smem + a.off_y);
     float* T1 = reinterpret_cast<float*>(smem + a.off_t1);
     float* T2 = reinterpret_cast<float*>(smem + a.off_t2);
     float* WL = reinterpret_cast<float*>(smem + a.off_w);
     int* KT = reinterpret_cast<int*>(smem + a.off_k);
-    double* red = reinterpret_cast<double*>(smem);   // 2*NW doubles (<= 256 bytes)
     const float* P = a.params;
     const float* X = a.aux;
     const int* off = a.offs + net * a.offs_per_net;   // see NetLdsArgs
     const bool ln = a.ln != 0;
+    double* sl = ln ? slots : nullptr;
     float mu = 0.f, rstd = 1.f;
-
-    // packed-image sizes of every conv of this net (floats)
-    const int r16 = ((nk + 15) / 16) * 16;                 // G*16 for cin = nk
-    const int sz_ci = a.ci_t9 ? 9 * ((a.dc1 + 15) / 16) * 16 * r16 : ((9 * a.dc1 + 3) / 4 * 4) * ns_of(nk);
-    const int sz_ca = r16 * r16;                           // PK_1X1 nk -> nk
-    const int sz_cb = ((gc + 15) / 16) * 16 * r16;         // PK_1X1 gc -> nk
-    const int co_nr = (9 * a.dc2 + 15) / 16;
-    const int sz_co = a.co_tap ? r16 * 16 * co_nr
-                      : a.co_t9 ? 9 * r16 * ((a.dc2 + 15) / 16) * 16 : ((9 * nk + 3) / 4 * 4) * ns_of(a.dc2);
-    auto sz_gc = [&](int bi) {
-        return a.br_t9[bi] ? 9 * ((a.br_cin[bi] + 15) / 16) * 16 * ((a.br_cout[bi] + 15) / 16) * 16
-                           : ((9 * a.br_cin[bi] + 3) / 4 * 4) * ns_of(a.br_cout[bi]);
-    };
     const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
     const int per_rb = 10 + 2 * a.nbr;
     auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
@@ -558,9 +551,8 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
 
     int sti = 0;
     STAMP(sti++);
-    // gather u1c (mask compress, :720-759) straight from u into the T2 region (stride SU)
-    wpf_load(pf, X + off[0], sz_ci);
-    const int SU = a.su;
+    wpf_load(pf, X + off[0], a.ci.size);
+    // gather u1c (mask compress) into T2 (stride SU)
     {
         const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
         const int n = HW * a.dc1;
@@ -569,98 +561,89 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             T2[p * SU + c] = ub[mask_pos_(a.mask, p, c, W, a.W, a.D)];
         }
     }
-    // conv_in (3x3, dc1 -> nk), PK_KN
+    // conv_in (3x3, dc1 -> nk) -> Y, LN stats of Y
     {
-        const int Kpad = (9 * a.dc1 + 3) / 4 * 4, NS = ns_of(nk);
-        if (!a.ci_t9) build_ktab(KT, a.dc1, 1, Kpad);
+        conv3_table(a.ci, KT, a.dc1, 0, 1);
         wpf_store(pf, WL, X + off[0]);
+        lst_zero(slots);
         __syncthreads();
         if (a.R > 0)
-            wpf_load(pf, X + rbo(0)[2], sz_ca);
+            wpf_load(pf, X + rbo(0)[2], a.ca.size);
         else
-            wpf_load(pf, X + oend[2], sz_co);
+            wpf_load(pf, X + oend[2], a.co.size);
         STAMP(sti++);
-        if (a.ci_t9)
-            conv3_t9_any(T2, SU, 0, a.dc1, 1, H, W, WL, Y, SY, 0, nk, X + off[1]);
-        else
-            conv_lds_any<3>(T2, SU, 0, a.dc1, 1, H, W, WL, Kpad, NS, KT, Y, SY, 0, nk, X + off[1], false);
+        conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, X + off[1], sl);
         __syncthreads();
         STAMP(sti++);
     }
     for (int r = 0; r < a.R; r++) {
         const int* o = rbo(r);
-        // LN1(LReLU(y)) -> T2 (scratch), conv_a (1x1 nk->nk) -> T1
-        if (ln) ln_stats(Y, SY, HW, nk, red, mu, rstd);
-        STAMP(sti++);
+        // LN1(LReLU(y)) -> T2, conv_a (1x1 nk->nk) -> T1 (+ LN2 stats)
+        if (ln) lst_final(slots, mu, rstd);
         ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
-        STAMP(sti++);
         wpf_store(pf, WL, X + o[2]);
-        __syncthreads();
-        wpf_load(pf, X + o[10], sz_gc(0));
+        __syncthreads();   // every wave has read the Y slots; T2 and W are complete
+        lst_zero(slots);
+        wpf_load(pf, X + o[10], a.gcv[0].size);
         STAMP(sti++);
-        conv1_lds_any(T2, S2, nk, HW, WL, T1, S1, nk, X + o[3], false);
+        conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, X + o[3], false, sl);
         __syncthreads();
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
-        if (ln) ln_stats(T1, S1, HW, nk, red, mu, rstd);
+        if (ln) lst_final(slots, mu, rstd);
         for (int wi = 0; wi < a.nwin; wi++)
             ln_apply(T1, S1, T1, S1, HW, a.win_off[wi], a.win_len[wi], nk, mu, rstd, ln ? P + o[4] : nullptr,
                      ln ? P + o[5] : nullptr, ln);
-        // grouped dilated branches -> T2[:, out_off : out_off + cout]
+        // grouped dilated branches -> T2[:, out_off : out_off + cout] (+ LN3 stats over all of them)
         for (int bi = 0; bi < a.nbr; bi++) {
-            const int cin = a.br_cin[bi], cout = a.br_cout[bi], d = a.br_dil[bi];
-            const int Kpad = (9 * cin + 3) / 4 * 4, NS = ns_of(cout);
-            __syncthreads();
-            if (!a.br_t9[bi]) build_ktab(KT, cin, d, Kpad);
+            const LdsConv& cv = a.gcv[bi];
+            __syncthreads();   // previous branch (or LN2 apply + slot reads) retired
+            if (bi == 0) lst_zero(slots);
+            conv3_table(cv, KT, a.br_cin[bi], a.br_cin_off[bi], a.br_dil[bi]);
             wpf_store(pf, WL, X + o[10 + 2 * bi]);
             __syncthreads();
             if (bi + 1 < a.nbr)
-                wpf_load(pf, X + o[10 + 2 * (bi + 1)], sz_gc(bi + 1));
+                wpf_load(pf, X + o[10 + 2 * (bi + 1)], a.gcv[bi + 1].size);
             else
-                wpf_load(pf, X + o[8], sz_cb);
+                wpf_load(pf, X + o[8], a.cb.size);
             STAMP(sti++);
-            if (a.br_t9[bi])
-                conv3_t9_any(T1, S1, a.br_cin_off[bi], cin, d, H, W, WL, T2, S2, a.br_out_off[bi], cout,
-                             X + o[11 + 2 * bi]);
-            else
-                conv_lds_any<3>(T1, S1, a.br_cin_off[bi], cin, d, H, W, WL, Kpad, NS, KT, T2, S2, a.br_out_off[bi],
-                                cout, X + o[11 + 2 * bi], false);
+            conv3_run(cv, T1, S1, H, W, WL, KT, T2 + a.br_out_off[bi], S2, a.br_cout[bi], X + o[11 + 2 * bi], sl);
             STAMP(sti++);
         }
         __syncthreads();
-        // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y
-        if (ln) ln_stats(T2, S2, HW, gc, red, mu, rstd);
-        STAMP(sti++);
+        // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
+        if (ln) lst_final(slots, mu, rstd);
         ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
-        STAMP(sti++);
         wpf_store(pf, WL, X + o[8]);
         __syncthreads();
+        lst_zero(slots);
         if (r + 1 < a.R)
-            wpf_load(pf, X + rbo(r + 1)[2], sz_ca);
+            wpf_load(pf, X + rbo(r + 1)[2], a.ca.size);
         else
-            wpf_load(pf, X + oend[2], sz_co);
+            wpf_load(pf, X + oend[2], a.co.size);
         STAMP(sti++);
-        conv1_lds_any(T2, S2, gc, HW, WL, Y, SY, nk, X + o[9], true);
+        conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, X + o[9], true, sl);
         __syncthreads();
         STAMP(sti++);
     }
     // LN_out(LReLU(y)) in place, conv_out (3x3 nk -> dc2) -> global
     {
         const int* o = oend;
-        if (ln) ln_stats(Y, SY, HW, nk, red, mu, rstd);
+        if (ln) lst_final(slots, mu, rstd);
         ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         STAMP(sti++);
         float* dst = a.so[net] + (size_t)img * HW * a.dc2;
         const float* __restrict__ bias = X + o[3];
-        if (a.co_tap) {
+        if (a.co.fmt == PK_TAP) {
             // tap-decomposed: C[p][(tap, o)] = sum_c y[p][c] W[tap][c][o] (1x1 GEMM, scratch over T1..T2),
             // out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]
             const int ncol = 9 * a.dc2;
+            const int co_nr = (ncol + 15) / 16;
             const int CS = 16 * co_nr + 1;
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
             __syncthreads();
-            conv1_lds_any(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false);
+            conv1_any(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, nullptr);
             __syncthreads();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -681,14 +664,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                 dst[e] = acc;
             }
         } else {
-            const int Kpad = (9 * nk + 3) / 4 * 4, NS = ns_of(a.dc2);
-            if (!a.co_t9) build_ktab(KT, nk, 1, Kpad);
+            conv3_table(a.co, KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
             __syncthreads();
-            if (a.co_t9)
-                conv3_t9_any(Y, SY, 0, nk, 1, H, W, WL, T2, S2, 0, a.dc2, bias);
-            else
-                conv_lds_any<3>(Y, SY, 0, nk, 1, H, W, WL, Kpad, NS, KT, T2, S2, 0, a.dc2, bias, false);
+            conv3_run(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, nullptr);
             __syncthreads();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {

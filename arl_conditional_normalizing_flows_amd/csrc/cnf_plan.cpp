@@ -54,10 +54,10 @@ std::vector<int> s2d(const std::vector<int>& in, int h, int w, int c) {
 
 // floats of a packed conv image and its K extent (see PackedConv); must match the pack lambda
 void packed_dims(int fmt, int ks, int cin, int cout, int64_t& size, int& kpad) {
-    if (fmt == PK_T9) {
-        const int G = (cin + 15) / 16;
-        kpad = 9 * G * 16;
-        size = 9LL * G * 16 * 16 * ((cout + 15) / 16);
+    if (fmt == PK_Q4) {
+        const int G = (9 * (cin / 4) + 3) / 4;   // groups of 4 channel quads
+        kpad = G * 16;
+        size = (int64_t)G * 16 * 16 * ((cout + 15) / 16);
     } else if (fmt == PK_KN) {
         int ns = 16 * ((cout + 15) / 16);
         if (ns % 32 == 0) ns += 16;
@@ -91,7 +91,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     g.sy = stride8(c.nk);
     g.s1 = stride8(c.nk);
     g.s2 = stride8(std::max(std::max(c.gc, c.nk), c.dc2));
-    g.su = ci_fmt == PK_T9 ? stride8(c.dc1) : stride2(c.dc1);
+    g.su = ci_fmt == PK_Q4 ? stride8(c.dc1) : stride2(c.dc1);
     g.s2r = std::max(g.s2, g.su);
     if (co_fmt == PK_TAP)   // tap-decomposed conv_out scratch (stride 16*nr+1) spans T1..T2
         g.s2r = std::max(g.s2r, 16 * ((9 * c.dc2 + 15) / 16) + 1 - g.s1);
@@ -100,7 +100,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     auto acc = [&](int fmt, int ks, int cin, int cout) {
         packed_dims(fmt, ks, cin, cout, sz, kp);
         wmax = std::max(wmax, sz);
-        if (fmt == PK_KN) kmax = std::max(kmax, kp);
+        if (fmt == PK_KN || fmt == PK_Q4) kmax = std::max(kmax, fmt == PK_Q4 ? kp / 4 : kp);   // tap / quad table
     };
     acc(ci_fmt, 3, c.dc1, c.nk);
     acc(co_fmt, 3, c.nk, c.dc2);
@@ -336,8 +336,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
         }
 
         // conv formats and which layers run the whole-net-in-LDS kernel (CNF_NETLDS=0 disables):
-        // prefer PK_T9 for its 3x3 convs (channel-quad reads, no tap table), fall back to PK_KN
-        // when the T9 images do not fit the 160 KiB LDS image, else stream the layer.
+        // prefer PK_Q4 for its 3x3 convs (channel-quad ds_read_b128 A reads), fall back to PK_KN
+        // when the Q4 images do not fit the 160 KiB LDS image, else stream the layer.
         {
             bool allow = true;
             if (const char* e = std::getenv("CNF_NETLDS")) allow = std::atoi(e) != 0;
@@ -348,10 +348,11 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.gc_fmt.assign(c.br.size(), PK_KN);
                 c.use_lds = false;
                 if (!allow) continue;
-                const int ci9 = c.dc1 % 4 == 0 ? PK_T9 : PK_KN;
-                const int co9 = tapco == PK_TAP ? PK_TAP : (c.nk % 4 == 0 ? PK_T9 : PK_KN);
+                const int ci9 = c.dc1 % 4 == 0 ? PK_Q4 : PK_KN;
+                // k_net_lds runs the tap-decomposed conv_out up to 80 tap columns (NR = 5)
+                const int co9 = 9 * c.dc2 <= 80 ? PK_TAP : (c.nk % 4 == 0 ? PK_Q4 : PK_KN);
                 std::vector<int> gc9;
-                for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_T9 : PK_KN);
+                for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_Q4 : PK_KN);
                 NetLdsGeom g;
                 if (netlds_geometry(c, ci9, co9, gc9, g)) {
                     c.ci_fmt = ci9;
@@ -372,20 +373,27 @@ Plan* build_plan(const cnf_flow_desc* d) {
             pc.cin = cin;
             pc.cout = cout;
             pc.w = p.n_aux;
-            if (fmt == PK_T9) {
+            if (fmt == PK_Q4) {
+                // K = 9*cin as a list of channel quads qd = tap*(cin/4) + cq (k = tap*cin + 4cq + s);
+                // image [g][q][j][s] with qd = 4g + q
+                const int cpq = cin / 4, nq = 9 * cpq;
                 pc.nr = (cout + 15) / 16;
                 pc.ns = 16 * pc.nr;
-                pc.G = (cin + 15) / 16;
-                pc.kpad = 9 * pc.G * 16;
-                pc.size = 9LL * pc.G * 16 * pc.ns;
-                for (int tap = 0; tap < 9; tap++)
-                    for (int g = 0; g < pc.G; g++)
-                        for (int q = 0; q < 4; q++)
-                            for (int j = 0; j < pc.ns; j++)
-                                for (int s4 = 0; s4 < 4; s4++) {
-                                    const int c2 = 16 * g + 4 * q + s4;
-                                    p.aux_map.push_back((c2 < cin && j < cout) ? src(tap * cin + c2, j) : -1);
+                pc.G = (nq + 3) / 4;
+                pc.kpad = pc.G * 16;
+                pc.size = (int64_t)pc.G * 16 * pc.ns;
+                for (int g = 0; g < pc.G; g++)
+                    for (int q = 0; q < 4; q++)
+                        for (int j = 0; j < pc.ns; j++)
+                            for (int s4 = 0; s4 < 4; s4++) {
+                                const int qd = 4 * g + q;
+                                int64_t v = -1;
+                                if (qd < nq && j < cout) {
+                                    const int tap = qd / cpq, cq = qd - tap * cpq;
+                                    v = src(tap * cin + 4 * cq + s4, j);
                                 }
+                                p.aux_map.push_back(v);
+                            }
             } else if (fmt == PK_KN) {
                 const int K = ks * ks * cin;
                 pc.nr = (cout + 15) / 16;
@@ -463,9 +471,9 @@ Plan* build_plan(const cnf_flow_desc* d) {
             }
         }
 
-        p.aux_zero = p.n_aux;   // 64 zeros (bias of bias-free GEMM stages)
-        for (int i = 0; i < 64; i++) p.aux_map.push_back(-1);
-        p.n_aux += 64;
+        p.aux_zero = p.n_aux;   // 128 zeros (bias of the bias-free tap GEMM, up to 80 columns)
+        for (int i = 0; i < 128; i++) p.aux_map.push_back(-1);
+        p.n_aux += 128;
 
         // k_net_lds offset table (params offsets for LN gamma/beta, kernel-image offsets for convs)
         require(p.n_params < (1ll << 31) && p.n_aux < (1ll << 31), "parameter image exceeds 2^31 floats");

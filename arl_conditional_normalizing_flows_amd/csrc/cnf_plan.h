@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/cnf.h"
+#include "cnf_kernels.h"
 
 namespace cnf {
 
@@ -26,8 +27,9 @@ struct Branch {
 //   PK_1X1  1x1 conv [cin][cout]: B image [g][q][j][s], element (c = 16g+4q+s, j), j < 16*nr
 //   PK_TAP  3x3 conv as tap GEMM: same image over c with columns j = tap*cout + o (9*cout <= 64)
 //   PK_KN   3x3 implicit GEMM: [kpad][ns], k = tap*cin + c, ns = 16*nr (+16 if ns % 32 == 0)
-//   PK_T9   3x3 with channel quads: [tap][g][q][j][s], element (tap, c = 16g+4q+s, j) (LDS kernel)
-enum { PK_1X1 = 0, PK_KN = 1, PK_TAP = 2, PK_T9 = 3 };
+//   PK_Q4   3x3 as a list of channel quads qd = tap*(cin/4) + cq: [g][q][j][s], qd = 4g + q,
+//           k = tap*cin + 4cq + s (cin % 4 == 0; LDS kernel: one ds_read_b128 per quad)
+// (the PK_* constants live in cnf_kernels.h, shared with the kernels)
 struct PackedConv {
     int fmt = PK_KN, cin = 0, cout = 0, nr = 0, ns = 0, G = 0, kpad = 0;
     int64_t w = -1, b = -1, size = 0;   // offsets (floats) into the kernel image; size of the weight image
@@ -128,7 +130,7 @@ struct Plan {
     std::vector<ParamTensor> params;
     int64_t n_params = 0;
     int64_t n_aux = 0;
-    int64_t aux_zero = 0;           // offset of 64 zero floats in the kernel image
+    int64_t aux_zero = 0;           // offset of 128 zero floats in the kernel image
     std::vector<int64_t> aux_map;   // kernel image: aux[i] = params[aux_map[i]] (or 0 if < 0)
     std::vector<Boundary> boundaries;
     std::vector<int> final_orig;    // last block layout -> xy position
@@ -141,6 +143,7 @@ struct Plan {
     int device = -1;
     // launch recording
     bool record = true;
+    bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     std::vector<Recorded> recorded;
 
     WsLayout layout(int B) const;

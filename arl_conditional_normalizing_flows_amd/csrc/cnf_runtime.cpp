@@ -110,6 +110,7 @@ WsLayout Plan::layout(int B) const {
         Geo g = conv_geo(c.hc, c.wc);
         parts = std::max(parts, 4 * g.tiles * (int)c.br.size());   // 4 waves per workgroup
         parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
+        parts = std::max(parts, 4 * ((c.hc * c.wc + 63) / 64));   // k_pw
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
     L.n_uv = n_uv;
@@ -215,9 +216,10 @@ static uint32_t magic_for(int d, int64_t xmax) {
     return (uint32_t)((((uint64_t)1 << 32) + (uint64_t)d - 1) / (uint64_t)d);
 }
 
-static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
-                        uint64_t store_mask = ~0ull) {
-    if (probs.empty()) return;
+// returns the LN-partial slots per image each problem writes (4 per workgroup tile)
+static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
+                       uint64_t store_mask = ~0ull) {
+    if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
     ConvArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -240,6 +242,7 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
     double flops = 0, bytes = 0;
     const double HWB = (double)h * w * E.B;
     bool vec = true;
+    int pw_nr = 0, pw_gm = 0;
     for (size_t i = 0; i < probs.size(); i++) {
         const ProbSpec& s = probs[i];
         ConvProb& q = a.p[i];
@@ -290,9 +293,12 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
             off = align_up(off + (size_t)q.Kpad * 4, 16);
         } else {
             const int G = (s.cin + 15) / 16;
+            if (off < 512) off = 512;   // k_pw keeps its per-image LN table at bytes [256, 384)
             q.lds_w_off = (int)off;
             off = align_up(off + (size_t)G * 16 * 16 * q.nr * 4, 16);
             if (s.cin % 4 || s.in_cs % 4 || s.in_off % 4) vec = false;
+            pw_nr = std::max(pw_nr, q.nr);
+            pw_gm = std::max(pw_gm, G);
         }
         lds = std::max(lds, off);
         flops += 2.0 * HWB * K * s.cout;
@@ -301,6 +307,15 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
     const int ilds = (int)lds;
+    if (pw_gm > 0) pw_gm = pw_gm <= 1 ? 1 : pw_gm <= 2 ? 2 : pw_gm <= 4 ? 4 : pw_gm <= 8 ? 8 : 0;
+    bool ln_uniform = true;
+    for (const ProbSpec& s : probs)
+        ln_uniform = ln_uniform && ((s.in_st.part != nullptr) == (probs[0].in_st.part != nullptr)) &&
+                     ((s.res != nullptr) == (probs[0].res != nullptr));
+    bool fits32 = true;   // k_pw addresses each tensor with 32-bit byte offsets (buffer resources)
+    for (const ProbSpec& s : probs)
+        fits32 = fits32 && (double)E.B * h * w * std::max(s.in_cs, s.out_cs) * 4.0 < 2147483648.0;
+    const bool pw_ok = ks == 1 && vec && pw_gm > 0 && ln_uniform && fits32 && E.p.use_pw;
     if (ks == 3) {
         const int grid_x = E.B * g.tiles;
         const int mr = g.MR;
@@ -308,6 +323,23 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
         E.record(name, flops, bytes, [mr, role, a, grid_x, ilds](void* st) {
             launch_conv(3, mr, role, a, grid_x, ilds, (hipStream_t)st);
         });
+        return 4 * g.tiles;
+    } else if (pw_ok) {
+        // k_pw: 64-pixel tiles x groups of MI images (see cnf_stream.hip)
+        const int tiles = (h * w + 63) / 64;
+        const int mi = (pw_gm <= 4 && probs[0].res == nullptr) ? 4 : 2;   // k_pw instantiations
+        a.tiles_per_img = tiles;
+        for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = 0;
+        const int grid_x = tiles * ((E.B + mi - 1) / mi);
+        const int nr = pw_nr, gm = pw_gm;
+        const bool lnf = probs[0].in_st.part != nullptr;
+        const bool resf = probs[0].res != nullptr;
+        std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
+                           std::to_string(mi) + "," + role_name(role) + ">";
+        E.record(name, flops, bytes, [nr, gm, mi, lnf, resf, a, grid_x, ilds](void* st) {
+            launch_pw(nr, gm, mi, lnf, resf, a, grid_x, ilds, (hipStream_t)st);
+        });
+        return 4 * tiles;
     } else {
         const int grid_x = E.B * g1.tiles;
         const int mr = g1.MR;
@@ -316,6 +348,7 @@ static void conv_launch(Exec& E, int ks, int role, int h, int w, const std::vect
         E.record(name, flops, bytes, [mr, vec, role, a, grid_x, ilds](void* st) {
             launch_conv1(mr, vec, role, a, grid_x, ilds, (hipStream_t)st);
         });
+        return 4 * g1.tiles;
     }
 }
 
@@ -338,6 +371,7 @@ static void convtap_launch(Exec& E, int h, int w, const std::vector<ProbSpec>& p
     double flops = 0, bytes = 0;
     const double HWB = (double)h * w * E.B;
     bool vec = true;
+    int pw_nr = 0, pw_gm = 0;
     for (size_t i = 0; i < probs.size(); i++) {
         const ProbSpec& s = probs[i];
         ConvProb& q = a.p[i];
@@ -434,10 +468,15 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     a.s1 = g.s1;
     a.s2 = g.s2;
     a.su = g.su;
-    a.co_tap = c.co_fmt == PK_TAP;
-    a.co_t9 = c.co_fmt == PK_T9;
-    a.ci_t9 = c.ci_fmt == PK_T9;
-    for (int i = 0; i < a.nbr; i++) a.br_t9[i] = c.gc_fmt[i] == PK_T9;
+    const NetParams& n0 = c.net[0];
+    auto desc = [](const PackedConv& pc) { return LdsConv{pc.fmt, (int)pc.size, pc.kpad, pc.ns}; };
+    a.ci = desc(n0.ci);
+    a.co = desc(n0.co);
+    if (!n0.rb.empty()) {
+        a.ca = desc(n0.rb[0].ca);
+        a.cb = desc(n0.rb[0].cb);
+        for (int i = 0; i < a.nbr; i++) a.gcv[i] = desc(n0.rb[0].gc[i]);
+    }
     a.off_y = g.off_y;
     a.off_t1 = g.off_t1;
     a.off_t2 = g.off_t2;
@@ -497,11 +536,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         for (int k = 0; k < 3; k++) {
             sl[n][k].part = E.at<double>(L.st_part[n][k]);
         }
-    // out_slab records how many partial slots the producing launch writes; in_slab hands that count on
-    auto out_slab = [&](int n, int k, int nparts) {
-        if (!ln) return Slab{};
-        sl[n][k].nparts = nparts;
-        return sl[n][k];
+    // a producing launch reports the partial slots it wrote per image (set_parts); in_slab hands
+    // that count on to the consumer
+    auto out_slab = [&](int n, int k, int) { return ln ? sl[n][k] : Slab{}; };
+    auto set_parts = [&](int k, int nparts) {
+        for (int n = 0; n < 2; n++) sl[n][k].nparts = nparts;
     };
     auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };
     const float* none = nullptr;
@@ -514,7 +553,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             pr.push_back(ProbSpec{u1c, c.dc1, 0, c.dc1, Slab{}, none, none, 0, X + np.ci.w, X + np.ci.b, y[n], c.nk, 0,
                                   c.nk, none, out_slab(n, 0, 4 * nt3), 0, 1});
         }
-        conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr);
+        set_parts(0, conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr));
     }
     for (int r = 0; r < c.R; r++) {
         // conv_a: LN1(LReLU(y)) -> 1x1 -> t1
@@ -529,7 +568,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             uint64_t used = 0;
             for (const Branch& b : c.br)
                 for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) used |= 1ull << ch;
-            conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used);
+            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used));
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]
         {
@@ -543,7 +582,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                           b.out_off, b.cout, none, out_slab(n, 2, 4 * nt3 * nbr), bi * nt3 * 4, b.dil});
                 }
             }
-            conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
+            set_parts(2, nbr * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr));
         }
         // conv_b: LN3(LReLU(t2)) -> 1x1 -> + shortcut -> y (in place)
         {
@@ -554,7 +593,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                       ln ? P + rb.ln3b : none, 1, X + rb.cb.w, X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n],
                                       out_slab(n, 0, 4 * nt1), 0, 1});
             }
-            conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr);
+            set_parts(0, conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr));
         }
     }
     // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b)
@@ -637,6 +676,7 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     *out = nullptr;
     CNF_TRY
     Plan* p = build_plan(desc);
+    if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     *out = new cnf_plan{p};
