@@ -518,7 +518,14 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.zero_bias = X + E.p.aux_zero;
         const int ilds = (int)nlds;
         const double fl = 2.0 * B * net_flops(c);
-        const double by = 4.0 * B * (double)c.hc * c.wc * (c.dc1 + c.dc2) * 2;
+        // algorithmic bytes: u1c in and s/t out per image and net, plus the per-element LN
+        // gamma/beta (only the branch input windows of LN2) and the conv weights once per launch
+        const double HWc = (double)c.hc * c.wc;
+        int win = 0;
+        for (int i = 0; i < na.nwin; i++) win += na.win_len[i];
+        const double ln_floats = ln ? 2.0 * HWc * (c.R * (c.nk + win + c.gc) + c.nk) : 0.0;
+        const double w_floats = net_flops(c) / (2.0 * HWc);
+        const double by = 4.0 * (B * HWc * (c.dc1 + c.dc2) * 2 + 2 * (ln_floats + w_floats));
         E.record("k_net_lds", fl, by, [na, B, ilds](void* st) { launch_net_lds(na, B, ilds, (hipStream_t)st); });
     } else {
     float* u1c = E.at<float>(L.u1c);

@@ -8,7 +8,7 @@
 A step = one cFlow.call(xy, +1) (zy + per-image log-det) + the NLL 4-sum over one batch of
 synthetic inputs already resident in HBM; with N>1 every rank processes its own batch
 (weak scaling, BASELINE configs[1] batch 64 per GPU) and the 4 NLL sums are all-reduced
-(the path's only exchange step, one RCCL all-reduce of 4 fp32). value = images processed by
+(the path's only exchange step, one RCCL all-reduce of 5 fp32: the 4 sums + the image count). value = images processed by
 all ranks / max-over-ranks wall time of the K timed steps.
 """
 from __future__ import annotations
@@ -94,8 +94,31 @@ def roofline_for(per):
     rf.update({'kernel': name, 'launches_per_step': d['launches'],
                'avg_launch_us': round(d['ms'] * 1e3 / d['launches'], 3),
                'alg_flops_per_launch': d['flops'] / d['launches'],
-               'alg_bytes_per_launch': d['bytes'] / d['launches'], 'traffic': None})
+               'alg_bytes_per_launch': d['bytes'] / d['launches']})
+    rf.update(pmc_traffic(name))
     return rf
+
+
+def pmc_traffic(kernel):
+    """HBM traffic per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_summary.json, written by profiles/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this bench command, gfx950 FETCH_SIZE x2 correction applied there)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_summary.json')))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                ks = json.load(fh).get('kernels', {})
+        except (OSError, ValueError):
+            continue
+        for k, e in ks.items():
+            sym = k.split('::')[-1]
+            if sym.startswith(kernel + '<') or sym == kernel:
+                h = e.get('hbm')
+                if h:
+                    return {'traffic': round(h['traffic_bytes'], 1), 'traffic_unit': 'bytes/launch',
+                            'traffic_source': os.path.relpath(f, ROOT)}
+    return {'traffic': None}
 
 
 def cpu_baseline(cfg, budget_s=12.0):
@@ -247,6 +270,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg)
         ld_mean = ld.mean().item()
+        # global batch-mean NLL (nats/image): the all-reduced sums when sharded
+        loss_mean = (red[0] / red[4]).item() if dist is not None else sums[0].item() / B
         out = {
             'metric': 'images/sec fwd+logdet, 32x32x3 3-scale flow @1/2/4/8 GPU; bits/dim vs ref'
             if args.config == 'cfg2' else f'images/sec fwd+logdet ({args.config})',
@@ -257,9 +282,9 @@ def main():
             'config': {'workload': f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, '
                                    f'{B} images per GPU', 'model': f'cFlow {cfg.name}', 'global_batch': B * world,
                        'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world} (batch shards, '
-                                                                          f'1 all-reduce of 4 fp32)',
+                                                                          f'1 all-reduce of 5 fp32)',
                        'graph': graph is not None},
-            'bits_per_dim': round(float(sums[0].item() / (B * world) / (np.log(2) * cfg.io_shape[0] * cfg.io_shape[1] * cfg.x_d)), 6),
+            'bits_per_dim': round(float(loss_mean / (np.log(2) * cfg.io_shape[0] * cfg.io_shape[1] * cfg.x_d)), 6),
             'logdet_mean': ld_mean,
             'roofline': roof,
             'cpu_baseline': cpu,
