@@ -74,6 +74,34 @@ __device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&
     }
 }
 
+// Streaming form of ln_partial for epilogues that produce their values in several steps: lanes
+// accumulate shifted fp32 sums; write() reduces over the wave and stores (n, mean, M2) in fp64.
+struct LnAcc {
+    float K, s1, s2, c;
+    __device__ __forceinline__ void reset() { K = s1 = s2 = c = 0.f; }
+    // shift = lane 0's value (call in wave-uniform control flow, before the first add)
+    __device__ __forceinline__ void set_shift(float lrelu_v) {
+        K = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lrelu_v)));
+    }
+    __device__ __forceinline__ void add(float lrelu_v, bool valid) {
+        const float d = valid ? lrelu_v - K : 0.f;
+        s1 += d;
+        s2 = fmaf(d, d, s2);
+        c += valid ? 1.f : 0.f;
+    }
+    __device__ __forceinline__ void write(double* __restrict__ dst) const {
+        const float S1f = wave_sum_f(s1), S2f = wave_sum_f(s2), cf = wave_sum_f(c);
+        if ((threadIdx.x & 63) == 0) {
+            const double n = cf, S1 = S1f;
+            const double m = n > 0.0 ? S1 / n : 0.0;
+            const double M2 = (double)S2f - S1 * m;
+            dst[0] = n;
+            dst[1] = n > 0.0 ? (double)K + m : 0.0;
+            dst[2] = M2 > 0.0 ? M2 : 0.0;
+        }
+    }
+};
+
 // (mean, rstd) of the input LayerNorm of image img from the producer's partials, merged by every
 // wave on its own (parallel-axis form: one division, fixed order, no barrier); identity without LN.
 __device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {

@@ -80,12 +80,39 @@ struct NetLdsArgs {
     const float* zero_bias;                      // >= 128 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
 };
+// k_gc (cnf_stream.hip): every grouped dilated branch of one residual block for a tile of TH
+// image rows of one net, `ipw` images per workgroup. Branch input windows are staged into LDS
+// bands with their own dilation halo (LN2 + LeakyReLU applied on the way in, zero padding), so
+// the 3x3 taps need no bounds checks; weights are PK_Q4 over cin padded to a multiple of 4.
+constexpr int GC_MAXBR = 8;
+struct GcBranch {
+    int cin_off, cin, cinp, cout, out_off, dil;   // input window, padded channels, outputs
+    int G;                                        // quad groups of the PK_Q4 image
+    int band_off, BW, BH, S;                      // LDS band: byte offset, width, height, pixel stride
+    int w_off, q_off;                             // LDS byte offsets: packed weights, quad offsets
+    uint32_t cpq_mag, bw_mag;                     // x / (cinp/4) == umulhi(x, cpq_mag) (cinp > 4), x / BW likewise
+};
+struct GcArgs {
+    const float* in[2];          // t1 per net [B][HW][in_cs]
+    float* out[2];               // t2 per net [B][HW][out_cs]
+    const double* in_part[2];    // LN2 partials of t1 (null: no LN)
+    double* out_part[2];         // LN3 partials of LeakyReLU(t2)
+    const float* gamma[2];       // LN2 gamma/beta [HW][in_cs]
+    const float* beta[2];
+    const float* w[2][GC_MAXBR];
+    const float* b[2][GC_MAXBR];
+    GcBranch br[GC_MAXBR];
+    int nbr, H, W, in_cs, out_cs, B, TH, tiles_per_img, ipw, in_nparts, part_stride;
+};
+void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st);
+int read_gc_stamps(long long* host, int n);
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
 int read_stamps(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
-void launch_pw(int nr, int gm, int mi, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_pw(int nr, int gm, int mi, bool ln, bool res, int nw, const ConvArgs& a, int grid_x, int lds,
+               hipStream_t st);
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

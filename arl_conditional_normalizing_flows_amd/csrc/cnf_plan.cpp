@@ -339,8 +339,9 @@ Plan* build_plan(const cnf_flow_desc* d) {
         // prefer PK_Q4 for its 3x3 convs (channel-quad ds_read_b128 A reads), fall back to PK_KN
         // when the Q4 images do not fit the 160 KiB LDS image, else stream the layer.
         {
-            bool allow = true;
+            bool allow = true, allow_gc = true;
             if (const char* e = std::getenv("CNF_NETLDS")) allow = std::atoi(e) != 0;
+            if (const char* e = std::getenv("CNF_GC")) allow_gc = std::atoi(e) != 0;
             for (auto& c : p.couplings) {
                 const int tapco = 9 * c.dc2 <= 64 ? PK_TAP : PK_KN;
                 c.ci_fmt = PK_KN;
@@ -363,6 +364,49 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     c.use_lds = true;
                 }
                 if (c.use_lds) c.lds = g;
+            }
+            // streamed layers: the grouped stage as one k_gc launch when its LDS image fits 80 KiB (2 per CU)
+            for (auto& c : p.couplings) {
+                c.gc_fused = false;
+                if (c.use_lds || c.R == 0 || c.br.empty() || c.br.size() > (size_t)GC_MAXBR || c.wc > 128) continue;
+                int TH = std::max(1, std::min(c.hc, 256 / c.wc));   // 256-pixel tiles (8 waves x 2 subtiles)
+                if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
+                int64_t off = 512;   // [256, 384): per-image LN table
+                std::vector<GcBranch> gb;
+                bool ok = true;
+                for (const Branch& b : c.br) {
+                    GcBranch g{};
+                    g.cin_off = b.cin_off;
+                    g.cin = b.cin;
+                    g.cinp = (b.cin + 3) / 4 * 4;
+                    g.cout = b.cout;
+                    g.out_off = b.out_off;
+                    g.dil = b.dil;
+                    g.G = (9 * (g.cinp / 4) + 3) / 4;
+                    g.BW = c.wc + 2 * b.dil;
+                    g.BH = TH + 2 * b.dil;
+                    g.S = stride8(g.cinp);
+                    // exact umulhi division for x < 2^16 (x * d < 2^32)
+                    g.cpq_mag = g.cinp == 4 ? 0u : (uint32_t)((((uint64_t)1 << 32) + (g.cinp / 4) - 1) / (g.cinp / 4));
+                    g.bw_mag = (uint32_t)((((uint64_t)1 << 32) + g.BW - 1) / g.BW);
+                    if ((int64_t)g.BH * g.BW * (g.cinp / 4) >= (1 << 16)) ok = false;
+                    if (b.cout > 64) ok = false;
+                    g.w_off = (int)off;
+                    off = align16(off + (int64_t)g.G * 16 * 16 * ((b.cout + 15) / 16) * 4);
+                    g.q_off = (int)off;
+                    off = align16(off + 16LL * g.G);
+                    g.band_off = (int)off;
+                    off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
+                    gb.push_back(g);
+                }
+                int64_t quads = 0;   // staged band quads: at most 4 per thread of the 512-thread workgroup
+                for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
+                if (!ok || off > 80 * 1024 || quads > 4 * 512 || !allow_gc) continue;
+                c.gc_fused = true;
+                c.gc_TH = TH;
+                c.gc_lds = (int)off;
+                c.gcb = gb;
+                for (size_t i = 0; i < c.br.size(); i++) c.gc_fmt[i] = PK_Q4;
             }
         }
 
@@ -440,14 +484,20 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         const std::vector<int64_t> gk = rb.gk[bi], gb = rb.gb[bi];
                         PackedConv pc;
                         // dense [9*cin][cout] view of the card per-group Conv2D kernels (:401-411)
-                        pack(pc, c.gc_fmt[bi], b.cin, b.cout,
+                        auto dense = [=](int k, int n) -> int64_t {
+                            const int tap = k / b.cin, ci2 = k - tap * b.cin;
+                            const int j = n / b.width, o = n - j * b.width;
+                            const int in_rel = b.in_offsets[j] - b.cin_off;
+                            const int cj = ci2 - in_rel;
+                            if (cj < 0 || cj >= b.width) return -1;
+                            return gk[j] + ((int64_t)tap * b.width + cj) * b.width + o;
+                        };
+                        // PK_Q4 over cin padded to a multiple of 4 (padding channels carry zero weights)
+                        const int cin_pk = c.gc_fmt[bi] == PK_Q4 ? (b.cin + 3) / 4 * 4 : b.cin;
+                        pack(pc, c.gc_fmt[bi], cin_pk, b.cout,
                              [=](int k, int n) -> int64_t {
-                                 const int tap = k / b.cin, ci2 = k - tap * b.cin;
-                                 const int j = n / b.width, o = n - j * b.width;
-                                 const int in_rel = b.in_offsets[j] - b.cin_off;
-                                 const int cj = ci2 - in_rel;
-                                 if (cj < 0 || cj >= b.width) return -1;
-                                 return gk[j] + ((int64_t)tap * b.width + cj) * b.width + o;
+                                 const int tap = k / cin_pk, ci = k - tap * cin_pk;
+                                 return ci < b.cin ? dense(tap * b.cin + ci, n) : -1;
                              },
                              [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gc.push_back(pc);

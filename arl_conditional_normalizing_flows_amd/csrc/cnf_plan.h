@@ -73,6 +73,9 @@ struct Coupling {
     int ci_fmt = PK_KN, co_fmt = PK_KN;   // packed formats of conv_in / conv_out
     std::vector<int> gc_fmt;              // per grouped branch
     NetLdsGeom lds;                       // valid when use_lds
+    bool gc_fused = false;                // streamed layer: grouped stage as one k_gc launch (PK_Q4, padded cin)
+    int gc_TH = 0, gc_lds = 0;            // k_gc tile rows, LDS bytes per workgroup
+    std::vector<GcBranch> gcb;            // k_gc branch geometry (offsets into LDS)
 };
 
 struct Layer {

@@ -111,6 +111,7 @@ WsLayout Plan::layout(int B) const {
         parts = std::max(parts, 4 * g.tiles * (int)c.br.size());   // 4 waves per workgroup
         parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
         parts = std::max(parts, 4 * ((c.hc * c.wc + 63) / 64));   // k_pw
+        if (c.gc_fused) parts = std::max(parts, 8 * ((c.hc + c.gc_TH - 1) / c.gc_TH));   // k_gc
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
     L.n_uv = n_uv;
@@ -325,21 +326,21 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         });
         return 4 * g.tiles;
     } else if (pw_ok) {
-        // k_pw: 64-pixel tiles x groups of MI images (see cnf_stream.hip)
-        const int tiles = (h * w + 63) / 64;
-        const int mi = (pw_gm <= 4 && probs[0].res == nullptr) ? 4 : 2;   // k_pw instantiations
+        // k_pw: (16 * nw)-pixel tiles x groups of MI images (see cnf_stream.hip)
+        const bool resf = probs[0].res != nullptr;
+        const int nw = resf ? 4 : 8, mi = 2;
+        const int tiles = (h * w + 16 * nw - 1) / (16 * nw);
         a.tiles_per_img = tiles;
         for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = 0;
         const int grid_x = tiles * ((E.B + mi - 1) / mi);
         const int nr = pw_nr, gm = pw_gm;
         const bool lnf = probs[0].in_st.part != nullptr;
-        const bool resf = probs[0].res != nullptr;
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
-                           std::to_string(mi) + "," + role_name(role) + ">";
-        E.record(name, flops, bytes, [nr, gm, mi, lnf, resf, a, grid_x, ilds](void* st) {
-            launch_pw(nr, gm, mi, lnf, resf, a, grid_x, ilds, (hipStream_t)st);
+                           std::to_string(mi) + "," + std::to_string(nw) + "," + role_name(role) + ">";
+        E.record(name, flops, bytes, [nr, gm, mi, lnf, resf, nw, a, grid_x, ilds](void* st) {
+            launch_pw(nr, gm, mi, lnf, resf, nw, a, grid_x, ilds, (hipStream_t)st);
         });
-        return 4 * tiles;
+        return nw * tiles;
     } else {
         const int grid_x = E.B * g1.tiles;
         const int mr = g1.MR;
@@ -578,7 +579,48 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used));
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]
-        {
+        if (c.gc_fused) {
+            GcArgs ga;
+            std::memset(&ga, 0, sizeof(ga));
+            for (int n = 0; n < 2; n++) {
+                const RBParams& rb = c.net[n].rb[r];
+                ga.in[n] = t1[n];
+                ga.out[n] = t2[n];
+                ga.in_part[n] = ln ? sl[n][1].part : nullptr;
+                ga.out_part[n] = ln ? sl[n][2].part : nullptr;
+                ga.gamma[n] = ln ? P + rb.ln2g : nullptr;
+                ga.beta[n] = ln ? P + rb.ln2b : nullptr;
+                for (int bi = 0; bi < nbr; bi++) {
+                    ga.w[n][bi] = X + rb.gc[bi].w;
+                    ga.b[n][bi] = X + rb.gc[bi].b;
+                }
+            }
+            for (int bi = 0; bi < nbr; bi++) ga.br[bi] = c.gcb[bi];
+            ga.nbr = nbr;
+            ga.H = c.hc;
+            ga.W = c.wc;
+            ga.in_cs = c.nk;
+            ga.out_cs = c.gc;
+            ga.B = B;
+            ga.TH = c.gc_TH;
+            ga.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
+            ga.in_nparts = sl[0][1].nparts;
+            ga.part_stride = L.st_parts;
+            // images per workgroup: the launch fits one dispatch round at 2 workgroups per CU
+            const int64_t units = (int64_t)ga.tiles_per_img * 2 * B;
+            ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+            if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::atoi(e));   // tuning override
+            if (8 * ga.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
+            const int grid_x = ga.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
+            const int ilds = c.gc_lds;
+            double fl = 0, by = 0;
+            for (const Branch& b : c.br) fl += 2.0 * B * c.hc * c.wc * 9.0 * b.cin * b.cout * 2;
+            int win = 0;
+            for (const Branch& b : c.br) win += b.cin;
+            by = 4.0 * B * c.hc * c.wc * (win + c.gc) * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
+            E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
+            set_parts(2, 8 * ga.tiles_per_img);   // 8 waves per k_gc workgroup
+        } else {
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
@@ -973,6 +1015,7 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
 
 // diagnostic: phase stamps of the last CNF_STAMPS=1 k_net_lds launch (s_memrealtime, 100 MHz)
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
+int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }
 
 int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)plan->p->recorded.size() : -1; }
 

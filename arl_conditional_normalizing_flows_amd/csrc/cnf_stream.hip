@@ -21,8 +21,8 @@ constexpr int PW_LDS_STAT = 256;    // byte offset of the per-image (mean, rstd)
 // every activation load of the workgroup is issued up front (one memory round trip), the LN
 // gamma/beta registers of the tile serve all MI images, and each B-quad LDS read feeds 4*MI
 // MFMAs. No loop-carried waits: latency is covered by the MI*G float4 loads each lane has in flight.
-template <int NR, int GM, int MI, bool LN, bool RES>
-__global__ __launch_bounds__(256, 2) void k_pw(ConvArgs a) {
+template <int NR, int GM, int MI, bool LN, bool RES, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const ConvProb P = a.p[blockIdx.y];
     const int HW = a.H * a.W;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256, 2) void k_pw(ConvArgs a) {
     const auto rout = buf_rsrc(P.out, (uint32_t)a.B * out_img);
 
     // A operand: lane (i16, kq) feeds pixel pa, channels 16g + 4kq + s at k-step s of group g
-    const int pa = tile * PW_TILE + wave * 16 + i16;
+    const int pa = tile * (16 * NW) + wave * 16 + i16;
     const bool pav = pa < HW;
     const uint32_t aoff = ((uint32_t)pa * P.in_cs + P.in_off + 4 * kq) * 4u;
     uint32_t goff[GM];   // byte offset of group g inside one image, BUF_OOB when masked
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256, 2) void k_pw(ConvArgs a) {
         }
     }
     // output: acc[m][n][r] = out[image img0+m][pixel po0 + r][channel 16n + i16]
-    const int po0 = tile * PW_TILE + wave * 16 + kq * 4;
+    const int po0 = tile * (16 * NW) + wave * 16 + kq * 4;
     uint32_t oo[NR][4];   // byte offset inside one image, BUF_OOB for masked pixels/channels
     bool valid[NR * 4];
 #pragma unroll
@@ -92,8 +92,8 @@ __global__ __launch_bounds__(256, 2) void k_pw(ConvArgs a) {
     }
 
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
-    copy_to_lds<256>(P.wt, lw, G * 16 * NSJ);
-    if (LN && wave < MI && img0 + wave < a.B) {
+    copy_to_lds<64 * NW>(P.wt, lw, G * 16 * NSJ);
+    if (LN && wave < MI && img0 + wave < a.B) {   // NW >= MI
         float mu, rs;
         in_ln(P, img0 + wave, mu, rs);
         if (lane == 0) {
@@ -159,28 +159,265 @@ __global__ __launch_bounds__(256, 2) void k_pw(ConvArgs a) {
             }
         if (P.out_part != nullptr)
             ln_partial(vals, valid,
-                       P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tile * 4 + wave) * 3);
+                       P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tile * NW + wave) * 3);
     }
 }
 
-void launch_pw(int nr, int gm, int mi, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
-    dim3 g(grid_x, a.nprob), b(256);
-#define CNF_PW_CASE(NR_, GM_, MI_, LN_, RES_)                                                  \
-    if (nr == NR_ && gm == GM_ && mi == MI_ && ln == LN_ && res == RES_) {                    \
-        hipLaunchKernelGGL((k_pw<NR_, GM_, MI_, LN_, RES_>), g, b, lds, st, a);               \
-        return;                                                                               \
+void launch_pw(int nr, int gm, int mi, bool ln, bool res, int nw, const ConvArgs& a, int grid_x, int lds,
+               hipStream_t st) {
+    dim3 g(grid_x, a.nprob), b(64 * nw);
+#define CNF_PW_CASE(NR_, GM_, MI_, LN_, RES_, NW_)                                              \
+    if (nr == NR_ && gm == GM_ && mi == MI_ && ln == LN_ && res == RES_ && nw == NW_) {         \
+        hipLaunchKernelGGL((k_pw<NR_, GM_, MI_, LN_, RES_, NW_>), g, b, lds, st, a);            \
+        return;                                                                                \
     }
-#define CNF_PW_NR(GM_, MI_, LN_, RES_)                                                        \
-    CNF_PW_CASE(1, GM_, MI_, LN_, RES_) CNF_PW_CASE(2, GM_, MI_, LN_, RES_)                   \
-    CNF_PW_CASE(3, GM_, MI_, LN_, RES_) CNF_PW_CASE(4, GM_, MI_, LN_, RES_)
-#define CNF_PW_GM(MI_, LN_, RES_) \
-    CNF_PW_NR(1, MI_, LN_, RES_) CNF_PW_NR(2, MI_, LN_, RES_) CNF_PW_NR(4, MI_, LN_, RES_) CNF_PW_NR(8, 2, LN_, RES_)
-    // MI = 4 for K <= 64 without residual, else 2 (register budget of 2 waves/SIMD, pw_images())
-    CNF_PW_GM(4, true, false) CNF_PW_GM(2, true, true) CNF_PW_GM(4, false, false) CNF_PW_GM(2, false, true)
+#define CNF_PW_NR(GM_, MI_, LN_, RES_, NW_)                                                    \
+    CNF_PW_CASE(1, GM_, MI_, LN_, RES_, NW_) CNF_PW_CASE(2, GM_, MI_, LN_, RES_, NW_)          \
+    CNF_PW_CASE(3, GM_, MI_, LN_, RES_, NW_) CNF_PW_CASE(4, GM_, MI_, LN_, RES_, NW_)
+#define CNF_PW_GM(LN_, RES_, NW_) \
+    CNF_PW_NR(1, 2, LN_, RES_, NW_) CNF_PW_NR(2, 2, LN_, RES_, NW_) CNF_PW_NR(4, 2, LN_, RES_, NW_) CNF_PW_NR(8, 2, LN_, RES_, NW_)
+    // MI = 2 images per wave; 8 waves (no residual) or 4 waves (residual) per workgroup (pw_shape())
+    CNF_PW_GM(true, false, 8) CNF_PW_GM(false, false, 8) CNF_PW_GM(true, true, 4) CNF_PW_GM(false, true, 4)
 #undef CNF_PW_GM
 #undef CNF_PW_NR
 #undef CNF_PW_CASE
     throw std::invalid_argument("k_pw: no instantiation for this shape");
+}
+
+}  // namespace cnf
+
+namespace cnf {
+
+// ---------------------------------------------------------------------------------------------
+// k_gc: the grouped dilated stage of a residual block (conv_cINN_base_functions.py:364-413,
+// 583-601) for the streamed layers — LN2(LeakyReLU(t1)) on the branch windows -> every branch's
+// dense 3x3 dilated conv -> t2 slices, plus the per-wave LN3 partials of LeakyReLU(t2).
+// ---------------------------------------------------------------------------------------------
+constexpr int GC_NW = 8;            // waves per k_gc workgroup
+constexpr int GC_NT = 64 * GC_NW;   // threads
+
+template <int NR>
+__device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, const unsigned char* smem,
+                                          const float* __restrict__ bias, float* __restrict__ outp, int npx,
+                                          int px0, LnAcc& st, bool& first, bool stats) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i16 = lane & 15, kq = lane >> 4;
+    constexpr int NSJ = 16 * NR;
+    const float* band = reinterpret_cast<const float*>(smem + br.band_off);
+    const float* lw = reinterpret_cast<const float*>(smem + br.w_off);
+    const int* qo = reinterpret_cast<const int*>(smem + br.q_off);
+    float bz[NR];
+    bool chv[NR];
+#pragma unroll
+    for (int n = 0; n < NR; n++) {
+        const int ch = n * 16 + i16;
+        chv[n] = ch < br.cout;
+        bz[n] = chv[n] ? bias[ch] : 0.f;
+    }
+    const int nsub = (npx + 15) >> 4;
+    for (int s = wave; s < nsub; s += GC_NW) {
+        const int pt = s * 16 + i16;
+        const int ptc = pt < npx ? pt : 0;
+        const int tr = ptc / a.W, tc = ptc - tr * a.W;
+        const float* base = band + (tr * br.BW + tc) * br.S;
+        f4 acc[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+        const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
+        for (int g = 0; g < br.G; g++) {
+            const f4 av = *reinterpret_cast<const f4*>(base + qo[4 * g + kq]);
+            f4 bq[NR];
+#pragma unroll
+            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int n = 0; n < NR; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bq[n][q], acc[n], 0, 0, 0);
+        }
+        if (stats && first) {
+            st.set_shift(lrelu(acc[0][0] + bz[0]));
+            first = false;
+        }
+#pragma unroll
+        for (int n = 0; n < NR; n++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int po = s * 16 + kq * 4 + r;
+                const bool ok = chv[n] && po < npx;
+                const float v = acc[n][r] + bz[n];
+                if (ok) outp[(size_t)(px0 + po) * a.out_cs + br.out_off + n * 16 + i16] = v;
+                if (stats) st.add(lrelu(v), ok);
+            }
+    }
+}
+
+constexpr int GC_GQ = 4;   // staged band quads per thread (the plan checks the total fits)
+
+// diagnostic phase stamps of workgroup (0, 0) (CNF_GC_STAMPS builds only; never in timed runs)
+__device__ long long g_gc_stamps[64];
+#ifdef CNF_GC_STAMPS
+#define GSTAMP(i)                                                                             \
+    do {                                                                                      \
+        __syncthreads();                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0)                           \
+            g_gc_stamps[(i)] = (long long)__builtin_amdgcn_s_memrealtime();                  \
+    } while (0)
+#else
+#define GSTAMP(i) do { } while (0)
+#endif
+
+__global__ __launch_bounds__(GC_NT, 2) void k_gc(GcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int net = blockIdx.y;
+    const int tile = blockIdx.x % a.tiles_per_img;
+    const int img0 = (blockIdx.x / a.tiles_per_img) * a.ipw;
+    const int nimg = min(a.ipw, a.B - img0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int H = a.H, W = a.W, HW = H * W;
+    const int r0 = tile * a.TH;
+    const int rows = min(a.TH, H - r0);
+    const int npx = rows * W, px0 = r0 * W;
+    const bool ln = a.in_part[net] != nullptr;
+    const bool stats = a.out_part[net] != nullptr;
+    float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
+    float* lds_f = reinterpret_cast<float*>(smem);
+    int gs = 0;
+    GSTAMP(gs++);
+
+    // image-independent staging plan of this thread: quad e = tid + GC_NT*u of the concatenated branch
+    // bands -> source offset inside one image, LDS float index, valid channels (0 = zero quad)
+    int soff[GC_GQ], loff[GC_GQ], nv[GC_GQ];
+#pragma unroll
+    for (int u = 0; u < GC_GQ; u++) {
+        int e = tid + GC_NT * u;
+        soff[u] = 0;
+        loff[u] = -1;
+        nv[u] = 0;
+        for (int bi = 0; bi < a.nbr; bi++) {
+            const GcBranch& br = a.br[bi];
+            const int cpq = br.cinp >> 2, nq = br.BH * br.BW * cpq;
+            if (e < nq) {
+                const int pix = cpq == 1 ? e : (int)__umulhi((unsigned)e, br.cpq_mag), cq = e - pix * cpq;
+                const int brr = (int)__umulhi((unsigned)pix, br.bw_mag), bc = pix - brr * br.BW;
+                const int y = r0 - br.dil + brr, x = bc - br.dil;
+                loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
+                if (y >= 0 && y < H && x >= 0 && x < W) {
+                    soff[u] = (y * W + x) * a.in_cs + br.cin_off + 4 * cq;
+                    const int v = min(4, br.cin - 4 * cq);
+                    const bool vec = v == 4 && ((br.cin_off | a.in_cs) & 3) == 0;
+                    nv[u] = v | (vec ? 8 : 0);
+                }
+                break;
+            }
+            e -= nq;
+        }
+    }
+    auto load_q = [&](const float* __restrict__ base, int u) -> f4 {
+        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+        const int n = nv[u] & 7;
+        if (nv[u] & 8) {
+            v = *reinterpret_cast<const f4*>(base + soff[u]);
+        } else if (n > 0) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (j < n) v[j] = base[soff[u] + j];
+        }
+        return v;
+    };
+    // packed weights and quad-offset tables of every branch (once per workgroup)
+    for (int bi = 0; bi < a.nbr; bi++) {
+        const GcBranch& br = a.br[bi];
+        const int nr = (br.cout + 15) >> 4;
+        copy_to_lds<GC_NT>(a.w[net][bi], reinterpret_cast<float*>(smem + br.w_off), br.G * 16 * 16 * nr);
+        int* qo = reinterpret_cast<int*>(smem + br.q_off);
+        const int cpq = br.cinp >> 2, nq = 9 * cpq;
+        for (int qd = tid; qd < 4 * br.G; qd += GC_NT) {
+            int o = 0;   // padding quads have zero weights: any in-band address is fine
+            if (qd < nq) {
+                const int tap = qd / cpq, cq = qd - tap * cpq;
+                o = (((tap / 3) * br.dil) * br.BW + (tap % 3) * br.dil) * br.S + 4 * cq;
+            }
+            qo[qd] = o;
+        }
+    }
+    // per-image LN2 (mean, rstd) from the producer's partials
+    if (ln) {
+        ConvProb P;
+        P.in_part = a.in_part[net];
+        P.in_nparts = a.in_nparts;
+        P.part_stride = a.part_stride;
+        for (int i = wave; i < nimg; i += GC_NW) {
+            float mu, rs;
+            in_ln(P, img0 + i, mu, rs);
+            if (lane == 0) {
+                lstat[2 * i] = mu;
+                lstat[2 * i + 1] = rs;
+            }
+        }
+    }
+    __syncthreads();
+    GSTAMP(gs++);
+
+    for (int ii = 0; ii < nimg; ii++) {
+        const int img = img0 + ii;
+        // stage this image's bands: LN2(LeakyReLU(t1)), zero outside the image / window
+        {
+            const float rs = ln ? lstat[2 * ii + 1] : 1.f;
+            const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
+            const float* __restrict__ src = a.in[net] + (size_t)img * HW * a.in_cs;
+            f4 xq[GC_GQ], gq[GC_GQ], bq[GC_GQ];
+#pragma unroll
+            for (int u = 0; u < GC_GQ; u++) {
+                xq[u] = load_q(src, u);
+                gq[u] = ln ? load_q(a.gamma[net], u) : f4{1.f, 1.f, 1.f, 1.f};
+                bq[u] = ln ? load_q(a.beta[net], u) : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < GC_GQ; u++) {
+                if (loff[u] < 0) continue;
+                f4 v = f4{0.f, 0.f, 0.f, 0.f};
+                if (nv[u] != 0) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const float t = lrelu(xq[u][j]);
+                        v[j] = ln ? fmaf(fmaf(t, rs, nmr), gq[u][j], bq[u][j]) : t;
+                    }
+                }
+                *reinterpret_cast<f4*>(lds_f + loff[u]) = v;
+            }
+        }
+        __syncthreads();
+        GSTAMP(gs++);
+        LnAcc st;
+        st.reset();
+        bool first = true;
+        float* outp = a.out[net] + (size_t)img * HW * a.out_cs;
+        for (int bi = 0; bi < a.nbr; bi++) {
+            const GcBranch& br = a.br[bi];
+            const float* bias = a.b[net][bi];
+            switch ((br.cout + 15) >> 4) {
+                case 1: gc_branch<1>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
+                case 2: gc_branch<2>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
+                case 3: gc_branch<3>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
+                default: gc_branch<4>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
+            }
+            GSTAMP(gs++);
+        }
+        if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * 3);
+        __syncthreads();   // bands are restaged for the next image
+        GSTAMP(gs++);
+    }
+#ifdef CNF_GC_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_gc_stamps[63] = gs;
+#endif
+}
+
+int read_gc_stamps(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gc_stamps), sizeof(long long) * (n > 64 ? 64 : n)) == hipSuccess ? 0 : -1;
+}
+
+void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
+    hipLaunchKernelGGL(k_gc, dim3(grid_x, 2), dim3(GC_NT), lds, st, a);
 }
 
 }  // namespace cnf

@@ -48,7 +48,9 @@ def _err(a, b):
 CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('small', 2, 'intended', True),
          ('cfg2', 2, 'reference', True), ('cfg3', 2, 'reference', True), ('ref_default', 2, 'reference', True),
          # the streamed (multi-kernel) path for every layer
-         ('small', 3, 'reference', False), ('cfg2', 2, 'reference', False), ('ref_default', 2, 'reference', False)]
+         # (group_mode='intended' on streamed layers needs the dense grouped image in LDS: small only)
+         ('small', 3, 'reference', False), ('small', 2, 'intended', False), ('cfg2', 2, 'reference', False),
+         ('ref_default', 2, 'reference', False)]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
