@@ -35,6 +35,12 @@ class cnf_layer_info(C.Structure):
                 ('fused_net', C.c_int)]
 
 
+class cnf_toy_desc(C.Structure):
+    _fields_ = [('io_shape', C.c_int), ('x_d', C.c_int), ('num_coupling_layers', C.c_int),
+                ('intermediate_dims', C.c_int), ('num_layers', C.c_int), ('mask_indices', C.POINTER(C.c_int)),
+                ('lambda_y', C.c_float)]
+
+
 # (name, restype, argtypes)
 _P = C.c_void_p
 _F = C.c_void_p   # device float* as integer address
@@ -58,6 +64,9 @@ _SIGS = [
     ('cnf_channel_copy', C.c_int, [_F, C.c_int, C.c_int, _F, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),
     ('cnf_nll', C.c_int, [_P, _F, _F, _F, _F, _F, C.c_int, _P]),
+    ('cnf_toy_num_params', C.c_int64, [C.POINTER(cnf_toy_desc)]),
+    ('cnf_toy_call', C.c_int, [C.POINTER(cnf_toy_desc), _F, _F, _F, _F, _F, C.c_int, C.c_int, _P]),
+    ('cnf_toy_nll_sums', C.c_int, [_F, _F, C.c_int, _P]),
     ('cnf_plan_num_recorded_launches', C.c_int, [_P]),
     ('cnf_plan_recorded_launch_info', C.c_int, [_P, C.c_int, C.c_char_p, C.c_int,
                                                 C.POINTER(C.c_double), C.POINTER(C.c_double)]),

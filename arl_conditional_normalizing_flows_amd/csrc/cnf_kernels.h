@@ -106,6 +106,21 @@ struct GcArgs {
 };
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st);
 int read_gc_stamps(long long* host, int n);
+// k_toy (cnf_toy.hip): TOYcINN dense flow, one thread per 3-dimensional sample
+constexpr int TOY_MAXL = 128;
+struct ToyArgs {
+    const float* params;   // canonical flat parameters (per network j: b-block then A-block)
+    const float* u;        // [B][3]
+    float* v;              // [B][3]
+    float* log_detJ;       // [B] (direction -1) or null
+    float* per_sample;     // [B][3] (llz, lly, log_detJ) of log_loss (direction -1) or null
+    int B, nl, H, L, x_d, dir;
+    float lambda_y;
+    int order[TOY_MAXL];        // mask_indices
+    int net_off[TOY_MAXL + 1];  // float offset of network j's parameters
+};
+void launch_toy(const ToyArgs& a, int lds_floats, hipStream_t st);
+void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st);
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
 int read_stamps(long long* host, int n);
 

@@ -748,6 +748,10 @@ void launch_nll(const float* xy, const float* zy, const float* ld, float* per_im
     hipLaunchKernelGGL(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
 }
 
+void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
+}
+
 void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st) {
     long long gx = (n + 255) / 256;
     if (gx > 4096) gx = 4096;

@@ -1014,6 +1014,87 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
 }
 
 // diagnostic: phase stamps of the last CNF_STAMPS=1 k_net_lds launch (s_memrealtime, 100 MHz)
+// ---- TOYcINN -------------------------------------------------------------------------------
+static int64_t toy_net_floats(int n1, int n2, int H, int L) {
+    return (int64_t)n1 * H + H + (int64_t)L * (H * H + H) + (int64_t)H * n2 + n2;
+}
+
+static void toy_check(const cnf_toy_desc* d) {
+    if (!d) throw std::invalid_argument("null toy descriptor");
+    if (d->io_shape != 3) throw std::invalid_argument("TOYcINN masks are defined for io_shape == 3 only");
+    if (d->x_d < 1 || d->x_d > 2) throw std::invalid_argument("x_d must be 1 or 2");
+    if (d->num_coupling_layers < 1 || d->num_coupling_layers > TOY_MAXL)
+        throw std::invalid_argument("num_coupling_layers must be in [1, 128]");
+    if (d->intermediate_dims < 1 || d->intermediate_dims > 64) throw std::invalid_argument("intermediate_dims must be in [1, 64]");
+    if (d->num_layers < 0) throw std::invalid_argument("num_layers must be >= 0");
+    if (!d->mask_indices) throw std::invalid_argument("mask_indices is required");
+    std::vector<int> seen(d->num_coupling_layers, 0);
+    for (int i = 0; i < d->num_coupling_layers; i++) {
+        const int j = d->mask_indices[i];
+        if (j < 0 || j >= d->num_coupling_layers || seen[j]++) throw std::invalid_argument("mask_indices must be a permutation");
+    }
+}
+
+int64_t cnf_toy_num_params(const cnf_toy_desc* d) {
+    CNF_TRY
+    toy_check(d);
+    int64_t n = 0;
+    for (int j = 0; j < d->num_coupling_layers; j++) {
+        const int n1 = (j % 6) < 3 ? 1 : 2;
+        n += 2 * toy_net_floats(n1, 3 - n1, d->intermediate_dims, d->num_layers);
+    }
+    return n;
+    CNF_CATCH
+}
+
+int cnf_toy_call(const cnf_toy_desc* d, const float* params, const float* u, float* v, float* log_detJ,
+                 float* per_sample, int B, int direction, void* stream) {
+    CNF_TRY
+    toy_check(d);
+    if (!params || !u || !v || B < 0) return fail(CNF_E_INVALID, "null pointer or negative batch");
+    if (direction != 1 && direction != -1) return fail(CNF_E_INVALID, "direction must be +1 or -1");
+    if (u == v) return fail(CNF_E_INVALID, "u and v must not alias");
+    if (B == 0) return CNF_OK;
+    ToyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.params = params;
+    a.u = u;
+    a.v = v;
+    a.log_detJ = direction < 0 ? log_detJ : nullptr;
+    a.per_sample = direction < 0 ? per_sample : nullptr;
+    a.B = B;
+    a.nl = d->num_coupling_layers;
+    a.H = d->intermediate_dims;
+    a.L = d->num_layers;
+    a.x_d = d->x_d;
+    a.dir = direction;
+    a.lambda_y = d->lambda_y;
+    int64_t off = 0, maxn = 0;
+    for (int j = 0; j < a.nl; j++) {
+        a.order[j] = d->mask_indices[j];
+        a.net_off[j] = (int)off;
+        const int n1 = (j % 6) < 3 ? 1 : 2;
+        const int64_t n = 2 * toy_net_floats(n1, 3 - n1, a.H, a.L);
+        off += n;
+        maxn = std::max(maxn, n);
+    }
+    a.net_off[a.nl] = (int)off;
+    if (maxn * 4 > 160 * 1024) return fail(CNF_E_INVALID, "toy coupling networks exceed the 160 KiB LDS staging budget");
+    launch_toy(a, (int)maxn, (hipStream_t)stream);
+    hip_check(hipGetLastError(), "k_toy");
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream) {
+    CNF_TRY
+    if (!per_sample || !sums || B < 1) return fail(CNF_E_INVALID, "null pointer or empty batch");
+    launch_nll_sums(per_sample, sums, B, (hipStream_t)stream);
+    hip_check(hipGetLastError(), "k_nll_sums");
+    return CNF_OK;
+    CNF_CATCH
+}
+
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }
 

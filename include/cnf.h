@@ -145,6 +145,34 @@ int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out
 int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image,
             float* per_image, float* sums, int B, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * TOYcINN (BASELINE configs[0]): the dense conditional flow of
+ * TOYcINN_make_model.py:29-506 on 3-dimensional points.
+ * ------------------------------------------------------------------------- */
+typedef struct cnf_toy_desc {
+    int io_shape;              /* must be 3 (the reference masks, :149-163) */
+    int x_d;                   /* 1 or 2 */
+    int num_coupling_layers;   /* <= 128 */
+    int intermediate_dims;     /* H <= 64 */
+    int num_layers;            /* hidden Dense layers after the first */
+    const int* mask_indices;   /* [num_coupling_layers], a permutation (cINN_affine.mask_indices) */
+    float lambda_y;            /* 100 in the reference */
+} cnf_toy_desc;
+
+/* Number of fp32 parameters: per network j (j = 0..L-1, mask type j % 6), the b net then the A
+ * net, each Dense as kernel [in][out] then bias [out] (:48-94). */
+int64_t cnf_toy_num_params(const cnf_toy_desc* d);
+
+/* cINN_affine.call(u, direction) (:237-417): direction -1 = xy' -> zy (reverse layer order,
+ * log_detJ[B] = per-sample sum of A), +1 = zy -> xy'. u, v: [B][3], must not alias.
+ * per_sample[B*3] (direction -1, optional) = (llz, lly, log_detJ) of log_loss (:419-451). */
+int cnf_toy_call(const cnf_toy_desc* d, const float* params, const float* u, float* v, float* log_detJ,
+                 float* per_sample, int B, int direction, void* stream);
+
+/* Batch sums of the toy log_loss terms: sums[4] = (sum loss_i, sum -llz_i, sum -lly_i,
+ * sum -log_detJ_i); divide by B for the reference's 4-tuple. */
+int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream);
+
 /* Measurement hooks (bench.py): number of kernel launches recorded by the last
  * forward/inverse call on this plan, their kernel symbol names, and a re-launch
  * of one recorded launch with identical arguments (same buffers). */
