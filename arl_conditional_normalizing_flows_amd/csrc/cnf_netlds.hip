@@ -30,6 +30,10 @@ namespace {
 #define CNF_NETLDS_NW 8
 #endif
 constexpr int NW = CNF_NETLDS_NW;   // waves per workgroup (one workgroup per CU: LDS-bound)
+#ifndef CNF_NETLDS_PAIR
+#define CNF_NETLDS_PAIR 1
+#endif
+constexpr bool PAIR = CNF_NETLDS_PAIR != 0;   // two 16-pixel subtiles per wave and pass
 constexpr int NT = NW * 64;         // threads
 
 // LeakyReLU(0.3) as max(x, 0.3x) (2 VALU ops; equal to the select form for every finite x)
@@ -187,6 +191,51 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
     }
 }
 
+// In-place LN(LeakyReLU) over the disjoint channel windows of buf (the grouped branches' inputs)
+// in ONE pass: the elements of all windows are enumerated together, so every gamma/beta load of
+// a thread is in flight at once (one L2 round trip instead of one per window).
+__device__ __forceinline__ void ln_windows(float* buf, int stride, int HW, int C_ln, int nwin, const int* woff,
+                                           const int* wlen, float mu, float rstd, const float* __restrict__ g,
+                                           const float* __restrict__ b, bool ln) {
+    int total = 0;
+    for (int k = 0; k < nwin; k++) total += HW * wlen[k];
+    const float nmr = -mu * rstd;
+    constexpr int US = 8;
+    for (int base = 0; base < total; base += NT * US) {
+        int pos[US], gi[US];
+        float xv[US], gv[US], bv[US];
+#pragma unroll
+        for (int u = 0; u < US; u++) {
+            int e = base + u * NT + (int)threadIdx.x;
+            pos[u] = -1;
+            gi[u] = 0;
+            if (e < total) {
+                for (int k = 0; k < nwin; k++) {
+                    const int m = HW * wlen[k];
+                    if (e < m) {
+                        const int p = e / wlen[k], c = woff[k] + (e - p * wlen[k]);
+                        pos[u] = p * stride + c;
+                        gi[u] = p * C_ln + c;
+                        break;
+                    }
+                    e -= m;
+                }
+            }
+            xv[u] = pos[u] >= 0 ? buf[pos[u]] : 0.f;
+            if (ln) {
+                gv[u] = g[gi[u]];
+                bv[u] = b[gi[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < US; u++) {
+            if (pos[u] < 0) continue;
+            const float t = lrelu_(xv[u]);
+            buf[pos[u]] = ln ? fmaf(fmaf(t, rstd, nmr), gv[u], bv[u]) : t;
+        }
+    }
+}
+
 // Register prefetch of the next conv's pre-packed weight image: loaded before the current conv's
 // MFMA loop, written to LDS after the barrier that retires the current conv.
 constexpr int WPF = NW >= 16 ? 2 : 4;   // float4 per thread -> up to WPF*NT*4 floats
@@ -270,9 +319,9 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
     LStat st;
     lst_reset(st);
     const bool stats = slots != nullptr;
-    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+    for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
-        const bool v1 = s1 < nsub;
+        const bool v1 = PAIR && s1 < nsub;
         const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
         const bool pva = pa < HW, pvb = v1 && pb < HW;
         f4 acc0[NR], acc1[NR];
@@ -355,9 +404,9 @@ __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, 
     LStat st;
     lst_reset(st);
     const bool stats = slots != nullptr;
-    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+    for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
-        const bool v1 = s1 < nsub;
+        const bool v1 = PAIR && s1 < nsub;
         const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
         const bool pva = pa < HW, pvb = v1 && pb < HW;
         const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
@@ -432,9 +481,9 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
     LStat st;
     lst_reset(st);
     const bool stats = slots != nullptr;
-    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+    for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
-        const bool v1 = s1 < nsub;
+        const bool v1 = PAIR && s1 < nsub;
         const int pa = s0 * 16 + i16, pb = s1 * 16 + i16;
         const bool pva = pa < HW, pvb = v1 && pb < HW;
         const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
@@ -591,9 +640,12 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
         if (ln) lst_final(slots, mu, rstd);
-        for (int wi = 0; wi < a.nwin; wi++)
-            ln_apply(T1, S1, T1, S1, HW, a.win_off[wi], a.win_len[wi], nk, mu, rstd, ln ? P + o[4] : nullptr,
+        if (a.nwin == 1)
+            ln_apply(T1, S1, T1, S1, HW, a.win_off[0], a.win_len[0], nk, mu, rstd, ln ? P + o[4] : nullptr,
                      ln ? P + o[5] : nullptr, ln);
+        else
+            ln_windows(T1, S1, HW, nk, a.nwin, a.win_off, a.win_len, mu, rstd, ln ? P + o[4] : nullptr,
+                       ln ? P + o[5] : nullptr, ln);
         // grouped dilated branches -> T2[:, out_off : out_off + cout] (+ LN3 stats over all of them)
         for (int bi = 0; bi < a.nbr; bi++) {
             const LdsConv& cv = a.gcv[bi];

@@ -109,7 +109,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
         acc(PK_1X1, 1, c.gc, c.nk);
         for (size_t bi = 0; bi < c.br.size(); bi++) acc(gc_fmt[bi], 3, c.br[bi].cin, c.br[bi].cout);
     }
-    int64_t off = 256;   // block reduction scratch (2 x NW doubles, NW <= 16)
+    int64_t off = 512;   // LN-statistics slots (NW x 3 doubles, NW <= 16)
     g.off_y = (int)off;
     off = align16(off + HW * g.sy * 4);
     g.off_t1 = (int)off;
