@@ -191,6 +191,65 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
     }
 }
 
+// Register prefetch of the next full-width LayerNorm's gamma/beta quads i = u*NT + tid (u < GPF),
+// issued before the conv that produces the tensor and consumed by ln_full after it; quads beyond
+// the window are loaded on demand.
+constexpr int GPF = 4;
+struct LnPre {
+    f4 g[GPF], b[GPF];
+};
+__device__ __forceinline__ void lnp_load(LnPre& L, const float* __restrict__ g, const float* __restrict__ b, int n4) {
+    const f4* g4 = reinterpret_cast<const f4*>(g);
+    const f4* b4 = reinterpret_cast<const f4*>(b);
+#pragma unroll
+    for (int u = 0; u < GPF; u++) {
+        const int i = u * NT + (int)threadIdx.x;
+        L.g[u] = i < n4 ? g4[i] : f4{0.f, 0.f, 0.f, 0.f};
+        L.b[u] = i < n4 ? b4[i] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+// dst = LN(LeakyReLU(src)) over a full-width C-channel tensor (C % 4 == 0; dst may alias src)
+__device__ __forceinline__ void ln_full(const float* src, int sstride, float* dst, int dstride, int HW, int C,
+                                        float mu, float rstd, const LnPre& L, const float* __restrict__ g,
+                                        const float* __restrict__ b) {
+    const int C4 = C >> 2, n4 = HW * C4;
+    const float nmr = -mu * rstd;
+#pragma unroll
+    for (int u = 0; u < GPF; u++) {
+        const int i = u * NT + (int)threadIdx.x;
+        if (i < n4) {
+            const int p = i / C4, c = (i - p * C4) << 2;
+            f4 x = *reinterpret_cast<const f4*>(src + p * sstride + c);
+#pragma unroll
+            for (int j = 0; j < 4; j++) x[j] = fmaf(fmaf(lrelu_(x[j]), rstd, nmr), L.g[u][j], L.b[u][j]);
+            *reinterpret_cast<f4*>(dst + p * dstride + c) = x;
+        }
+    }
+    const f4* g4 = reinterpret_cast<const f4*>(g);
+    const f4* b4 = reinterpret_cast<const f4*>(b);
+    for (int i0 = GPF * NT; i0 < n4; i0 += NT * 8) {
+        f4 gv[8], bv[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            const int p = i / C4, c = (i - p * C4) << 2;
+            gv[u] = i < n4 ? g4[i] : f4{0.f, 0.f, 0.f, 0.f};
+            bv[u] = i < n4 ? b4[i] : f4{0.f, 0.f, 0.f, 0.f};
+            xv[u] = i < n4 ? *reinterpret_cast<const f4*>(src + p * sstride + c) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            if (i >= n4) continue;
+            const int p = i / C4, c = (i - p * C4) << 2;
+            f4 x = xv[u];
+#pragma unroll
+            for (int j = 0; j < 4; j++) x[j] = fmaf(fmaf(lrelu_(x[j]), rstd, nmr), gv[u][j], bv[u][j]);
+            *reinterpret_cast<f4*>(dst + p * dstride + c) = x;
+        }
+    }
+}
+
 // In-place LN(LeakyReLU) over the disjoint channel windows of buf (the grouped branches' inputs)
 // in ONE pass: the elements of all windows are enumerated together, so every gamma/beta load of
 // a thread is in flight at once (one L2 round trip instead of one per window).
@@ -597,6 +656,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
     const int* oend = off + RB0 + a.R * per_rb;
     WPre pf;
+    LnPre lp;
+    // full-width LNs (Y: nk channels, T2: gc channels) take the prefetched path when quad-shaped
+    const bool yq = ln && (nk & 3) == 0, tq = ln && (gc & 3) == 0;
 
     int sti = 0;
     STAMP(sti++);
@@ -620,6 +682,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_load(pf, X + rbo(0)[2], a.ca.size);
         else
             wpf_load(pf, X + oend[2], a.co.size);
+        if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
         conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, X + off[1], sl);
         __syncthreads();
@@ -629,7 +692,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const int* o = rbo(r);
         // LN1(LReLU(y)) -> T2, conv_a (1x1 nk->nk) -> T1 (+ LN2 stats)
         if (ln) lst_final(slots, mu, rstd);
-        ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
+        if (yq)
+            ln_full(Y, SY, T2, S2, HW, nk, mu, rstd, lp, P + o[0], P + o[1]);
+        else
+            ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         wpf_store(pf, WL, X + o[2]);
         __syncthreads();   // every wave has read the Y slots; T2 and W are complete
         lst_zero(slots);
@@ -646,6 +712,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         else
             ln_windows(T1, S1, HW, nk, a.nwin, a.win_off, a.win_len, mu, rstd, ln ? P + o[4] : nullptr,
                        ln ? P + o[5] : nullptr, ln);
+        if (tq) lnp_load(lp, P + o[6], P + o[7], HW * gc / 4);
         // grouped dilated branches -> T2[:, out_off : out_off + cout] (+ LN3 stats over all of them)
         for (int bi = 0; bi < a.nbr; bi++) {
             const LdsConv& cv = a.gcv[bi];
@@ -665,7 +732,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         __syncthreads();
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
         if (ln) lst_final(slots, mu, rstd);
-        ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
+        if (tq)
+            ln_full(T2, S2, T2, S2, HW, gc, mu, rstd, lp, P + o[6], P + o[7]);
+        else
+            ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
         wpf_store(pf, WL, X + o[8]);
         __syncthreads();
         lst_zero(slots);
@@ -673,6 +743,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_load(pf, X + rbo(r + 1)[2], a.ca.size);
         else
             wpf_load(pf, X + oend[2], a.co.size);
+        if (yq)
+            lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
+                     HW * nk / 4);
         STAMP(sti++);
         conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, X + o[9], true, sl);
         __syncthreads();
@@ -682,7 +755,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     {
         const int* o = oend;
         if (ln) lst_final(slots, mu, rstd);
-        ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
+        if (yq)
+            ln_full(Y, SY, Y, SY, HW, nk, mu, rstd, lp, P + o[0], P + o[1]);
+        else
+            ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         STAMP(sti++);
         float* dst = a.so[net] + (size_t)img * HW * a.dc2;
         const float* __restrict__ bias = X + o[3];
