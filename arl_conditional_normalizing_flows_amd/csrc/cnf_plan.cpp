@@ -518,6 +518,16 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     pack(np.co, c.co_fmt, nk, dc2,
                          [=](int k, int n) { return ok + (int64_t)k * dc2 + n; },
                          [=](int n) { return ob + n; });
+                // the streamed kernels produce at most 64 output channels per problem
+                if (!c.use_lds && c.co_fmt != PK_TAP && dc2 > 64) {
+                    for (int c0 = 0; c0 < dc2; c0 += 64) {
+                        const int w = std::min(64, dc2 - c0);
+                        PackedConv pc;
+                        pack(pc, PK_KN, nk, w, [=](int k, int n) { return ok + (int64_t)k * dc2 + c0 + n; },
+                             [=](int n) { return ob + c0 + n; });
+                        np.co_chunks.push_back(pc);
+                    }
+                }
             }
         }
 

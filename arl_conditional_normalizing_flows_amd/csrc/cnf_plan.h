@@ -48,6 +48,7 @@ struct NetParams {
     std::vector<RBParams> rb;
     int64_t ln_out_g = -1, ln_out_b = -1, conv_out_k = -1, conv_out_b = -1, tanh_w = -1;
     PackedConv ci, co;                         // conv_in (PK_KN), conv_out (PK_TAP or PK_KN)
+    std::vector<PackedConv> co_chunks;         // streamed conv_out with > 64 outputs: 64-column PK_KN chunks
 };
 
 // LDS image of k_net_lds (cnf_netlds.hip): Y | T1 | T2 | W | K, byte offsets; pixel strides in floats

@@ -645,11 +645,19 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             set_parts(0, conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr));
         }
     }
-    // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b)
+    // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b); > 64 outputs in 64-channel chunks
     {
         std::vector<ProbSpec> pr;
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];
+            if (!np.co_chunks.empty()) {
+                for (size_t k = 0; k < np.co_chunks.size(); k++)
+                    pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + np.ln_out_g : none,
+                                          ln ? P + np.ln_out_b : none, 1, X + np.co_chunks[k].w,
+                                          X + np.co_chunks[k].b, so[n], c.dc2, (int)(64 * k),
+                                          np.co_chunks[k].cout, none, Slab{}, 0, 1});
+                continue;
+            }
             pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + np.ln_out_g : none,
                                   ln ? P + np.ln_out_b : none, 1, X + np.co.w, X + np.co.b, so[n], c.dc2, 0, c.dc2,
                                   none, Slab{}, 0, 1});

@@ -50,7 +50,9 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          # the streamed (multi-kernel) path for every layer
          # (group_mode='intended' on streamed layers needs the dense grouped image in LDS: small only)
          ('small', 3, 'reference', False), ('small', 2, 'intended', False), ('cfg2', 2, 'reference', False),
-         ('ref_default', 2, 'reference', False)]
+         ('ref_default', 2, 'reference', False),
+         # BASELINE configs[3] / configs[4] architectures (64x64 4-scale, 128x128 5-scale) at a small batch
+         ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True)]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
