@@ -64,6 +64,12 @@ _SIGS = [
     ('cnf_channel_copy', C.c_int, [_F, C.c_int, C.c_int, _F, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, _P]),
     ('cnf_nll', C.c_int, [_P, _F, _F, _F, _F, _F, C.c_int, _P]),
+    ('cnf_plan_train_workspace_bytes', C.c_size_t, [_P, C.c_int]),
+    ('cnf_flow_forward_train', C.c_int, [_P, _F, _F, _F, _F, _F, _P, C.c_int, _P]),
+    ('cnf_flow_backward', C.c_int, [_P, _F, _F, _F, _P, C.c_int, C.c_float, _F, _P]),
+    ('cnf_coupling_backward', C.c_int, [_P, C.c_int, _F, _F, _F, _F, C.c_float, _P, C.c_int, _F, _P]),
+    ('cnf_adam_step', C.c_int, [_F, _F, _F, _F, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
+                                _P]),
     ('cnf_toy_num_params', C.c_int64, [C.POINTER(cnf_toy_desc)]),
     ('cnf_toy_call', C.c_int, [C.POINTER(cnf_toy_desc), _F, _F, _F, _F, _F, C.c_int, C.c_int, _P]),
     ('cnf_toy_nll_sums', C.c_int, [_F, _F, C.c_int, _P]),

@@ -151,4 +151,21 @@ __device__ __forceinline__ void copy_to_lds(const float* __restrict__ src, float
 }
 
 
+// masks (conv_cINN_make_model.py:720-759, 896-1071)
+// position in u (per-image element index) of element (compressed pixel p, channel c) of the
+// compressed half selected by mask m.
+__device__ __forceinline__ int mask_pos(int m, int p, int c, int wc, int W, int D) {
+    const int pr = p / wc, pc = p - pr * wc;
+    if (m < 2) {
+        const int half = c >= D ? 1 : 0;
+        const int ch = c - half * D;
+        // mask 0: c0 -> (even, even), c1 -> (odd, odd); mask 1: c0 -> (even, odd), c1 -> (odd, even)
+        const int dr = half;
+        const int dc = (m == 0) ? half : 1 - half;
+        return ((2 * pr + dr) * W + (2 * pc + dc)) * D + ch;
+    }
+    const int ch = (m == 2) ? 2 * c : 2 * c + 1;
+    return (pr * W + pc) * D + ch;
+}
+
 }  // namespace cnf

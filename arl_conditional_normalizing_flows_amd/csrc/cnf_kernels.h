@@ -143,4 +143,75 @@ void launch_nll(const float* xy, const float* zy, const float* ld, float* per_im
                 int D, int x_d, float lambda_y, hipStream_t st);
 void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st);
 
+
+// ---- training (cnf_train.hip) -------------------------------------------------------------------
+// Generic fp32 convolution for the training path over the dense backward image (taps x k x n):
+//   out[b,p,n] (=|+=) bias[n] + res[b,p,n] + sum_{tap,k} X[b, p + sgn*dil*off(tap), k] * W(tap,k,n)
+// with W(tap,k,n) = w[tap*wt + k*wk + n*wn] and X = LN(LeakyReLU(in)) on load when stats != null
+// (LeakyReLU only when act && !stats). sgn = +1 is the forward conv; sgn = -1 with transposed
+// strides is the data gradient (dX = conv^T dY). Zero padding outside the image.
+struct TConvArgs {
+    const float* in;
+    int in_cs, in_off, K;
+    const float* stats;       // [B][2] (mean, rstd) of LeakyReLU(in) over the whole tensor, or null
+    const float* gamma;       // per element [npx][in_cs] (channel in_off + k)
+    const float* beta;
+    int act;
+    const float* w;
+    long long wt;
+    int wk, wn;
+    const float* bias;        // [N] or null
+    const float* res;         // [B][npx][out_cs] window or null
+    float* out;
+    int out_cs, out_off, N, accumulate;
+    int H, W, taps, dil, sgn, B;
+};
+void launch_tconv(const TConvArgs& a, hipStream_t st);
+
+// weight gradient: part[chunk][(tap*CI + ci)*CO + co] = sum over the chunk's pixels of
+// X[b, p + dil*off(tap), ci] * dY[b, p, co] (X with LN-on-load as in TConvArgs); bpart[chunk][co]
+// = sum dY (bias gradient) when non-null
+struct WGradArgs {
+    const float* x;
+    int x_cs, x_off, CI;
+    const float* stats;
+    const float* gamma;
+    const float* beta;
+    int act;
+    const float* dy;
+    int dy_cs, dy_off, CO;
+    float* part;
+    float* bpart;
+    int H, W, taps, dil, B, chunks, chunk_px;
+};
+void launch_wgrad(const WGradArgs& a, hipStream_t st);
+// dparams[map[i]] += sum_c part[c][i] for i < n (map[i] >= 0)
+void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st);
+void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st);
+// LN + LeakyReLU backward: dx (=|+=) d/dx of LN(LeakyReLU(x)) given dxo = dL/d(LN output);
+// dgamma/dbeta (+=) per element; stats == null: LeakyReLU backward only
+void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
+                        long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
+                        hipStream_t st);
+struct CoupBwArgs {
+    const float* u;           // layer input [B][H][W][D]
+    const float* dv;          // dL/dv
+    const float* s_pre;       // raw conv_out of net A
+    const float* tanh_w;
+    float* du;                // dL/du (u1 positions: dL/dv1 only; the nets' share is added later)
+    float* ds_pre;            // dL/d s_pre  [B][hc][wc][dc2]
+    float* dt;                // dL/dt
+    double* dw_part;          // [B][gridDim.x]
+    float g_ld;               // dL/d(per-image log-det)
+    int H, W, D, mask, mask_c, hc, wc, dc1, dc2;
+};
+void launch_coupling_backward(const CoupBwArgs& a, int B, int nparts, hipStream_t st);
+void launch_scatter_add_u1c(const float* du1c, float* du, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
+                            hipStream_t st);
+void launch_dsum(const double* part, long long n, float* out, hipStream_t st);
+// dL/dzy of the NLL (conv_cINN_make_model.py:1800-1848): z / Bg, lambda_y * sign(y - y') / Bg
+void launch_nll_grad(const float* xy, const float* zy, float* dzy, int B, int HW, int D, int x_d, float lambda_y,
+                     float inv_batch, hipStream_t st);
+void launch_adam(float* params, const float* grads, float* m, float* v, long long n, float alpha, float b1, float b2,
+                 float eps, hipStream_t st);
 }  // namespace cnf

@@ -468,6 +468,19 @@ Plan* build_plan(const cnf_flow_desc* d) {
             for (int n = 0; n < bpad; n++) p.aux_map.push_back(n < cout ? bsrc(n) : -1);
             p.n_aux += bpad;
         };
+        // dense backward image: every conv as [taps][cin][cout] + [cout] bias (training kernels)
+        auto dense_img = [&](PackedConv& pc, int taps, int cin, int cout, const std::function<int64_t(int, int)>& src,
+                             const std::function<int64_t(int)>& bsrc) {
+            pc.taps = taps;
+            pc.dw = p.n_bw;
+            for (int k = 0; k < taps * cin; k++)
+                for (int n = 0; n < cout; n++) p.bw_map.push_back(src(k, n));
+            p.n_bw += (int64_t)taps * cin * cout;
+            pc.db = p.n_bw;
+            for (int n = 0; n < cout; n++) p.bw_map.push_back(bsrc(n));
+            p.n_bw += (cout + 3) / 4 * 4;
+            for (int n = cout; n < (cout + 3) / 4 * 4; n++) p.bw_map.push_back(-1);
+        };
         for (auto& c : p.couplings) {
             for (int net = 0; net < 2; net++) {
                 NetParams& np = c.net[net];
@@ -475,10 +488,14 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 const int nk = c.nk;
                 pack(np.ci, c.ci_fmt, c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
                      [=](int n) { return cib + n; });
+                dense_img(np.ci, ks * ks, c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
+                          [=](int n) { return cib + n; });
                 for (auto& rb : np.rb) {
                     const int64_t ak = rb.conv_a_k, ab = rb.conv_a_b, bk = rb.conv_b_k, bb = rb.conv_b_b;
                     pack(rb.ca, PK_1X1, nk, nk, [=](int ci2, int j) { return ak + (int64_t)ci2 * nk + j; },
                          [=](int n) { return ab + n; });
+                    dense_img(rb.ca, 1, nk, nk, [=](int ci2, int j) { return ak + (int64_t)ci2 * nk + j; },
+                              [=](int n) { return ab + n; });
                     for (size_t bi = 0; bi < c.br.size(); bi++) {
                         const Branch b = c.br[bi];
                         const std::vector<int64_t> gk = rb.gk[bi], gb = rb.gb[bi];
@@ -500,10 +517,13 @@ Plan* build_plan(const cnf_flow_desc* d) {
                                  return ci < b.cin ? dense(tap * b.cin + ci, n) : -1;
                              },
                              [=](int n) { return gb[n / b.width] + (n % b.width); });
+                        dense_img(pc, ks * ks, b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gc.push_back(pc);
                     }
                     pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
                          [=](int n) { return bb + n; });
+                    dense_img(rb.cb, 1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
+                              [=](int n) { return bb + n; });
                 }
                 const int64_t ok = np.conv_out_k, ob = np.conv_out_b;
                 const int dc2 = c.dc2;
@@ -518,6 +538,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     pack(np.co, c.co_fmt, nk, dc2,
                          [=](int k, int n) { return ok + (int64_t)k * dc2 + n; },
                          [=](int n) { return ob + n; });
+                dense_img(np.co, ks * ks, nk, dc2, [=](int k, int n) { return ok + (int64_t)k * dc2 + n; },
+                          [=](int n) { return ob + n; });
                 // the streamed kernels produce at most 64 output channels per problem
                 if (!c.use_lds && c.co_fmt != PK_TAP && dc2 > 64) {
                     for (int c0 = 0; c0 < dc2; c0 += 64) {

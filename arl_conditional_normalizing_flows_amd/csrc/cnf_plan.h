@@ -33,6 +33,9 @@ struct Branch {
 struct PackedConv {
     int fmt = PK_KN, cin = 0, cout = 0, nr = 0, ns = 0, G = 0, kpad = 0;
     int64_t w = -1, b = -1, size = 0;   // offsets (floats) into the kernel image; size of the weight image
+    // training: offsets into the dense backward image (bw image): [taps][cin][cout] weights, [cout] bias
+    int64_t dw = -1, db = -1;
+    int taps = 9;
 };
 
 struct RBParams {
@@ -126,6 +129,17 @@ struct WsLayout {
     int ld_parts = 0;   // log-det partial slots per image per coupling layer
 };
 
+// training workspace (after the inference layout): saved coupling inputs, the dense backward
+// weight image, one coupling layer's recomputed activations and the gradient buffers
+struct TrainLayout {
+    size_t total = 0;
+    std::vector<size_t> save_u;   // per coupling index: its input u [B][H][W][D]
+    size_t bw = 0;
+    size_t ys[2] = {}, t1s[2] = {}, t2s[2] = {}, so[2] = {}, dso[2] = {}, stats[2] = {};
+    size_t dy = 0, dln = 0, dbuf = 0, dt1 = 0, dc = 0, dt2 = 0, u1c = 0, du1c = 0, duv[2] = {}, dzy = 0;
+    size_t lnsum = 0, wpart = 0, bpart = 0, dwpart = 0;
+};
+
 struct Plan {
     cnf_flow_desc desc{};
     std::vector<int> sfbl, rbl, nkl, cl;
@@ -136,6 +150,11 @@ struct Plan {
     int64_t n_aux = 0;
     int64_t aux_zero = 0;           // offset of 128 zero floats in the kernel image
     std::vector<int64_t> aux_map;   // kernel image: aux[i] = params[aux_map[i]] (or 0 if < 0)
+    // training: dense backward image bw[i] = params[bw_map[i]] (0 if < 0); the same map scatters
+    // dense weight gradients back onto the canonical parameters
+    std::vector<int64_t> bw_map;
+    int64_t n_bw = 0;
+    int64_t* dev_bw_map = nullptr;
     std::vector<Boundary> boundaries;
     std::vector<int> final_orig;    // last block layout -> xy position
     int last_n = 0;                 // elements per image of the last block layout
@@ -151,7 +170,16 @@ struct Plan {
     std::vector<Recorded> recorded;
 
     WsLayout layout(int B) const;
+    TrainLayout train_layout(int B) const;
 };
+
+// cnf_train.cpp: dL/dparams of the NLL (loss scaled by inv_batch = 1 / global batch) into dparams,
+// from the coupling inputs saved by the training forward in `workspace`
+void flow_backward(Plan& p, const float* params, const float* xy, const float* zy, void* workspace, int B,
+                   float inv_batch, float* dparams, hipStream_t st);
+// one coupling layer's backward: du, dparams (zeroed first) for dL/dv = dv and dL/d logdet_b = g_ld
+void coupling_layer_backward(Plan& p, int ci, const float* params, const float* u, const float* dv, float* du,
+                             float g_ld, void* workspace, int B, float* dparams, hipStream_t st);
 
 // builds the plan; throws std::invalid_argument with the reference's assertion text
 Plan* build_plan(const cnf_flow_desc* d);

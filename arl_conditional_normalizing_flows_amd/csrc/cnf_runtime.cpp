@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -711,6 +712,11 @@ static void ensure_tables(Plan& p) {
     if (!p.aux_map.empty())
         hip_check(hipMemcpy(p.dev_aux_map, p.aux_map.data(), p.aux_map.size() * sizeof(int64_t), hipMemcpyHostToDevice),
                   "hipMemcpy(aux map)");
+    size_t nbw = std::max<size_t>(1, p.bw_map.size()) * sizeof(int64_t);
+    hip_check(hipMalloc(&p.dev_bw_map, nbw), "hipMalloc(bw map)");
+    if (!p.bw_map.empty())
+        hip_check(hipMemcpy(p.dev_bw_map, p.bw_map.data(), p.bw_map.size() * sizeof(int64_t), hipMemcpyHostToDevice),
+                  "hipMemcpy(bw map)");
     p.device = dev;
 }
 
@@ -746,6 +752,7 @@ void cnf_plan_destroy(cnf_plan* plan) {
     if (plan->p) {
         if (plan->p->dev_table) (void)hipFree(plan->p->dev_table);
         if (plan->p->dev_aux_map) (void)hipFree(plan->p->dev_aux_map);
+        if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
         delete plan->p;
     }
     delete plan;
@@ -820,15 +827,17 @@ size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
     return plan->p->layout(B).total;
 }
 
-int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
-                     float* logdet_per_image, void* workspace, int B, void* stream) {
-    if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !workspace || B <= 0)
-        return fail(CNF_E_INVALID, "null argument or B <= 0");
-    CNF_TRY
-    Plan& p = *plan->p;
+}  // extern "C"
+
+// the forward schedule; save_inputs: also copy every coupling layer's input into the training
+// workspace (cnf_flow_forward_train)
+static void flow_forward(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
+                         float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs) {
     ensure_tables(p);
     p.recorded.clear();
-    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
+    TrainLayout TL;
+    if (save_inputs) TL = p.train_layout(B);
     const WsLayout& L = E.L;
     double* ld = E.at<double>(L.ld);
     float* buf[2] = {E.at<float>(L.uv[0]), E.at<float>(L.uv[1])};
@@ -840,6 +849,14 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
             float* nxt = buf[which];
+            if (save_inputs) {
+                float* dst = E.at<float>(TL.save_u[c.index]);
+                const float* src = cur;
+                const size_t bytes = (size_t)B * c.H * c.W * c.D * 4;
+                E.record("copy", 0, 2.0 * bytes, [=](void* st) {
+                    (void)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)st);
+                });
+            }
             run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1);
             cur = nxt;
             which ^= 1;
@@ -876,6 +893,75 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
         const int nl = (int)p.couplings.size(), np = L.ld_parts;
         E.record("k_ld_reduce", 0, 0, [=](void* st) { launch_ld_reduce(ld, logdet_per_image, B, nl, np, 0, (hipStream_t)st); });
     }
+    check_launch();
+}
+
+extern "C" {
+
+int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
+                     float* logdet_per_image, void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !workspace || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    flow_forward(*plan->p, params, aux, xy, zy, logdet_per_image, workspace, B, (hipStream_t)stream, false);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+size_t cnf_plan_train_workspace_bytes(const cnf_plan* plan, int B) {
+    if (!plan || B <= 0) return 0;
+    try {
+        return plan->p->train_layout(B).total;
+    } catch (...) {
+        return 0;
+    }
+}
+
+int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
+                           float* logdet_per_image, void* train_workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !train_workspace || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    flow_forward(*plan->p, params, aux, xy, zy, logdet_per_image, train_workspace, B, (hipStream_t)stream, true);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, const float* zy, void* train_workspace,
+                      int B, float inv_batch, float* dparams, void* stream) {
+    if (!plan || !params || !xy || !zy || !train_workspace || !dparams || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    flow_backward(p, params, xy, zy, train_workspace, B, inv_batch, dparams, (hipStream_t)stream);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_coupling_backward(cnf_plan* plan, int layer, const float* params, const float* u, const float* dv, float* du,
+                          float dlogdet, void* train_workspace, int B, float* dparams, void* stream) {
+    if (!plan || !params || !u || !dv || !du || !train_workspace || !dparams || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    Plan& p = *plan->p;
+    if (layer < 0 || layer >= (int)p.layers.size() || p.layers[layer].kind != CNF_LAYER_COUPLING)
+        return fail(CNF_E_INVALID, "layer is not a coupling layer");
+    if (du == dv || du == u) return fail(CNF_E_INVALID, "du must not alias u or dv");
+    ensure_tables(p);
+    coupling_layer_backward(p, p.layers[layer].ci, params, u, dv, du, dlogdet, train_workspace, B, dparams,
+                            (hipStream_t)stream);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_adam_step(float* params, const float* grads, float* m, float* v, int64_t n, float lr, float beta_1,
+                  float beta_2, float epsilon, int step, void* stream) {
+    if (!params || !grads || !m || !v || n < 0 || step < 1) return fail(CNF_E_INVALID, "bad argument");
+    CNF_TRY
+    const double b1t = std::pow((double)beta_1, step), b2t = std::pow((double)beta_2, step);
+    const float alpha = (float)((double)lr * std::sqrt(1.0 - b2t) / (1.0 - b1t));
+    if (n > 0) launch_adam(params, grads, m, v, (long long)n, alpha, beta_1, beta_2, epsilon, (hipStream_t)stream);
     check_launch();
     return CNF_OK;
     CNF_CATCH

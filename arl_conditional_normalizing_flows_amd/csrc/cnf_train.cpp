@@ -1,0 +1,387 @@
+// cnf_train.cpp — backward pass of the NLL training step (cFlow.train_step,
+// conv_cINN_make_model.py:1850-1880: tf.GradientTape over log_loss :1800-1848).
+//
+// Gradient of loss = -(mean_b(llz_b + lly_b) + mean_b(logdet_b)) with respect to the canonical
+// parameter vector. The forward (cnf_flow_forward_train) saves every coupling layer's input; the
+// backward walks the layer schedule in reverse:
+//   - layout layers (squeeze / factor-out / final restoration) are permutations: their gradient is
+//     the inverse map applied to dL/dv (the same index tables as cnf_flow_inverse);
+//   - a coupling layer recomputes both s,t networks from its saved input (activations of every
+//     residual block kept for this one layer), runs the coupling-law backward, then each network
+//     in reverse: conv weight gradients (k_wgrad + scatter through the dense map onto the
+//     canonical parameters, so the grouped-conv closure quirk and group boundaries come out
+//     exactly), data gradients (k_tconv with transposed weights), LayerNorm backward with the
+//     per-element gamma/beta gradients.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cnf_kernels.h"
+#include "cnf_plan.h"
+
+namespace cnf {
+
+namespace {
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+void hchk(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// LN-on-load descriptor of a conv input
+struct LnIn {
+    const float* stats = nullptr;
+    const float* gamma = nullptr;
+    const float* beta = nullptr;
+    int act = 0;
+};
+
+int wgrad_chunks(int B, int npx) {
+    const long long total = (long long)B * npx;
+    return (int)std::max<long long>(1, std::min<long long>(64, (total + 511) / 512));
+}
+
+}  // namespace
+
+TrainLayout Plan::train_layout(int B) const {
+    TrainLayout T;
+    const WsLayout L = layout(B);
+    size_t off = align_up(L.total, 256);
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + std::max<size_t>(bytes, 4), 256);
+        return o;
+    };
+    const size_t Bz = (size_t)B;
+    int64_t m_y = 0, m_t1 = 0, m_t2 = 0, m_so = 0, m_nk = 0, m_gc = 0, m_u1 = 0, m_dense = 0, m_co = 0;
+    int m_st = 1;
+    for (const Coupling& c : couplings) {
+        const int64_t npx = (int64_t)c.hc * c.wc;
+        m_y = std::max<int64_t>(m_y, (int64_t)(c.R + 1) * npx * c.nk);
+        m_t1 = std::max<int64_t>(m_t1, (int64_t)c.R * npx * c.nk);
+        m_t2 = std::max<int64_t>(m_t2, (int64_t)c.R * npx * c.gc);
+        m_so = std::max<int64_t>(m_so, npx * c.dc2);
+        m_nk = std::max<int64_t>(m_nk, npx * c.nk);
+        m_gc = std::max<int64_t>(m_gc, npx * c.gc);
+        m_u1 = std::max<int64_t>(m_u1, npx * c.dc1);
+        m_st = std::max(m_st, 3 * c.R + 1);
+        m_dense = std::max<int64_t>(m_dense, 9LL * c.dc1 * c.nk);
+        m_dense = std::max<int64_t>(m_dense, (int64_t)c.nk * c.nk);
+        m_dense = std::max<int64_t>(m_dense, (int64_t)c.gc * c.nk);
+        m_dense = std::max<int64_t>(m_dense, 9LL * c.nk * c.dc2);
+        for (const Branch& b : c.br) m_dense = std::max<int64_t>(m_dense, 9LL * b.cin * b.cout);
+        m_co = std::max<int64_t>(m_co, std::max(std::max(c.nk, c.dc2), c.gc));
+    }
+    T.save_u.assign(couplings.size(), 0);
+    for (const Coupling& c : couplings) T.save_u[c.index] = take(Bz * c.H * c.W * c.D * 4);
+    T.bw = take((size_t)std::max<int64_t>(n_bw, 1) * 4);
+    for (int n = 0; n < 2; n++) {
+        T.ys[n] = take(Bz * m_y * 4);
+        T.t1s[n] = take(Bz * m_t1 * 4);
+        T.t2s[n] = take(Bz * m_t2 * 4);
+        T.so[n] = take(Bz * m_so * 4);
+        T.dso[n] = take(Bz * m_so * 4);
+        T.stats[n] = take(Bz * m_st * 2 * 4);
+    }
+    T.dy = take(Bz * m_nk * 4);
+    T.dln = take(Bz * m_nk * 4);
+    T.dbuf = take(Bz * m_nk * 4);
+    T.dt1 = take(Bz * m_nk * 4);
+    T.dc = take(Bz * m_gc * 4);
+    T.dt2 = take(Bz * m_gc * 4);
+    T.u1c = take(Bz * m_u1 * 4);
+    T.du1c = take(Bz * m_u1 * 4);
+    for (int k = 0; k < 2; k++) T.duv[k] = take(Bz * L.n_uv * 4);
+    T.dzy = take(Bz * L.n_uv * 4);
+    T.lnsum = take(Bz * 2 * 8);
+    int chunks = 1;
+    for (const Coupling& c : couplings) chunks = std::max(chunks, wgrad_chunks(B, c.hc * c.wc));
+    T.wpart = take((size_t)chunks * m_dense * 4);
+    T.bpart = take((size_t)chunks * m_co * 4);
+    T.dwpart = take(Bz * std::max(1, L.ld_parts) * 8);
+    T.total = off;
+    return T;
+}
+
+namespace {
+
+struct TExec {
+    Plan& p;
+    const float* params;
+    float* dparams;
+    char* ws;
+    WsLayout L;
+    TrainLayout T;
+    int B;
+    hipStream_t st;
+    float inv_batch_ = 0.f;
+    const float* bw() const { return reinterpret_cast<const float*>(ws + T.bw); }
+    template <class X>
+    X* at(size_t off) const {
+        return reinterpret_cast<X*>(ws + off);
+    }
+};
+
+// out = conv(in) over the dense image of pc (forward, sgn = +1)
+void conv_fwd(TExec& E, int h, int w, const float* in, int in_cs, int in_off, int K, const LnIn& ln,
+              const PackedConv& pc, int cout, int dil, const float* res, float* out, int out_cs, int out_off) {
+    TConvArgs a{};
+    a.in = in;
+    a.in_cs = in_cs;
+    a.in_off = in_off;
+    a.K = K;
+    a.stats = ln.stats;
+    a.gamma = ln.gamma;
+    a.beta = ln.beta;
+    a.act = ln.act;
+    a.w = E.bw() + pc.dw;
+    a.wt = (long long)K * cout;
+    a.wk = cout;
+    a.wn = 1;
+    a.bias = E.bw() + pc.db;
+    a.res = res;
+    a.out = out;
+    a.out_cs = out_cs;
+    a.out_off = out_off;
+    a.N = cout;
+    a.accumulate = 0;
+    a.H = h;
+    a.W = w;
+    a.taps = pc.taps;
+    a.dil = dil;
+    a.sgn = 1;
+    a.B = E.B;
+    launch_tconv(a, E.st);
+}
+
+// dx (=|+=) conv^T(dy): dy has cout channels at (dy_cs, dy_off), dx gets cin channels at (dx_cs, dx_off)
+void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int cin,
+                int dil, float* dx, int dx_cs, int dx_off, int accumulate) {
+    TConvArgs a{};
+    a.in = dy;
+    a.in_cs = dy_cs;
+    a.in_off = dy_off;
+    a.K = cout;
+    a.w = E.bw() + pc.dw;
+    a.wt = (long long)cin * cout;
+    a.wk = 1;
+    a.wn = cout;
+    a.out = dx;
+    a.out_cs = dx_cs;
+    a.out_off = dx_off;
+    a.N = cin;
+    a.accumulate = accumulate;
+    a.H = h;
+    a.W = w;
+    a.taps = pc.taps;
+    a.dil = dil;
+    a.sgn = -1;
+    a.B = E.B;
+    launch_tconv(a, E.st);
+}
+
+// dW, db of a conv: X (cin channels at x_cs/x_off, LN-on-load) and dY (cout at dy_cs/dy_off)
+void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int cin, const LnIn& ln, const float* dy,
+                int dy_cs, int dy_off, int cout, const PackedConv& pc, int dil) {
+    WGradArgs a{};
+    a.x = x;
+    a.x_cs = x_cs;
+    a.x_off = x_off;
+    a.CI = cin;
+    a.stats = ln.stats;
+    a.gamma = ln.gamma;
+    a.beta = ln.beta;
+    a.act = ln.act;
+    a.dy = dy;
+    a.dy_cs = dy_cs;
+    a.dy_off = dy_off;
+    a.CO = cout;
+    a.part = E.at<float>(E.T.wpart);
+    a.bpart = E.at<float>(E.T.bpart);
+    a.H = h;
+    a.W = w;
+    a.taps = pc.taps;
+    a.dil = dil;
+    a.B = E.B;
+    a.chunks = wgrad_chunks(E.B, h * w);
+    const long long total = (long long)E.B * h * w;
+    a.chunk_px = (int)(((total + a.chunks - 1) / a.chunks + 15) / 16 * 16);
+    launch_wgrad(a, E.st);
+    const int64_t* map = E.p.dev_bw_map;
+    launch_grad_scatter(a.part, a.chunks, (long long)pc.taps * cin * cout, map + pc.dw, E.dparams, E.st);
+    launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
+}
+
+void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
+            int64_t g_off, int64_t b_off) {
+    launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum), n, E.B, 1, dx, accumulate,
+                       ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr, E.st);
+}
+
+void coupling_backward(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
+    const int B = E.B, h = c.hc, w = c.wc, nk = c.nk, gc = c.gc, R = c.R;
+    const int64_t npx = (int64_t)h * w;
+    const bool ln = E.p.desc.layer_norm != 0;
+    const float* P = E.params;
+    float* u1c = E.at<float>(E.T.u1c);
+    launch_gather_u1c(u, u1c, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
+    // activations of both nets: y_r (r = 0..R), t1_r, t2_r; LN stats st[0..R] (y), st[R+1+r] (t1),
+    // st[2R+1+r] (t2), each [B][2]
+    auto Y = [&](int n, int r) { return E.at<float>(E.T.ys[n]) + (size_t)r * B * npx * nk; };
+    auto T1 = [&](int n, int r) { return E.at<float>(E.T.t1s[n]) + (size_t)r * B * npx * nk; };
+    auto T2 = [&](int n, int r) { return E.at<float>(E.T.t2s[n]) + (size_t)r * B * npx * gc; };
+    auto ST = [&](int n, int i) { return E.at<float>(E.T.stats[n]) + (size_t)i * B * 2; };
+    auto lnin = [&](int n, int i, int64_t g, int64_t b) {
+        LnIn l;
+        l.act = 1;
+        if (ln) {
+            l.stats = ST(n, i);
+            l.gamma = P + g;
+            l.beta = P + b;
+        }
+        return l;
+    };
+    const LnIn raw{};
+    for (int n = 0; n < 2; n++) {
+        const NetParams& np = c.net[n];
+        conv_fwd(E, h, w, u1c, c.dc1, 0, c.dc1, raw, np.ci, nk, 1, nullptr, Y(n, 0), nk, 0);
+        if (ln) launch_ln_stats(Y(n, 0), npx * nk, B, 1, ST(n, 0), E.st);
+        for (int r = 0; r < R; r++) {
+            const RBParams& rb = np.rb[r];
+            conv_fwd(E, h, w, Y(n, r), nk, 0, nk, lnin(n, r, rb.ln1g, rb.ln1b), rb.ca, nk, 1, nullptr, T1(n, r), nk, 0);
+            if (ln) launch_ln_stats(T1(n, r), npx * nk, B, 1, ST(n, R + 1 + r), E.st);
+            for (size_t bi = 0; bi < c.br.size(); bi++) {
+                const Branch& b = c.br[bi];
+                conv_fwd(E, h, w, T1(n, r), nk, b.cin_off, b.cin, lnin(n, R + 1 + r, rb.ln2g, rb.ln2b), rb.gc[bi],
+                         b.cout, b.dil, nullptr, T2(n, r), gc, b.out_off);
+            }
+            if (ln) launch_ln_stats(T2(n, r), npx * gc, B, 1, ST(n, 2 * R + 1 + r), E.st);
+            conv_fwd(E, h, w, T2(n, r), gc, 0, gc, lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b), rb.cb, nk, 1, Y(n, r),
+                     Y(n, r + 1), nk, 0);
+            if (ln) launch_ln_stats(Y(n, r + 1), npx * nk, B, 1, ST(n, r + 1), E.st);
+        }
+        conv_fwd(E, h, w, Y(n, R), nk, 0, nk, lnin(n, R, np.ln_out_g, np.ln_out_b), np.co, c.dc2, 1, nullptr,
+                 E.at<float>(E.T.so[n]), c.dc2, 0);
+    }
+    // coupling law backward -> du (u2 part, u1 copy), dL/d s_pre, dL/dt, dL/dw
+    {
+        CoupBwArgs a{};
+        a.u = u;
+        a.dv = dv;
+        a.s_pre = E.at<float>(E.T.so[0]);
+        a.tanh_w = P + c.net[0].tanh_w;
+        a.du = du;
+        a.ds_pre = E.at<float>(E.T.dso[0]);
+        a.dt = E.at<float>(E.T.dso[1]);
+        a.dw_part = E.at<double>(E.T.dwpart);
+        a.g_ld = -E.inv_batch_;
+        a.H = c.H;
+        a.W = c.W;
+        a.D = c.D;
+        a.mask = c.mask;
+        a.mask_c = c.mask_c;
+        a.hc = h;
+        a.wc = w;
+        a.dc1 = c.dc1;
+        a.dc2 = c.dc2;
+        const int np = std::max(1, E.L.ld_parts);
+        launch_coupling_backward(a, B, np, E.st);
+        launch_dsum(a.dw_part, (long long)B * np, E.dparams + c.net[0].tanh_w, E.st);
+    }
+    float* dy = E.at<float>(E.T.dy);
+    float* dln = E.at<float>(E.T.dln);
+    float* dbuf = E.at<float>(E.T.dbuf);
+    float* dt1 = E.at<float>(E.T.dt1);
+    float* dcb = E.at<float>(E.T.dc);
+    float* dt2 = E.at<float>(E.T.dt2);
+    float* du1c = E.at<float>(E.T.du1c);
+    for (int n = 0; n < 2; n++) {
+        const NetParams& np = c.net[n];
+        const float* dso = E.at<float>(E.T.dso[n]);
+        const LnIn lo = lnin(n, R, np.ln_out_g, np.ln_out_b);
+        conv_wgrad(E, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
+        conv_dgrad(E, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
+        ln_bwd(E, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+        for (int r = R - 1; r >= 0; r--) {
+            const RBParams& rb = np.rb[r];
+            // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
+            const LnIn l3 = lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b);
+            conv_wgrad(E, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
+            conv_dgrad(E, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
+            ln_bwd(E, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
+            // grouped dilated branches
+            const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
+            hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, E.st), "hipMemsetAsync");
+            for (size_t bi = 0; bi < c.br.size(); bi++) {
+                const Branch& b = c.br[bi];
+                conv_wgrad(E, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.dil);
+                conv_dgrad(E, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
+            }
+            ln_bwd(E, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
+            // conv_a
+            const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
+            conv_wgrad(E, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
+            conv_dgrad(E, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
+            ln_bwd(E, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
+        }
+        conv_wgrad(E, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
+        conv_dgrad(E, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, n > 0 ? 1 : 0);
+    }
+    launch_scatter_add_u1c(du1c, du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
+}
+
+}  // namespace
+
+void flow_backward(Plan& p, const float* params, const float* xy, const float* zy, void* workspace, int B,
+                   float inv_batch, float* dparams, hipStream_t st) {
+    TExec E{p, params, dparams, (char*)workspace, p.layout(B), p.train_layout(B), B, st};
+    E.inv_batch_ = inv_batch;
+    const WsLayout& L = E.L;
+    const int* T = p.dev_table;
+    if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
+    hchk(hipMemsetAsync(dparams, 0, (size_t)p.n_params * 4, st), "hipMemsetAsync");
+    const int nuv = (int)L.n_uv;
+    const cnf_flow_desc& d = p.desc;
+    float* dzy = E.at<float>(E.T.dzy);
+    launch_nll_grad(xy, zy, dzy, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y, inv_batch, st);
+    float* buf[2] = {E.at<float>(E.T.duv[0]), E.at<float>(E.T.duv[1])};
+    int which = 0;
+    launch_map_gather(dzy, buf[which], T + p.dev_final_orig, p.last_n, nuv, p.last_n, B, st);
+    float* cur = buf[which];
+    which ^= 1;
+    int bi = (int)p.boundaries.size() - 1;
+    for (int li = (int)p.layers.size() - 1; li >= 0; li--) {
+        const Layer& ly = p.layers[li];
+        if (ly.kind == CNF_LAYER_COUPLING) {
+            const Coupling& c = p.couplings[ly.ci];
+            float* nxt = buf[which];
+            coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
+            cur = nxt;
+            which ^= 1;
+        } else if (ly.kind == CNF_LAYER_FACTOR) {
+            const Boundary& b = p.boundaries[bi--];
+            float* prev = buf[which];
+            launch_map_scatter(cur, prev, nullptr, T + b.dev_keep_src, b.n_next, b.n_next, b.n_cur, B, st);
+            launch_map_scatter(dzy, prev, T + b.dev_fac_orig, T + b.dev_fac_src, b.n_fac, nuv, b.n_cur, B, st);
+            cur = prev;
+            which ^= 1;
+        }
+    }
+    hchk(hipGetLastError(), "training kernel launch");
+}
+
+void coupling_layer_backward(Plan& p, int ci, const float* params, const float* u, const float* dv, float* du,
+                             float g_ld, void* workspace, int B, float* dparams, hipStream_t st) {
+    TExec E{p, params, dparams, (char*)workspace, p.layout(B), p.train_layout(B), B, st};
+    E.inv_batch_ = -g_ld;
+    if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
+    hchk(hipMemsetAsync(dparams, 0, (size_t)p.n_params * 4, st), "hipMemsetAsync");
+    coupling_backward(E, p.couplings[ci], u, dv, du);
+    hchk(hipGetLastError(), "training kernel launch");
+}
+
+}  // namespace cnf

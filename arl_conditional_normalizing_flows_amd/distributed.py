@@ -42,3 +42,16 @@ def reduce_nll_sums(sums: torch.Tensor, n_local: int, group=None, all_reduce: bo
     n = buf[4]
     m = buf[:4] / n
     return m[0], m[1], m[2], m[3]
+
+
+def allreduce_grads(grads: torch.Tensor, group=None, bucket_floats: int = 1 << 24) -> torch.Tensor:
+    """Sum the flat gradient over ranks (the training step's exchange, cFlow.train_step on a
+    data-parallel batch). Buckets of up to 64 MiB: large enough to run each ring collective at
+    the xGMI link rate, small enough to bound the staging memory."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return grads
+    flat = grads.reshape(-1)
+    for lo in range(0, flat.numel(), bucket_floats):
+        dist.all_reduce(flat[lo:lo + bucket_floats], group=group)
+    return grads

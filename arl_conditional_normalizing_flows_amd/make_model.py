@@ -227,6 +227,22 @@ class coupling_layer(Layer):
                                                ptr(ws), B, _stream()), 'cnf_coupling_inverse')
         return u, zy
 
+    def gradients(self, u, dv, dlogdet=0.0):
+        """Vector-Jacobian product of forward_and_Jacobian at u: (dL/du, dL/dparams) for
+        dL/dv = dv and dL/d(per-image log-det) = dlogdet (the training backward of this layer;
+        dparams is the flat canonical vector, zero outside this layer's parameters)."""
+        u = self._check(u, 'u')
+        dv = self._check(dv, 'dv')
+        f = self._flow
+        B = u.shape[0]
+        du = torch.empty_like(u)
+        dp = torch.empty(f.num_params, device=u.device, dtype=torch.float32)
+        ws = f._train_workspace(B)
+        check(_lib.load().cnf_coupling_backward(f._plan, self._layer, ptr(f.params), ptr(u), ptr(dv), ptr(du),
+                                                float(dlogdet), ptr(ws), B, ptr(dp), _stream()),
+              'cnf_coupling_backward')
+        return du, dp
+
 
 # ---------------------------------------------------------------------------------------------
 # metrics (keras.metrics.Mean stand-in, :1692-1718)
@@ -491,9 +507,69 @@ class cFlow:
         grp = None if process_group is True else process_group
         return reduce_nll_sums(sums, xy.shape[0], group=grp, all_reduce=process_group is not None)
 
-    def train_step(self, xy):
-        raise NotImplementedError('the NLL training step (backward kernels + Adam) is the next milestone; '
-                                  'see DESIGN.md "Out of scope / next"')
+    # -- training -------------------------------------------------------------------------------
+    def compile(self, optimizer=None):
+        """keras Model.compile(optimizer=Adam(...)) (conv_cINN.py:567-569)."""
+        from .optimizers import Adam
+        self.optimizer = optimizer if optimizer is not None else Adam()
+
+    def _train_workspace(self, B):
+        key = ('train', B)
+        ws = self._ws.get(key)
+        if ws is None:
+            nbytes = int(_lib.load().cnf_plan_train_workspace_bytes(self._plan, B))
+            if nbytes <= 0:
+                raise RuntimeError(_lib.load().cnf_last_error().decode())
+            ws = torch.empty(nbytes, device=self.device, dtype=torch.uint8)
+            self._ws[key] = ws
+        return ws
+
+    def gradients(self, xy, process_group=None):
+        """tape.gradient(loss, trainable_variables) of train_step (:1863-1869) as one flat
+        vector in the canonical parameter order, plus the 4 loss terms (batch means). With
+        process_group (True = default group) the loss sums and the gradient are all-reduced, so
+        both are those of the global batch."""
+        from .distributed import allreduce_grads, pack_nll_sums
+        xy = _as_input(xy, 'xy')
+        if tuple(xy.shape[1:]) != tuple(self.io_shape):
+            raise ValueError(f'input shape {tuple(xy.shape)} != [None, {self.io_shape}]')
+        lib = _lib.load()
+        B = xy.shape[0]
+        ws = self._train_workspace(B)
+        zy = torch.empty_like(xy)
+        ld = torch.empty(B, device=xy.device, dtype=torch.float32)
+        check(lib.cnf_flow_forward_train(self._plan, ptr(self.params), ptr(self._aux), ptr(xy), ptr(zy), ptr(ld),
+                                         ptr(ws), B, _stream()), 'cnf_flow_forward_train')
+        sums, _ = self.nll_sums(xy, zy, ld)
+        buf = pack_nll_sums(sums, B)
+        grp = None if process_group is True else process_group
+        if process_group is not None:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                dist.all_reduce(buf, group=grp)
+        n_global = float(buf[4].item())
+        if getattr(self, '_grads', None) is None or self._grads.numel() != self.num_params:
+            self._grads = torch.empty(self.num_params, device=self.device, dtype=torch.float32)
+        check(lib.cnf_flow_backward(self._plan, ptr(self.params), ptr(xy), ptr(zy), ptr(ws), B, 1.0 / n_global,
+                                    ptr(self._grads), _stream()), 'cnf_flow_backward')
+        if process_group is not None:
+            allreduce_grads(self._grads, group=grp)
+        m = buf[:4] / buf[4]
+        return self._grads, (m[0], m[1], m[2], m[3])
+
+    def train_step(self, xy, process_group=None):
+        """cFlow.train_step (:1850-1880): NLL gradient (GradientTape), optimizer.apply_gradients,
+        Mean trackers; returns {'loss', 'z_loss', 'y_loss', 'detJ_loss'}. Data-parallel with
+        process_group: the loss sums and the gradient are all-reduced over the global batch."""
+        if getattr(self, 'optimizer', None) is None:
+            self.compile()
+        grads, terms = self.gradients(xy, process_group)
+        self.optimizer.apply_flat(self.params, grads)
+        check(_lib.load().cnf_pack_params(self._plan, ptr(self.params), ptr(self._aux), _stream()), 'pack params')
+        vals = torch.stack(list(terms)).cpu().tolist()
+        for t, v in zip(self.metrics, vals):
+            t.update_state(v)
+        return {t.name: t.result() for t in self.metrics}
 
     def test_step(self, xy):
         """:1882-1904 — loss without a weight update; updates the Mean trackers."""

@@ -146,6 +146,41 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
             float* per_image, float* sums, int B, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * NLL training step (cFlow.train_step, :1850-1880: GradientTape over log_loss,
+ * then Adam). Replaces the TF autodiff of the whole log_loss graph.
+ * ------------------------------------------------------------------------- */
+
+/* Training workspace bytes for B images (the inference workspace, the saved
+ * coupling-layer inputs, one layer's recomputed activations, gradient buffers). */
+size_t cnf_plan_train_workspace_bytes(const cnf_plan* plan, int B);
+
+/* cnf_flow_forward that also saves every coupling layer's input into
+ * train_workspace (for cnf_flow_backward on the same xy / zy). */
+int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux,
+                           const float* xy, float* zy, float* logdet_per_image,
+                           void* train_workspace, int B, void* stream);
+
+/* dparams[num_params] = d loss / d params for this shard, where
+ * loss = -(sum_i (llz_i + lly_i + logdet_i)) * inv_batch (inv_batch = 1 / global
+ * batch size: summing dparams over data-parallel shards gives the gradient of the
+ * reference's batch-mean loss). d|y - y'| / dy = sign(y - y') (0 at 0), as TF. */
+int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, const float* zy,
+                      void* train_workspace, int B, float inv_batch, float* dparams, void* stream);
+
+/* Backward of one coupling layer (layer index into layers_list) at input u:
+ * du = dL/du and dparams = dL/dparams (zeroed first; only this layer's entries
+ * are non-zero) for upstream dv = dL/dv and dlogdet = dL/d(per-image log-det). */
+int cnf_coupling_backward(cnf_plan* plan, int layer, const float* params, const float* u,
+                          const float* dv, float* du, float dlogdet, void* train_workspace,
+                          int B, float* dparams, void* stream);
+
+/* Keras Adam (conv_cINN.py:567 Adam(3e-4); keras defaults beta_1 0.9, beta_2 0.999,
+ * epsilon 1e-7): m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);
+ * p -= lr sqrt(1 - b2^t) / (1 - b1^t) * m / (sqrt(v) + eps), t = step >= 1. */
+int cnf_adam_step(float* params, const float* grads, float* m, float* v, int64_t n, float lr,
+                  float beta_1, float beta_2, float epsilon, int step, void* stream);
+
+/* ---------------------------------------------------------------------------
  * TOYcINN (BASELINE configs[0]): the dense conditional flow of
  * TOYcINN_make_model.py:29-506 on 3-dimensional points.
  * ------------------------------------------------------------------------- */

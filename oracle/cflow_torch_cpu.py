@@ -24,7 +24,7 @@ def _conv(x, k, b, d=1):
     """x NHWC, k HWIO -> Keras Conv2D 'same' (symmetric pad for odd k)."""
     kh = k.shape[0]
     pad = (kh - 1) * d // 2
-    y = F.conv2d(x.permute(0, 3, 1, 2), k.permute(3, 2, 0, 1), b, padding=pad, dilation=d)
+    y = F.conv2d(x.permute(0, 3, 1, 2), k.permute(3, 2, 0, 1).contiguous(), b, padding=pad, dilation=d)
     return y.permute(0, 2, 3, 1)
 
 

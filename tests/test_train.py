@@ -1,0 +1,248 @@
+"""NLL training step (cFlow.train_step, conv_cINN_make_model.py:1850-1880).
+
+Gradient oracle: torch autograd (float64) over oracle.cflow_torch_cpu.TorchCPUFlow, the op-for-op
+restatement of the reference graph (its forward is pinned to the numpy oracle in
+tests/test_oracle.py). The autograd conventions that matter are TF's: d|x|/dx = sign(x) (0 at 0),
+LeakyReLU'(x) = 1 if x > 0 else alpha, LayerNorm with biased variance. CPU tests check the oracle's
+gradient against central finite differences and the Keras Adam restatement; the GPU tests compare
+the HIP backward (cnf_flow_backward through the C ABI) per parameter tensor.
+
+Tolerance. The deep configurations are ill-conditioned in fp32 (cfg2 layer c3's net b loses
+~1e-2 relative in some gradients even in torch's own fp32 autograd), so the bar is relative to
+the same graph's fp32 autograd error: per parameter tensor, with g_ref the float64 gradient and
+g32 torch fp32 autograd on the CPU,
+  max|g - g_ref| <= K * max|g32 - g_ref| + GRAD_RTOL * max|g_ref| + GRAD_ATOL * max_all|g_ref|,
+K = K32_LAYER for one coupling layer's backward, K32 for the whole flow. The whole-flow bar adds
+CHAIN_RTOL * max|g_ref|: an ill-conditioned layer (cfg2 c3) turns the 1e-6 relative rounding of
+the GPU forward (zy) into ~5e-4 relative gradient differences in the layers below it, where torch's
+fp32 forward, rounding differently, lands closer by chance; each layer's own backward is held to
+the strict per-layer bar in test_coupling_layer_vjp_matches_oracle."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from arl_conditional_normalizing_flows_amd.config import PRESETS
+from oracle.cflow_np import OracleCFlow, synthetic_class_batch, synthetic_sr_batch
+from oracle.cflow_torch_cpu import TorchCPUFlow
+
+K32 = 10.0        # whole flow: 16 layers of fp32 rounding compound differently than torch's
+K32_LAYER = 4.0   # one coupling layer
+CHAIN_RTOL = 2e-3  # whole flow: the ill-conditioned layer amplifies the fp32 forward's own rounding
+GRAD_RTOL = 1e-4
+GRAD_ATOL = 1e-5
+
+
+def _batch(cfg, B, seed):
+    H, W, D = cfg.io_shape
+    if cfg.data == 'class':
+        return synthetic_class_batch(B, H, W, cfg.x_d, seed=seed)
+    return synthetic_sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=seed)
+
+
+def oracle_grads(kw, P, xy, dtype=torch.float64):
+    """autograd gradient of the reference loss; returns ({name: float64 grad}, loss terms)."""
+    tf = TorchCPUFlow(**kw)
+    T = {k: torch.tensor(np.asarray(v, np.float64), dtype=dtype, requires_grad=True) for k, v in P.items()}
+    terms = tf.log_loss(torch.from_numpy(np.asarray(xy, np.float64)).to(dtype), T)
+    terms[0].backward()
+    return {k: v.grad.double().numpy().copy() for k, v in T.items()}, [float(t.detach()) for t in terms]
+
+
+def _tol(ref, g32, gmax, k=K32):
+    return k * float(np.max(np.abs(g32 - ref))) + GRAD_RTOL * float(np.max(np.abs(ref))) + GRAD_ATOL * gmax
+
+
+def adam_np(p, g, m, v, t, lr=1e-3, b1=0.9, b2=0.999, eps=1e-7):
+    """keras Adam restatement (float64)."""
+    m = m + (g - m) * (1 - b1)
+    v = v + (g * g - v) * (1 - b2)
+    alpha = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    return p - alpha * m / (np.sqrt(v) + eps), m, v
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU: the oracle itself
+# ---------------------------------------------------------------------------------------------
+
+def test_oracle_gradient_matches_finite_differences():
+    cfg = PRESETS['tiny']
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(3)
+    xy = _batch(cfg, 2, 4)
+    G, _ = oracle_grads(kw, P, xy)
+    tf = TorchCPUFlow(**kw)
+    rng = np.random.default_rng(0)
+
+    def loss(Pd):
+        T = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in Pd.items()}
+        return float(tf.log_loss(torch.from_numpy(np.asarray(xy, np.float64)), T)[0])
+
+    names = sorted(P)
+    checked = 0
+    for name in rng.choice(names, size=8, replace=False):
+        a = np.asarray(P[name], np.float64)
+        idx = tuple(int(rng.integers(0, s)) for s in a.shape) if a.shape else ()
+        eps = 1e-6
+        Pp = dict(P)
+        Pm = dict(P)
+        ap, am = a.copy(), a.copy()
+        ap[idx] += eps
+        am[idx] -= eps
+        Pp[name], Pm[name] = ap, am
+        fd = (loss(Pp) - loss(Pm)) / (2 * eps)
+        g = G[name][idx]
+        assert abs(fd - g) <= 1e-4 * max(1.0, abs(g)), (name, idx, fd, g)   # |y - y'| kinks bound the FD accuracy
+        checked += 1
+    assert checked == 8
+
+
+def test_adam_restatement_first_step():
+    # step 1: m = 0.1 g, v = 0.001 g^2, alpha = lr sqrt(0.001)/0.1 -> update ~ lr * sign(g)
+    g = np.array([0.5, -2.0, 1e-2])
+    p, m, v = adam_np(np.zeros(3), g, np.zeros(3), np.zeros(3), 1, lr=1e-2)
+    assert np.allclose(p, -1e-2 * np.sign(g), rtol=1e-3)
+
+
+def test_train_workspace_is_larger_than_inference(lib):
+    from arl_conditional_normalizing_flows_amd import _lib
+    cfg = PRESETS['small']
+    kw = cfg.kwargs()
+    lists = [(C.c_int * len(kw[k]))(*kw[k]) for k in ('squeeze_factor_block_list', 'ResNeXt_block_list',
+                                                        'num_kernels_list', 'cardinality_list')]
+    d = _lib.cnf_flow_desc(*kw['io_shape'], kw['x_d'], len(lists[0]), *lists, 100.0, 3, 1, 1, 0)
+    plan = C.c_void_p()
+    assert lib.cnf_plan_create(C.byref(d), C.byref(plan)) == 0
+    try:
+        inf = lib.cnf_plan_workspace_bytes(plan, 4)
+        tr = lib.cnf_plan_train_workspace_bytes(plan, 4)
+        assert tr > inf > 0
+    finally:
+        lib.cnf_plan_destroy(plan)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: the HIP backward and the training step
+# ---------------------------------------------------------------------------------------------
+
+def _gpu_flow(kw, P, gpu):
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    flow = cFlow(**kw, device=gpu)
+    flow.set_weights(P)
+    return flow
+
+
+GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'intended'}),
+              ('tiny', 2, {'LAYER_NORM': False}), ('cfg2', 2, {})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,B,extra', GRAD_CASES)
+def test_gradients_match_oracle(gpu, name, B, extra):
+    cfg = PRESETS[name]
+    kw = dict(cfg.kwargs(), **extra)
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(5)
+    xy = _batch(cfg, B, 6)
+    G_ref, terms_ref = oracle_grads(kw, P, xy)
+    G32, _ = oracle_grads(kw, P, xy, torch.float32)
+    flow = _gpu_flow(kw, P, gpu)
+    g, terms = flow.gradients(torch.from_numpy(xy).to(gpu))
+    g = g.cpu().numpy().astype(np.float64)
+    terms = [float(t) for t in terms]
+    for r, t in zip(terms_ref, terms):
+        assert abs(r - t) <= 1e-5 * max(1.0, abs(r)) * 10, (terms_ref, terms)
+    gmax = max(float(np.max(np.abs(v))) for v in G_ref.values())
+    worst = (0.0, '')
+    for n, o, s in flow.param_specs:
+        size = int(np.prod(s)) if s else 1
+        ref = np.asarray(G_ref[n], np.float64).reshape(-1)
+        got = g[o:o + size]
+        err = float(np.max(np.abs(got - ref)))
+        tol = _tol(ref, np.asarray(G32[n]).reshape(-1), gmax) + CHAIN_RTOL * float(np.max(np.abs(ref)))
+        worst = max(worst, (err / max(tol, 1e-30), n))
+        assert err <= tol, f'{n}: max|dg| {err:.3e} > tol {tol:.3e} (max|g_ref| {np.max(np.abs(ref)):.3e})'
+    print(f'{name} {extra} B={B}: worst gradient error / tolerance {worst[0]:.3f} ({worst[1]}), max|g| {gmax:.3e}')
+
+
+@pytest.mark.gpu
+def test_train_step_adam_update_and_descent(gpu):
+    from arl_conditional_normalizing_flows_amd.optimizers import Adam
+    cfg = PRESETS['small']
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(7)
+    xy = torch.from_numpy(_batch(cfg, 4, 8)).to(gpu)
+    flow = _gpu_flow(kw, P, gpu)
+    flow.compile(optimizer=Adam(learning_rate=1e-5))
+    p0 = flow.params.detach().cpu().numpy().astype(np.float64)
+    g, _ = flow.gradients(xy)
+    g = g.detach().cpu().numpy().astype(np.float64)
+    out = flow.train_step(xy)
+    assert set(out) == {'loss', 'z_loss', 'y_loss', 'detJ_loss'}
+    p1 = flow.params.detach().cpu().numpy().astype(np.float64)
+    exp, _, _ = adam_np(p0, g, np.zeros_like(g), np.zeros_like(g), 1, lr=1e-5)
+    assert np.max(np.abs(p1 - exp)) <= 1e-6 + 1e-5 * np.max(np.abs(exp))
+    # a few more steps on the same batch lower the loss
+    losses = [out['loss']]
+    for _ in range(5):
+        flow.loss_tracker.reset_state()
+        losses.append(flow.train_step(xy)['loss'])
+    print('train_step losses', losses)
+    assert losses[-1] < losses[0]
+    # forward / inverse still consistent after the update (aux image repacked)
+    zy, _ = flow(xy, 1)
+    x2 = flow(zy, -1)
+    assert float((x2 - xy).abs().max()) <= 1e-4 * float(xy.abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['small', 'cfg2'])
+def test_coupling_layer_vjp_matches_oracle(gpu, name):
+    """Per-layer backward (cnf_coupling_backward) for every coupling layer: random u, dv and
+    dlogdet against torch float64 autograd of the oracle coupling (TorchCPUFlow._coupling)."""
+    cfg = PRESETS[name]
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(9)
+    flow = _gpu_flow(kw, P, gpu)
+    tf = TorchCPUFlow(**kw)
+    couplings = [e.coupling for e in tf.layers if e.kind == 'coupling']
+    layers = [L for L in flow.layers_list if hasattr(L, 'coupling_index')]
+    rng = np.random.default_rng(1)
+    B, g_ld = 2, -0.37
+    worst = []
+    for L, c in zip(layers, couplings):
+        shp = (B, L.input_height, L.input_width, L.input_depth)
+        u = rng.standard_normal(shp)
+        dv = rng.standard_normal(shp)
+        grads = {}
+        for dt in (torch.float64, torch.float32):
+            T = {k: torch.tensor(np.asarray(v, np.float64), dtype=dt, requires_grad=True) for k, v in P.items()
+                 if k.startswith(f'c{c.index}.')}
+            ut = torch.tensor(u, dtype=dt, requires_grad=True)
+            v, ld = tf._coupling(ut, c, T, +1)
+            (torch.sum(v * torch.from_numpy(dv).to(dt)) + g_ld * B * ld).backward()
+            grads[dt] = ({k: t.grad.double().numpy().reshape(-1) for k, t in T.items()}, ut.grad.double().numpy())
+        (G, gu), (G32, gu32) = grads[torch.float64], grads[torch.float32]
+        du, dp = L.gradients(torch.from_numpy(u).float().to(gpu), torch.from_numpy(dv).float().to(gpu), g_ld)
+        du = du.cpu().numpy()
+        dp = dp.cpu().numpy().astype(np.float64)
+        e_u = float(np.max(np.abs(du - gu)))
+        tol_u = _tol(gu, gu32, 0.0, K32_LAYER)
+        gmax = max(float(np.max(np.abs(v))) for v in G.values())
+        rel = 0.0
+        for n, o, s in flow.param_specs:
+            if n not in G:
+                continue
+            size = int(np.prod(s)) if s else 1
+            err = float(np.max(np.abs(dp[o:o + size] - G[n])))
+            tol = _tol(G[n], G32[n], gmax, K32_LAYER)
+            rel = max(rel, err / tol)
+            assert err <= tol, (c.index, n, err, tol, float(np.max(np.abs(G[n]))))
+        worst.append((c.index, e_u / tol_u, rel))
+        assert e_u <= tol_u, (c.index, e_u, tol_u)
+    print(name, ' '.join(f'c{i}: du/tol {a:.2f} dp/tol {b:.2f}' for i, a, b in worst))
