@@ -81,3 +81,47 @@ def test_single_process_reduce_is_local_mean():
     sums = torch.tensor([10.0, 4.0, 2.0, 4.0])
     out = torch.stack(reduce_nll_sums(sums, 4, all_reduce=False))
     assert torch.allclose(out, sums / 4)
+
+
+# ---- training step: data-parallel gradient (cFlow.train_step on a sharded batch) ----------------
+
+def _flat_grad(kw, P, xy, scale):
+    from oracle.cflow_torch_cpu import TorchCPUFlow
+    tf = TorchCPUFlow(**kw)
+    T = {k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in sorted(P.items())}
+    (tf.log_loss(torch.from_numpy(xy), T)[0] * scale).backward()
+    return torch.cat([t.grad.reshape(-1) for t in T.values()])
+
+
+def _grad_worker(rank, world, port, G, out_dir):
+    from arl_conditional_normalizing_flows_amd.distributed import allreduce_grads
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        kw = PRESETS['tiny'].kwargs()
+        P = OracleCFlow(**kw).init_params(2)
+        H, W, D = PRESETS['tiny'].io_shape
+        xy = synthetic_class_batch(G, H, W, PRESETS['tiny'].x_d, seed=3).astype(np.float64)
+        lo, hi = shard_range(G, rank, world)
+        # this shard's loss sum over the global batch size: what cnf_flow_backward computes with
+        # inv_batch = 1 / G; summing over ranks gives the gradient of the global batch mean
+        g = _flat_grad(kw, P, xy[lo:hi], (hi - lo) / G)
+        allreduce_grads(g, bucket_floats=1000)   # several buckets
+        np.save(os.path.join(out_dir, f'g{rank}.npy'), g.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('G', [4, 5])
+def test_gloo_world2_gradient_matches_global_batch(tmp_path, G):
+    world = 2
+    mp.spawn(_grad_worker, args=(world, _free_port(), G, str(tmp_path)), nprocs=world, join=True)
+    kw = PRESETS['tiny'].kwargs()
+    P = OracleCFlow(**kw).init_params(2)
+    H, W, D = PRESETS['tiny'].io_shape
+    xy = synthetic_class_batch(G, H, W, PRESETS['tiny'].x_d, seed=3).astype(np.float64)
+    ref = _flat_grad(kw, P, xy, 1.0).numpy()
+    g0, g1 = np.load(tmp_path / 'g0.npy'), np.load(tmp_path / 'g1.npy')
+    assert np.array_equal(g0, g1)
+    assert np.allclose(g0, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())
