@@ -31,18 +31,43 @@ def needs_build() -> bool:
     return any(p.stat().st_mtime > t for p in deps if p.exists())
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    if not force and not needs_build():
-        return LIB
-    LIB.parent.mkdir(parents=True, exist_ok=True)
-    tmp = LIB.with_suffix('.so.tmp')
-    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared',
-           '-Wno-pass-failed', '-o', str(tmp)] + [str(CSRC / s) for s in SOURCES]
+def _compile(src: Path, obj: Path, verbose: bool) -> None:
+    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wno-pass-failed', '-c',
+           '-o', str(obj), str(src)]
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f'hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')
+        raise RuntimeError(f'hipcc failed on {src.name} ({r.returncode}):\n{r.stdout}\n{r.stderr}')
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every translation unit to an object (in parallel, each only when it or a header
+    changed), then link libcnf_hip.so."""
+    if not force and not needs_build():
+        return LIB
+    from concurrent.futures import ThreadPoolExecutor
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    objdir = PKG / 'build'
+    objdir.mkdir(exist_ok=True)
+    hdr_t = max((CSRC / h).stat().st_mtime for h in HEADERS)
+    hdr_t = max(hdr_t, (PKG.parent / 'include' / 'cnf.h').stat().st_mtime)
+    jobs = []
+    objs = []
+    for s in SOURCES:
+        src, obj = CSRC / s, objdir / (s + '.o')
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
+            jobs.append((src, obj))
+    workers = max(1, min(len(jobs), int(os.environ.get('MAX_JOBS', os.cpu_count() or 4)), 8))
+    with ThreadPoolExecutor(workers) as ex:
+        for f in [ex.submit(_compile, src, obj, verbose) for src, obj in jobs]:
+            f.result()
+    tmp = LIB.with_suffix('.so.tmp')
+    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(tmp)] + [str(o) for o in objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')
     os.replace(tmp, LIB)
     return LIB
 

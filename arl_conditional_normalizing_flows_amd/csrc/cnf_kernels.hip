@@ -466,16 +466,16 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
     const float* __restrict__ tb = a.t + (size_t)img * npx * a.dc2;
     const float w = *a.tanh_w;
     float lsum = 0.f;
-    for (int p = blockIdx.x * 256 + threadIdx.x; p < npx; p += gridDim.x * 256) {
-        for (int c = 0; c < a.dc1; c++) {
-            int e = mask_pos(a.mask, p, c, a.wc, a.W, a.D);
-            vb[e] = ub[e];
-        }
-        for (int c = 0; c < a.dc2; c++) {
-            int e = mask_pos(a.mask_c, p, c, a.wc, a.W, a.D);
-            float s = w * tanhf(sb[p * a.dc2 + c]);
-            float t = tb[p * a.dc2 + c];
-            float x = ub[e];
+    // one thread per element: the transformed half (coalesced s, t reads) first, then the copy of
+    // the conditioning half (small layers have few pixels but many channels per pixel)
+    const int n2 = npx * a.dc2, n1 = npx * a.dc1;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < n2 + n1; e += gridDim.x * 256) {
+        if (e < n2) {
+            const int p = e / a.dc2, c = e - p * a.dc2;
+            const int q = mask_pos(a.mask_c, p, c, a.wc, a.W, a.D);
+            const float s = w * tanhf(sb[e]);
+            const float t = tb[e];
+            const float x = ub[q];
             float y;
             if (a.dir > 0) {
                 y = expf(s) * x + t;
@@ -483,7 +483,12 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
             } else {
                 y = (1.0f / expf(s)) * (x - t);
             }
-            vb[e] = y;
+            vb[q] = y;
+        } else {
+            const int e1 = e - n2;
+            const int p = e1 / a.dc1, c = e1 - p * a.dc1;
+            const int q = mask_pos(a.mask, p, c, a.wc, a.W, a.D);
+            vb[q] = ub[q];
         }
     }
     if (a.ld_part != nullptr) {

@@ -7,16 +7,18 @@ LeakyReLU'(x) = 1 if x > 0 else alpha, LayerNorm with biased variance. CPU tests
 gradient against central finite differences and the Keras Adam restatement; the GPU tests compare
 the HIP backward (cnf_flow_backward through the C ABI) per parameter tensor.
 
-Tolerance. The deep configurations are ill-conditioned in fp32 (cfg2 layer c3's net b loses
-~1e-2 relative in some gradients even in torch's own fp32 autograd), so the bar is relative to
-the same graph's fp32 autograd error: per parameter tensor, with g_ref the float64 gradient and
-g32 torch fp32 autograd on the CPU,
-  max|g - g_ref| <= K * max|g32 - g_ref| + GRAD_RTOL * max|g_ref| + GRAD_ATOL * max_all|g_ref|,
-K = K32_LAYER for one coupling layer's backward, K32 for the whole flow. The whole-flow bar adds
-CHAIN_RTOL * max|g_ref|: an ill-conditioned layer (cfg2 c3) turns the 1e-6 relative rounding of
-the GPU forward (zy) into ~5e-4 relative gradient differences in the layers below it, where torch's
-fp32 forward, rounding differently, lands closer by chance; each layer's own backward is held to
-the strict per-layer bar in test_coupling_layer_vjp_matches_oracle."""
+Tolerance. The loss is piecewise smooth: LeakyReLU (and |y - y'|) have kinks, and the deep
+configurations put millions of activations through them, some within 1e-7 of a kink. An fp32
+forward differs from float64 by ~1e-6 relative, so a few activations sit on the other side of a
+kink and the gradient of whole tensors moves by a DISCRETE amount (cfg2 B=2: float64 autograd
+itself moves by 7.5e-3 relative in layer c11, 2e-1 in c5, when xy is perturbed by 1e-7..1e-6
+relative, while each layer's own VJP at the float64 activations matches to ~1e-6). The bar is
+therefore, per parameter tensor, with g_ref the float64 gradient, g32 torch fp32 autograd and
+spread = max over 4 float64 gradients at xy * (1 + eps * N(0,1)), eps in PERTURB, of |g_pert - g_ref|:
+  max|g - g_ref| <= K * max|g32 - g_ref| + KP * max(spread)
+                    + GRAD_RTOL * max|g_ref| + GRAD_ATOL * max_all|g_ref|,
+K = K32_LAYER for one coupling layer's backward (no perturbation term: the strict per-layer bar of
+test_coupling_layer_vjp_matches_oracle), K32 for the whole flow."""
 import ctypes as C
 import math
 
@@ -30,7 +32,9 @@ from oracle.cflow_torch_cpu import TorchCPUFlow
 
 K32 = 10.0        # whole flow: 16 layers of fp32 rounding compound differently than torch's
 K32_LAYER = 4.0   # one coupling layer
-CHAIN_RTOL = 2e-3  # whole flow: the ill-conditioned layer amplifies the fp32 forward's own rounding
+PERTURB = (1e-7, 1e-6)   # relative input perturbations ~ the fp32 forward's own rounding (2 seeds each)
+PERTURB_CASES = ('cfg2',)  # deep enough for kink flips (the small presets pass without the term)
+KP = 2.0          # whole flow: multiple of the float64 gradient's spread under PERTURB
 GRAD_RTOL = 1e-4
 GRAD_ATOL = 1e-5
 
@@ -149,6 +153,15 @@ def test_gradients_match_oracle(gpu, name, B, extra):
     xy = _batch(cfg, B, 6)
     G_ref, terms_ref = oracle_grads(kw, P, xy)
     G32, _ = oracle_grads(kw, P, xy, torch.float32)
+    # float64 gradient's own spread under input perturbations of the fp32 forward's rounding size
+    G_spread = {k: np.zeros(np.size(v)) for k, v in G_ref.items()}
+    if name in PERTURB_CASES:
+        rng = np.random.default_rng(11)
+        for eps in PERTURB:
+            for _ in range(2):
+                Gp, _ = oracle_grads(kw, P, np.asarray(xy, np.float64) * (1.0 + eps * rng.standard_normal(xy.shape)))
+                for k in G_spread:
+                    G_spread[k] = np.maximum(G_spread[k], np.abs(Gp[k].reshape(-1) - G_ref[k].reshape(-1)))
     flow = _gpu_flow(kw, P, gpu)
     g, terms = flow.gradients(torch.from_numpy(xy).to(gpu))
     g = g.cpu().numpy().astype(np.float64)
@@ -157,15 +170,20 @@ def test_gradients_match_oracle(gpu, name, B, extra):
         assert abs(r - t) <= 1e-5 * max(1.0, abs(r)) * 10, (terms_ref, terms)
     gmax = max(float(np.max(np.abs(v))) for v in G_ref.values())
     worst = (0.0, '')
+    bad = []
     for n, o, s in flow.param_specs:
         size = int(np.prod(s)) if s else 1
         ref = np.asarray(G_ref[n], np.float64).reshape(-1)
         got = g[o:o + size]
+        g32 = np.asarray(G32[n]).reshape(-1)
         err = float(np.max(np.abs(got - ref)))
-        tol = _tol(ref, np.asarray(G32[n]).reshape(-1), gmax) + CHAIN_RTOL * float(np.max(np.abs(ref)))
+        tol = _tol(ref, g32, gmax) + KP * float(np.max(G_spread[n]))
         worst = max(worst, (err / max(tol, 1e-30), n))
-        assert err <= tol, f'{n}: max|dg| {err:.3e} > tol {tol:.3e} (max|g_ref| {np.max(np.abs(ref)):.3e})'
+        if err > tol:
+            bad.append(f'{n}: max|dg| {err:.3e} > tol {tol:.3e} (max|g_ref| {np.max(np.abs(ref)):.3e}, '
+                       f'fp32 autograd err {np.max(np.abs(g32 - ref)):.3e})')
     print(f'{name} {extra} B={B}: worst gradient error / tolerance {worst[0]:.3f} ({worst[1]}), max|g| {gmax:.3e}')
+    assert not bad, '\n'.join(bad)
 
 
 @pytest.mark.gpu
@@ -246,3 +264,69 @@ def test_coupling_layer_vjp_matches_oracle(gpu, name):
         worst.append((c.index, e_u / tol_u, rel))
         assert e_u <= tol_u, (c.index, e_u, tol_u)
     print(name, ' '.join(f'c{i}: du/tol {a:.2f} dp/tol {b:.2f}' for i, a, b in worst))
+
+
+@pytest.mark.gpu
+def test_flow_layer_vjps_at_oracle_activations(gpu):
+    """Every coupling layer's HIP backward at the TRUE activations of a cfg2 flow: u = the float64
+    forward's input to the layer, dv = the float64 gradient of the reference loss at its output,
+    per-image log-det cotangent -1/B (loss = -(mean ll + mean log-det)). Isolates the backward
+    kernels from the kink flips of the whole-flow comparison (module docstring): strict per-layer
+    bar against float64 and torch fp32 autograd of the same layer."""
+    cfg = PRESETS['cfg2']
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(5)
+    B = 2
+    xy = _batch(cfg, B, 6)
+    tf = TorchCPUFlow(**kw)
+    T = {k: torch.tensor(np.asarray(v, np.float64), requires_grad=True) for k, v in P.items()}
+    ins, outs = [], []
+    orig = tf._coupling
+
+    def rec(u, c, PP, d):
+        v, ld = orig(u, c, PP, d)
+        v.retain_grad()
+        ins.append(u.detach().numpy().copy())
+        outs.append(v)
+        return v, ld
+    tf._coupling = rec
+    try:
+        tf.log_loss(torch.from_numpy(np.asarray(xy, np.float64)), T)[0].backward()
+    finally:
+        tf._coupling = orig
+    flow = _gpu_flow(kw, P, gpu)
+    layers = [L for L in flow.layers_list if hasattr(L, 'coupling_index')]
+    couplings = [e.coupling for e in tf.layers if e.kind == 'coupling']
+    assert len(layers) == len(couplings) == len(ins) == 16
+    g_ld = -1.0 / B
+    report = []
+    for L, c, u, v in zip(layers, couplings, ins, outs):
+        dv = v.grad.numpy()
+        grads = {}
+        for dt in (torch.float64, torch.float32):
+            TT = {k: torch.tensor(np.asarray(x, np.float64), dtype=dt, requires_grad=True) for k, x in P.items()
+                  if k.startswith(f'c{c.index}.')}
+            ut = torch.tensor(u, dtype=dt, requires_grad=True)
+            vv, ld = tf._coupling(ut, c, TT, +1)
+            (torch.sum(vv * torch.from_numpy(dv).to(dt)) + g_ld * B * ld).backward()
+            grads[dt] = ({k: t.grad.double().numpy().reshape(-1) for k, t in TT.items()}, ut.grad.double().numpy())
+        (G, gu), (G32, gu32) = grads[torch.float64], grads[torch.float32]
+        du, dp = L.gradients(torch.from_numpy(u).float().to(gpu), torch.from_numpy(dv).float().to(gpu), g_ld)
+        du = du.cpu().numpy().astype(np.float64)
+        dp = dp.cpu().numpy().astype(np.float64)
+        gmax = max(float(np.max(np.abs(x))) for x in G.values())
+        rel = 0.0
+        for n, o, s in flow.param_specs:
+            if n not in G:
+                continue
+            size = int(np.prod(s)) if s else 1
+            err = float(np.max(np.abs(dp[o:o + size] - G[n])))
+            tol = _tol(G[n], G32[n], gmax, K32_LAYER)
+            rel = max(rel, err / tol)
+            assert err <= tol, (c.index, n, err, tol)
+        e_u = float(np.max(np.abs(du - gu)))
+        tol_u = _tol(gu, gu32, 0.0, K32_LAYER)
+        assert e_u <= tol_u, (c.index, e_u, tol_u)
+        report.append(f'c{c.index}: du/tol {e_u / tol_u:.2f} dp/tol {rel:.2f}')
+    print(' '.join(report))
