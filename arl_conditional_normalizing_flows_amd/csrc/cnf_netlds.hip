@@ -104,21 +104,27 @@ __device__ __forceinline__ void lst_flush(const LStat& a, double* slots) {
         }
     }
 }
-// (mean, rstd) of the tensor from the NW slots (every wave, after the producer's barrier)
+// (mean, rstd) of the tensor from the NW slots (every wave, after the producer's barrier). Every
+// lane reads all slots (uniform-address LDS broadcasts) and merges them in the same fixed order:
+// one LDS round trip and a short fp64 chain, no cross-lane shuffles. Single-pass fp64 form
+// (M2 = sum(M2_i + n_i m_i^2) - N mean^2): fp64 keeps > 1e-10 relative even at |mean| = 1e3 std.
 __device__ __forceinline__ void lst_final(const double* slots, float& mu, float& rstd) {
-    const int lane = threadIdx.x & 63;
-    double n = 0.0, m = 0.0, M2 = 0.0;
-    if (lane < NW) {
-        n = slots[3 * lane];
-        m = slots[3 * lane + 1];
-        M2 = slots[3 * lane + 2];
+    double q[3 * NW];
+#pragma unroll
+    for (int i = 0; i < 3 * NW; i++) q[i] = slots[i];
+    double N = 0.0, S = 0.0, Q = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const double n = q[3 * w], m = q[3 * w + 1];
+        N += n;
+        S = fma(n, m, S);
+        Q += fma(n * m, m, q[3 * w + 2]);
     }
-    const double N = wsum_d(n);
-    const double mean = wsum_d(n * m) / N;
-    const double d = m - mean;
-    const double M2t = wsum_d(M2 + n * d * d);
+    const double mean = S / N;
+    double var = Q / N - mean * mean;
+    if (var < 0.0) var = 0.0;
     mu = (float)mean;
-    rstd = (float)(1.0 / sqrt(M2t / N + (double)LN_EPS));
+    rstd = (float)(1.0 / sqrt(var + (double)LN_EPS));
 }
 
 // dst[p][c] = LN(LeakyReLU(src[p][c])) for channels [c0, c0+nc) of a C_ln-channel LN tensor;
@@ -662,7 +668,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
 
     int sti = 0;
     STAMP(sti++);
-    wpf_load(pf, X + off[0], a.ci.size);
+    // packed conv images carry their bias right behind the weights (cnf_plan.cpp pack()): one
+    // copy stages both, and every conv reads its bias from LDS
+    auto wb = [](const LdsConv& cv, int cout) { return cv.size + ((cout + 3) & ~3); };
+    wpf_load(pf, X + off[0], wb(a.ci, nk));
     // gather u1c (mask compress) into T2 (stride SU)
     {
         const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
@@ -679,12 +688,12 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         lst_zero(slots);
         __syncthreads();
         if (a.R > 0)
-            wpf_load(pf, X + rbo(0)[2], a.ca.size);
+            wpf_load(pf, X + rbo(0)[2], wb(a.ca, nk));
         else
-            wpf_load(pf, X + oend[2], a.co.size);
+            wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
         if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
-        conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, X + off[1], sl);
+        conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, sl);
         __syncthreads();
         STAMP(sti++);
     }
@@ -699,9 +708,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         wpf_store(pf, WL, X + o[2]);
         __syncthreads();   // every wave has read the Y slots; T2 and W are complete
         lst_zero(slots);
-        wpf_load(pf, X + o[10], a.gcv[0].size);
+        wpf_load(pf, X + o[10], wb(a.gcv[0], a.br_cout[0]));
         STAMP(sti++);
-        conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, X + o[3], false, sl);
+        conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
         __syncthreads();
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
@@ -722,11 +731,11 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_store(pf, WL, X + o[10 + 2 * bi]);
             __syncthreads();
             if (bi + 1 < a.nbr)
-                wpf_load(pf, X + o[10 + 2 * (bi + 1)], a.gcv[bi + 1].size);
+                wpf_load(pf, X + o[10 + 2 * (bi + 1)], wb(a.gcv[bi + 1], a.br_cout[bi + 1]));
             else
-                wpf_load(pf, X + o[8], a.cb.size);
+                wpf_load(pf, X + o[8], wb(a.cb, nk));
             STAMP(sti++);
-            conv3_run(cv, T1, S1, H, W, WL, KT, T2 + a.br_out_off[bi], S2, a.br_cout[bi], X + o[11 + 2 * bi], sl);
+            conv3_run(cv, T1, S1, H, W, WL, KT, T2 + a.br_out_off[bi], S2, a.br_cout[bi], WL + cv.size, sl);
             STAMP(sti++);
         }
         __syncthreads();
@@ -740,14 +749,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         __syncthreads();
         lst_zero(slots);
         if (r + 1 < a.R)
-            wpf_load(pf, X + rbo(r + 1)[2], a.ca.size);
+            wpf_load(pf, X + rbo(r + 1)[2], wb(a.ca, nk));
         else
-            wpf_load(pf, X + oend[2], a.co.size);
+            wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
         if (yq)
             lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
                      HW * nk / 4);
         STAMP(sti++);
-        conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, X + o[9], true, sl);
+        conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, sl);
         __syncthreads();
         STAMP(sti++);
     }
@@ -761,7 +770,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         STAMP(sti++);
         float* dst = a.so[net] + (size_t)img * HW * a.dc2;
-        const float* __restrict__ bias = X + o[3];
+        const float* bias = WL + a.co.size;
         if (a.co.fmt == PK_TAP) {
             // tap-decomposed: C[p][(tap, o)] = sum_c y[p][c] W[tap][c][o] (1x1 GEMM, scratch over T1..T2),
             // out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]

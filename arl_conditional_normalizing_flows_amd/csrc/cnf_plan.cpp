@@ -99,7 +99,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     int kmax = 4, kp;
     auto acc = [&](int fmt, int ks, int cin, int cout) {
         packed_dims(fmt, ks, cin, cout, sz, kp);
-        wmax = std::max(wmax, sz);
+        wmax = std::max(wmax, sz + (cout + 3) / 4 * 4);   // the bias follows the weights in LDS
         if (fmt == PK_KN || fmt == PK_Q4) kmax = std::max(kmax, fmt == PK_Q4 ? kp / 4 : kp);   // tap / quad table
     };
     acc(ci_fmt, 3, c.dc1, c.nk);
