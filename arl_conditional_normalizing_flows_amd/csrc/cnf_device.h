@@ -14,10 +14,21 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
 __device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
 
+// Wave-wide fp32 sum by DPP lane moves (quad_perm, row_shr, row_bcast: a few cycles each instead
+// of an LDS-routed ds_bpermute per step); lane 63 ends with the total, broadcast by readlane.
+// Out-of-range source lanes read 0 (update_dpp with old = 0). Fixed order: bitwise reproducible.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v += dpp_f<0xb1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f<0x4e>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f<0x114>(v);   // row_shr:4
+    v += dpp_f<0x118>(v);   // row_shr:8   -> lane 15 of each row holds the row sum
+    v += dpp_f<0x142>(v);   // row_bcast:15
+    v += dpp_f<0x143>(v);   // row_bcast:31 -> lane 63 holds the wave sum
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 
 // raw buffer resource over [base, base + bytes): loads beyond the range return 0, stores beyond it

@@ -18,11 +18,9 @@
 #include <cstdint>
 #include <cstdlib>
 
-#include "cnf_kernels.h"
+#include "cnf_device.h"
 
 namespace cnf {
-
-typedef float f4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -39,11 +37,7 @@ constexpr int NT = NW * 64;         // threads
 // LeakyReLU(0.3) as max(x, 0.3x) (2 VALU ops; equal to the select form for every finite x)
 __device__ __forceinline__ float lrelu_(float x) { return __builtin_fmaxf(x, LRELU_ALPHA * x); }
 
-__device__ __forceinline__ float wsum_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ float wsum_f(float v) { return wave_sum_f(v); }   // DPP (cnf_device.h)
 __device__ __forceinline__ double wsum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
