@@ -589,6 +589,9 @@ __device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, 
     }
 }
 
+// entries of the tap (PK_KN) / quad (PK_Q4) table of a 3x3 conv, rounded to 4
+__device__ __forceinline__ int ktab_len(const LdsConv& cv) { return cv.fmt == PK_Q4 ? cv.kpad / 4 : cv.kpad; }
+
 // build the table a 3x3 conv of format fmt needs (caller barriers before the conv)
 __device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin, int ic0, int d) {
     if (cv.fmt == PK_Q4)
@@ -665,6 +668,11 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     // packed conv images carry their bias right behind the weights (cnf_plan.cpp pack()): one
     // copy stages both, and every conv reads its bias from LDS
     auto wb = [](const LdsConv& cv, int cout) { return cv.size + ((cout + 3) & ~3); };
+    // floats of all branch images of a residual block (contiguous from offs[10])
+    auto brw = [&](const int* o) {
+        const int l = a.nbr - 1;
+        return o[11 + 2 * l] + ((a.br_cout[l] + 3) & ~3) - o[10];
+    };
     wpf_load(pf, X + off[0], wb(a.ci, nk));
     // gather u1c (mask compress) into T2 (stride SU)
     {
@@ -702,7 +710,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         wpf_store(pf, WL, X + o[2]);
         __syncthreads();   // every wave has read the Y slots; T2 and W are complete
         lst_zero(slots);
-        wpf_load(pf, X + o[10], wb(a.gcv[0], a.br_cout[0]));
+        wpf_load(pf, X + o[10], brw(o));
         STAMP(sti++);
         conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
         __syncthreads();
@@ -717,21 +725,33 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                        ln ? P + o[5] : nullptr, ln);
         if (tq) lnp_load(lp, P + o[6], P + o[7], HW * gc / 4);
         // grouped dilated branches -> T2[:, out_off : out_off + cout] (+ LN3 stats over all of them)
-        for (int bi = 0; bi < a.nbr; bi++) {
-            const LdsConv& cv = a.gcv[bi];
-            __syncthreads();   // previous branch (or LN2 apply + slot reads) retired
-            if (bi == 0) lst_zero(slots);
-            conv3_table(cv, KT, a.br_cin[bi], a.br_cin_off[bi], a.br_dil[bi]);
-            wpf_store(pf, WL, X + o[10 + 2 * bi]);
-            __syncthreads();
-            if (bi + 1 < a.nbr)
-                wpf_load(pf, X + o[10 + 2 * (bi + 1)], wb(a.gcv[bi + 1], a.br_cout[bi + 1]));
-            else
-                wpf_load(pf, X + o[8], wb(a.cb, nk));
-            STAMP(sti++);
-            conv3_run(cv, T1, S1, H, W, WL, KT, T2 + a.br_out_off[bi], S2, a.br_cout[bi], WL + cv.size, sl);
-            STAMP(sti++);
+        // every branch's packed image (contiguous in aux: weights + bias per branch) and tap / quad
+        // table staged at once: the branches run back to back without barriers between them (they
+        // read T1 and write disjoint T2 slices), each wave merging its LN3 partials across them
+        {
+            int kto = 0;
+            for (int bi = 0; bi < a.nbr; bi++) {
+                const LdsConv& cv = a.gcv[bi];
+                conv3_table(cv, KT + kto, a.br_cin[bi], a.br_cin_off[bi], a.br_dil[bi]);
+                kto += ktab_len(cv);
+            }
         }
+        wpf_store(pf, WL, X + o[10]);
+        __syncthreads();   // LN2 applied, slots read, branch images and tables complete
+        lst_zero(slots);
+        wpf_load(pf, X + o[8], wb(a.cb, nk));
+        STAMP(sti++);
+        {
+            int kto = 0;
+            for (int bi = 0; bi < a.nbr; bi++) {
+                const LdsConv& cv = a.gcv[bi];
+                const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
+                conv3_run(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
+                          WL + (o[11 + 2 * bi] - o[10]), sl);
+                kto += ktab_len(cv);
+            }
+        }
+        STAMP(sti++);
         __syncthreads();
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
         if (ln) lst_final(slots, mu, rstd);

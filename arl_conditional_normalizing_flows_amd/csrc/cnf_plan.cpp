@@ -107,7 +107,17 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     if (c.R > 0) {
         acc(PK_1X1, 1, c.nk, c.nk);
         acc(PK_1X1, 1, c.gc, c.nk);
-        for (size_t bi = 0; bi < c.br.size(); bi++) acc(gc_fmt[bi], 3, c.br[bi].cin, c.br[bi].cout);
+        // the grouped branches are staged together: images back to back, tables back to back
+        int64_t wsum = 0;
+        int ksum = 0;
+        for (size_t bi = 0; bi < c.br.size(); bi++) {
+            const int cin_pk = gc_fmt[bi] == PK_Q4 ? (c.br[bi].cin + 3) / 4 * 4 : c.br[bi].cin;
+            packed_dims(gc_fmt[bi], 3, cin_pk, c.br[bi].cout, sz, kp);
+            wsum += sz + (c.br[bi].cout + 3) / 4 * 4;
+            ksum += gc_fmt[bi] == PK_Q4 ? kp / 4 : kp;
+        }
+        wmax = std::max(wmax, wsum);
+        kmax = std::max(kmax, ksum);
     }
     int64_t off = 512;   // LN-statistics slots (NW x 3 doubles, NW <= 16)
     g.off_y = (int)off;
