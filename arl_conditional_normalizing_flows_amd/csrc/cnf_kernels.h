@@ -103,6 +103,7 @@ struct GcArgs {
     const float* b[2][GC_MAXBR];
     GcBranch br[GC_MAXBR];
     int nbr, H, W, in_cs, out_cs, B, TH, tiles_per_img, ipw, in_nparts, part_stride;
+    int band_bytes;              // offset of the second band buffer (double-buffered staging)
 };
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st);
 int read_gc_stamps(long long* host, int n);

@@ -411,10 +411,14 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 }
                 int64_t quads = 0;   // staged band quads: at most 4 per thread of the 512-thread workgroup
                 for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
-                if (!ok || off > 80 * 1024 || quads > 4 * 512 || !allow_gc) continue;
+                // two band buffers: the next image is staged while the current one is computed
+                const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
+                off += band_bytes;
+                if (!ok || off > 160 * 1024 || quads > 4 * 512 || !allow_gc) continue;
                 c.gc_fused = true;
                 c.gc_TH = TH;
                 c.gc_lds = (int)off;
+                c.gc_band_bytes = (int)band_bytes;
                 c.gcb = gb;
                 for (size_t i = 0; i < c.br.size(); i++) c.gc_fmt[i] = PK_Q4;
             }

@@ -79,6 +79,7 @@ struct Coupling {
     NetLdsGeom lds;                       // valid when use_lds
     bool gc_fused = false;                // streamed layer: grouped stage as one k_gc launch (PK_Q4, padded cin)
     int gc_TH = 0, gc_lds = 0;            // k_gc tile rows, LDS bytes per workgroup
+    int gc_band_bytes = 0;                // k_gc: bytes of one set of branch bands (buffer 1 follows buffer 0)
     std::vector<GcBranch> gcb;            // k_gc branch geometry (offsets into LDS)
 };
 

@@ -607,9 +607,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
             ga.in_nparts = sl[0][1].nparts;
             ga.part_stride = L.st_parts;
-            // images per workgroup: the launch fits one dispatch round at 2 workgroups per CU
+            // images per workgroup: one workgroup per CU, looping over its images with the next
+            // image's band staged behind the current one's MFMAs
             const int64_t units = (int64_t)ga.tiles_per_img * 2 * B;
-            ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+            ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
+            ga.band_bytes = c.gc_band_bytes;
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::atoi(e));   // tuning override
             if (8 * ga.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);

@@ -199,11 +199,11 @@ constexpr int GC_NT = 64 * GC_NW;   // threads
 template <int NR>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, const unsigned char* smem,
                                           const float* __restrict__ bias, float* __restrict__ outp, int npx,
-                                          int px0, LnAcc& st, bool& first, bool stats) {
+                                          int px0, LnAcc& st, bool& first, bool stats, int boff) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     constexpr int NSJ = 16 * NR;
-    const float* band = reinterpret_cast<const float*>(smem + br.band_off);
+    const float* band = reinterpret_cast<const float*>(smem + br.band_off + boff);
     const float* lw = reinterpret_cast<const float*>(smem + br.w_off);
     const int* qo = reinterpret_cast<const int*>(smem + br.q_off);
     float bz[NR];
@@ -215,39 +215,73 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
         bz[n] = chv[n] ? bias[ch] : 0.f;
     }
     const int nsub = (npx + 15) >> 4;
-    for (int s = wave; s < nsub; s += GC_NW) {
-        const int pt = s * 16 + i16;
-        const int ptc = pt < npx ? pt : 0;
-        const int tr = ptc / a.W, tc = ptc - tr * a.W;
-        const float* base = band + (tr * br.BW + tc) * br.S;
-        f4 acc[NR];
+    // two subtiles per wave and pass (s0, s0 + GC_NW) share every B read: two independent MFMA
+    // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
+    constexpr int GQ = 6;
+    const int G = br.G;
+    const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
+    for (int s0 = wave; s0 < nsub; s0 += 2 * GC_NW) {
+        const int s1 = s0 + GC_NW;
+        const bool v1 = s1 < nsub;
+        const float* base[2];
 #pragma unroll
-        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
-        const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
-        for (int g = 0; g < br.G; g++) {
-            const f4 av = *reinterpret_cast<const f4*>(base + qo[4 * g + kq]);
-            f4 bq[NR];
+        for (int h = 0; h < 2; h++) {
+            const int pt = (h ? s1 : s0) * 16 + i16;
+            const int ptc = pt < npx ? pt : 0;
+            const int tr = ptc / a.W, tc = ptc - tr * a.W;
+            base[h] = band + (tr * br.BW + tc) * br.S;
+        }
+        f4 acc0[NR], acc1[NR];
 #pragma unroll
-            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
+        for (int n = 0; n < NR; n++) {
+            acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
+            acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+        for (int g0 = 0; g0 < G; g0 += GQ) {
+            int qv[GQ];
 #pragma unroll
-            for (int q = 0; q < 4; q++)
+            for (int j = 0; j < GQ; j++) qv[j] = g0 + j < G ? qo[4 * (g0 + j) + kq] : 0;
+            f4 a0[GQ], a1[GQ];
 #pragma unroll
-                for (int n = 0; n < NR; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bq[n][q], acc[n], 0, 0, 0);
+            for (int j = 0; j < GQ; j++) {
+                a0[j] = *reinterpret_cast<const f4*>(base[0] + qv[j]);
+                a1[j] = *reinterpret_cast<const f4*>(base[1] + qv[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < GQ; j++) {
+                if (g0 + j >= G) break;
+                const int g = g0 + j;
+                f4 bq[NR];
+#pragma unroll
+                for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int n = 0; n < NR; n++) {
+                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][q], bq[n][q], acc0[n], 0, 0, 0);
+                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][q], bq[n][q], acc1[n], 0, 0, 0);
+                    }
+            }
         }
         if (stats && first) {
-            st.set_shift(lrelu(acc[0][0] + bz[0]));
+            st.set_shift(lrelu(acc0[0][0] + bz[0]));
             first = false;
         }
 #pragma unroll
-        for (int n = 0; n < NR; n++)
+        for (int h = 0; h < 2; h++) {
+            if (h == 1 && !v1) break;
+            const int sb = h ? s1 : s0;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int po = s * 16 + kq * 4 + r;
-                const bool ok = chv[n] && po < npx;
-                const float v = acc[n][r] + bz[n];
-                if (ok) outp[(size_t)(px0 + po) * a.out_cs + br.out_off + n * 16 + i16] = v;
-                if (stats) st.add(lrelu(v), ok);
-            }
+            for (int n = 0; n < NR; n++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int po = sb * 16 + kq * 4 + r;
+                    const bool ok = chv[n] && po < npx;
+                    const float v = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
+                    if (ok) outp[(size_t)(px0 + po) * a.out_cs + br.out_off + n * 16 + i16] = v;
+                    if (stats) st.add(lrelu(v), ok);
+                }
+        }
     }
 }
 
@@ -266,7 +300,11 @@ __device__ long long g_gc_stamps[64];
 #define GSTAMP(i) do { } while (0)
 #endif
 
-__global__ __launch_bounds__(GC_NT, 2) void k_gc(GcArgs a) {
+// One workgroup per CU: a tile of TH rows of one net, looping over `ipw` images. The bands are
+// double-buffered: the next image's t1 quads are loaded into registers before the current image's
+// MFMAs and written (LN2 + LeakyReLU applied) into the other buffer after them, so the staging
+// latency hides behind the compute; the tile's LN2 gamma/beta stay in registers for all images.
+__global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
     const int tile = blockIdx.x % a.tiles_per_img;
@@ -324,6 +362,38 @@ __global__ __launch_bounds__(GC_NT, 2) void k_gc(GcArgs a) {
         }
         return v;
     };
+    // tile LN2 gamma/beta (image-independent) and the first image's raw quads, all in flight together
+    f4 gq[GC_GQ], bq[GC_GQ], xq[GC_GQ];
+#pragma unroll
+    for (int u = 0; u < GC_GQ; u++) {
+        gq[u] = ln ? load_q(a.gamma[net], u) : f4{1.f, 1.f, 1.f, 1.f};
+        bq[u] = ln ? load_q(a.beta[net], u) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto load_img = [&](int ii) {
+        const float* __restrict__ src = a.in[net] + (size_t)(img0 + ii) * HW * a.in_cs;
+#pragma unroll
+        for (int u = 0; u < GC_GQ; u++) xq[u] = load_q(src, u);
+    };
+    // LN2(LeakyReLU(t1)) of the quads in xq -> band buffer (ii & 1); zero outside the image / window
+    auto store_img = [&](int ii) {
+        const float rs = ln ? lstat[2 * ii + 1] : 1.f;
+        const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
+        float* dst = lds_f + (ii & 1) * (a.band_bytes / 4);
+#pragma unroll
+        for (int u = 0; u < GC_GQ; u++) {
+            if (loff[u] < 0) continue;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (nv[u] != 0) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float t = lrelu(xq[u][j]);
+                    v[j] = ln ? fmaf(fmaf(t, rs, nmr), gq[u][j], bq[u][j]) : t;
+                }
+            }
+            *reinterpret_cast<f4*>(dst + loff[u]) = v;
+        }
+    };
+    load_img(0);
     // packed weights and quad-offset tables of every branch (once per workgroup)
     for (int bi = 0; bi < a.nbr; bi++) {
         const GcBranch& br = a.br[bi];
@@ -356,55 +426,32 @@ __global__ __launch_bounds__(GC_NT, 2) void k_gc(GcArgs a) {
         }
     }
     __syncthreads();
+    store_img(0);
+    __syncthreads();
     GSTAMP(gs++);
 
     for (int ii = 0; ii < nimg; ii++) {
         const int img = img0 + ii;
-        // stage this image's bands: LN2(LeakyReLU(t1)), zero outside the image / window
-        {
-            const float rs = ln ? lstat[2 * ii + 1] : 1.f;
-            const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
-            const float* __restrict__ src = a.in[net] + (size_t)img * HW * a.in_cs;
-            f4 xq[GC_GQ], gq[GC_GQ], bq[GC_GQ];
-#pragma unroll
-            for (int u = 0; u < GC_GQ; u++) {
-                xq[u] = load_q(src, u);
-                gq[u] = ln ? load_q(a.gamma[net], u) : f4{1.f, 1.f, 1.f, 1.f};
-                bq[u] = ln ? load_q(a.beta[net], u) : f4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int u = 0; u < GC_GQ; u++) {
-                if (loff[u] < 0) continue;
-                f4 v = f4{0.f, 0.f, 0.f, 0.f};
-                if (nv[u] != 0) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const float t = lrelu(xq[u][j]);
-                        v[j] = ln ? fmaf(fmaf(t, rs, nmr), gq[u][j], bq[u][j]) : t;
-                    }
-                }
-                *reinterpret_cast<f4*>(lds_f + loff[u]) = v;
-            }
-        }
-        __syncthreads();
-        GSTAMP(gs++);
+        if (ii + 1 < nimg) load_img(ii + 1);   // lands while this image's MFMAs run
         LnAcc st;
         st.reset();
         bool first = true;
         float* outp = a.out[net] + (size_t)img * HW * a.out_cs;
+        const int boff = (ii & 1) * a.band_bytes;
         for (int bi = 0; bi < a.nbr; bi++) {
             const GcBranch& br = a.br[bi];
             const float* bias = a.b[net][bi];
             switch ((br.cout + 15) >> 4) {
-                case 1: gc_branch<1>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
-                case 2: gc_branch<2>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
-                case 3: gc_branch<3>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
-                default: gc_branch<4>(a, br, smem, bias, outp, npx, px0, st, first, stats); break;
+                case 1: gc_branch<1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                case 2: gc_branch<2>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                case 3: gc_branch<3>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                default: gc_branch<4>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
             }
             GSTAMP(gs++);
         }
         if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * 3);
-        __syncthreads();   // bands are restaged for the next image
+        if (ii + 1 < nimg) store_img(ii + 1);   // the other buffer: nobody reads it this iteration
+        __syncthreads();
         GSTAMP(gs++);
     }
 #ifdef CNF_GC_STAMPS
