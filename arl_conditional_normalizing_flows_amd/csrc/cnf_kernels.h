@@ -44,6 +44,7 @@ struct ConvArgs {
     ConvProb p[MAXPROB];
     int H, W, TH, tiles_per_img, nprob, B;
     int P;     // 1x1 kernels: pixels per tile (tiles are runs of pixels inside one image)
+    int ipw;   // k_pw: images per workgroup (looped, next image prefetched)
 };
 
 struct CoupArgs {
@@ -127,8 +128,7 @@ int read_stamps(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
-void launch_pw(int nr, int gm, int mi, bool ln, bool res, int nw, const ConvArgs& a, int grid_x, int lds,
-               hipStream_t st);
+void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

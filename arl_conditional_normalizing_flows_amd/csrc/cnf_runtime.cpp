@@ -327,19 +327,22 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         });
         return 4 * g.tiles;
     } else if (pw_ok) {
-        // k_pw: (16 * nw)-pixel tiles x groups of MI images (see cnf_stream.hip)
+        // k_pw: 64-pixel tiles (4 waves x 16 pixels), each workgroup looping over ipw images, sized
+        // so the launch is one round of two workgroups per CU (see cnf_stream.hip)
         const bool resf = probs[0].res != nullptr;
-        const int nw = resf ? 4 : 8, mi = 2;
+        const int nw = 4;
         const int tiles = (h * w + 16 * nw - 1) / (16 * nw);
         a.tiles_per_img = tiles;
         for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = 0;
-        const int grid_x = tiles * ((E.B + mi - 1) / mi);
+        const int64_t units = (int64_t)tiles * a.nprob * E.B;
+        a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+        const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool lnf = probs[0].in_st.part != nullptr;
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
-                           std::to_string(mi) + "," + std::to_string(nw) + "," + role_name(role) + ">";
-        E.record(name, flops, bytes, [nr, gm, mi, lnf, resf, nw, a, grid_x, ilds](void* st) {
-            launch_pw(nr, gm, mi, lnf, resf, nw, a, grid_x, ilds, (hipStream_t)st);
+                           role_name(role) + ">";
+        E.record(name, flops, bytes, [nr, gm, lnf, resf, a, grid_x, ilds](void* st) {
+            launch_pw(nr, gm, lnf, resf, a, grid_x, ilds, (hipStream_t)st);
         });
         return nw * tiles;
     } else {
