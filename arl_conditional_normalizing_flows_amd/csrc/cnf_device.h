@@ -11,6 +11,12 @@ namespace cnf {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, then s_barrier.
+// Unlike __syncthreads() it does not drain outstanding global loads (vmcnt), so register prefetches
+// issued before a barrier (next conv's weights, LN gamma/beta) stay in flight across it. Global
+// data never passes between the waves of a workgroup through these barriers.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
 __device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
 
@@ -138,7 +144,6 @@ __device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, flo
     mu = (float)mt;
     rstd = (float)(1.0 / sqrt(M2 / nt + (double)LN_EPS));
 }
-
 
 // Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.
 template <int NTH>

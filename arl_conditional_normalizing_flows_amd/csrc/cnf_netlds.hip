@@ -688,7 +688,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         conv3_table(a.ci, KT, a.dc1, 0, 1);
         wpf_store(pf, WL, X + off[0]);
         lst_zero(slots);
-        __syncthreads();
+        lds_barrier();
         if (a.R > 0)
             wpf_load(pf, X + rbo(0)[2], wb(a.ca, nk));
         else
@@ -696,7 +696,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
         conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, sl);
-        __syncthreads();
+        lds_barrier();
         STAMP(sti++);
     }
     for (int r = 0; r < a.R; r++) {
@@ -708,12 +708,12 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         else
             ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         wpf_store(pf, WL, X + o[2]);
-        __syncthreads();   // every wave has read the Y slots; T2 and W are complete
+        lds_barrier();   // every wave has read the Y slots; T2 and W are complete
         lst_zero(slots);
         wpf_load(pf, X + o[10], brw(o));
         STAMP(sti++);
         conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
-        __syncthreads();
+        lds_barrier();
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
         if (ln) lst_final(slots, mu, rstd);
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             }
         }
         wpf_store(pf, WL, X + o[10]);
-        __syncthreads();   // LN2 applied, slots read, branch images and tables complete
+        lds_barrier();   // LN2 applied, slots read, branch images and tables complete
         lst_zero(slots);
         wpf_load(pf, X + o[8], wb(a.cb, nk));
         STAMP(sti++);
@@ -752,7 +752,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             }
         }
         STAMP(sti++);
-        __syncthreads();
+        lds_barrier();
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
         if (ln) lst_final(slots, mu, rstd);
         if (tq)
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         else
             ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
         wpf_store(pf, WL, X + o[8]);
-        __syncthreads();
+        lds_barrier();
         lst_zero(slots);
         if (r + 1 < a.R)
             wpf_load(pf, X + rbo(r + 1)[2], wb(a.ca, nk));
@@ -771,7 +771,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                      HW * nk / 4);
         STAMP(sti++);
         conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, sl);
-        __syncthreads();
+        lds_barrier();
         STAMP(sti++);
     }
     // LN_out(LReLU(y)) in place, conv_out (3x3 nk -> dc2) -> global
@@ -793,9 +793,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             const int CS = 16 * co_nr + 1;
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
-            __syncthreads();
+            lds_barrier();
             conv1_any(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, nullptr);
-            __syncthreads();
+            lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
                 const int p = e / a.dc2, oc = e - p * a.dc2;
@@ -817,9 +817,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         } else {
             conv3_table(a.co, KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
-            __syncthreads();
+            lds_barrier();
             conv3_run(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, nullptr);
-            __syncthreads();
+            lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
                 const int p = e / a.dc2, c = e - p * a.dc2;

@@ -615,7 +615,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             const int64_t units = (int64_t)ga.tiles_per_img * 2 * B;
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
             ga.band_bytes = c.gc_band_bytes;
-            if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::atoi(e));   // tuning override
+            if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
             if (8 * ga.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
             const int ilds = c.gc_lds;
