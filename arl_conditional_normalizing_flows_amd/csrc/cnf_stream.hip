@@ -200,14 +200,18 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
     const float* band = reinterpret_cast<const float*>(smem + br.band_off + boff);
     const float* lw = reinterpret_cast<const float*>(smem + br.w_off);
     const int* qo = reinterpret_cast<const int*>(smem + br.q_off);
-    float bz[NR];
-    bool chv[NR];
+    // operands swapped (A = weights, B = activations): lane (i16, kq) ends with pixel i16, channels
+    // 16n + 4kq + r (r < 4) of the subtile, i.e. one 16-byte channel quad per n -> f4 stores
+    f4 bz[NR];
+    int nq[NR];   // valid channels of the lane's quad (0..4)
 #pragma unroll
     for (int n = 0; n < NR; n++) {
-        const int ch = n * 16 + i16;
-        chv[n] = ch < br.cout;
-        bz[n] = chv[n] ? bias[ch] : 0.f;
+        const int c0 = n * 16 + 4 * kq;
+        nq[n] = max(0, min(4, br.cout - c0));
+#pragma unroll
+        for (int r = 0; r < 4; r++) bz[n][r] = r < nq[n] ? bias[c0 + r] : 0.f;
     }
+    const bool vq = ((a.out_cs | br.out_off) & 3) == 0;
     const int nsub = (npx + 15) >> 4;
     // two subtiles per wave and pass (s0, s0 + GC_NW) share every B read: two independent MFMA
     // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
@@ -252,29 +256,36 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
                 for (int q = 0; q < 4; q++)
 #pragma unroll
                     for (int n = 0; n < NR; n++) {
-                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][q], bq[n][q], acc0[n], 0, 0, 0);
-                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][q], bq[n][q], acc1[n], 0, 0, 0);
+                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(bq[n][q], a0[j][q], acc0[n], 0, 0, 0);
+                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(bq[n][q], a1[j][q], acc1[n], 0, 0, 0);
                     }
             }
         }
         if (stats && first) {
-            st.set_shift(lrelu(acc0[0][0] + bz[0]));
+            st.set_shift(lrelu(acc0[0][0] + bz[0][0]));
             first = false;
         }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             if (h == 1 && !v1) break;
-            const int sb = h ? s1 : s0;
+            const int po = (h ? s1 : s0) * 16 + i16;
+            const bool pv = po < npx;
+            float* orow = outp + (size_t)(px0 + po) * a.out_cs + br.out_off + 4 * kq;
 #pragma unroll
-            for (int n = 0; n < NR; n++)
+            for (int n = 0; n < NR; n++) {
+                f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
+                if (pv && nq[n] == 4 && vq) {
+                    *reinterpret_cast<f4*>(orow + n * 16) = v;
+                } else if (pv) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int po = sb * 16 + kq * 4 + r;
-                    const bool ok = chv[n] && po < npx;
-                    const float v = (h ? acc1[n][r] : acc0[n][r]) + bz[n];
-                    if (ok) outp[(size_t)(px0 + po) * a.out_cs + br.out_off + n * 16 + i16] = v;
-                    if (stats) st.add(lrelu(v), ok);
+                    for (int r = 0; r < 4; r++)
+                        if (r < nq[n]) orow[n * 16 + r] = v[r];
                 }
+                if (stats) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) st.add(lrelu(v[r]), pv && r < nq[n]);
+                }
+            }
         }
     }
 }
