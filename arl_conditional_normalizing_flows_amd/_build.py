@@ -10,7 +10,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / 'csrc'
 LIB = PKG / 'lib' / 'libcnf_hip.so'
-SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_runtime.cpp',
+SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
            'cnf_plan.cpp', 'cnf_train.cpp']
 HEADERS = ['cnf_kernels.h', 'cnf_device.h', 'cnf_plan.h']
 ARCH = os.environ.get('CNF_OFFLOAD_ARCH', 'gfx950')

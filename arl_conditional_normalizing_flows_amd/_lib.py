@@ -73,6 +73,11 @@ _SIGS = [
     ('cnf_toy_num_params', C.c_int64, [C.POINTER(cnf_toy_desc)]),
     ('cnf_toy_call', C.c_int, [C.POINTER(cnf_toy_desc), _F, _F, _F, _F, _F, C.c_int, C.c_int, _P]),
     ('cnf_toy_nll_sums', C.c_int, [_F, _F, C.c_int, _P]),
+    ('cnf_logit', C.c_int, [_F, _F, C.c_int64, C.c_float, C.c_int, _P]),
+    ('cnf_sr_preprocess', C.c_int, [_F, _F, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    ('cnf_down', C.c_int, [_F, _F, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    ('cnf_up', C.c_int, [_F, _F, C.c_int, C.c_int, C.c_int, C.c_int, _P]),
+    ('cnf_instance_noise', C.c_int, [_F, _F, C.c_int64, C.c_float, C.c_uint64, C.c_uint64, _P]),
     ('cnf_plan_num_recorded_launches', C.c_int, [_P]),
     ('cnf_plan_recorded_launch_info', C.c_int, [_P, C.c_int, C.c_char_p, C.c_int,
                                                 C.POINTER(C.c_double), C.POINTER(C.c_double)]),

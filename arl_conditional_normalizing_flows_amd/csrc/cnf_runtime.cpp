@@ -60,6 +60,9 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 namespace cnf {
 
+// error reporting for the entry points defined outside this file (cnf_transforms.hip)
+int set_error(int code, const char* msg) { return fail(code, msg); }
+
 // ----------------------------------------------------------------------------------------------
 // geometry
 // ----------------------------------------------------------------------------------------------

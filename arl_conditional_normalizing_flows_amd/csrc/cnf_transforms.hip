@@ -1,0 +1,216 @@
+// cnf_transforms.hip — the input transforms that feed the flow (conv_cINN_base_functions.py):
+// logit preprocessing / de_logitify, super-resolution down / up / residual assembly, and
+// instance / renewed Gaussian noise. All elementwise or 2x2-block HBM-bound kernels, one thread
+// per output element (float4-free: every output is computed from a handful of inputs).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+
+#include "../../include/cnf.h"
+
+namespace cnf {
+
+int set_error(int code, const char* msg);   // cnf_runtime.cpp (cnf_last_error)
+
+namespace {
+
+// fp32 constants of the reference's logit map (TF evaluates the Python-float constants in fp32):
+// c1 = (1-a) b, lo = logit(a), span = logit(1-a) - logit(a)
+struct LogitK {
+    float a, c1, lo, span, inv_bc;
+};
+LogitK logit_consts(float a) {
+    const double ad = a;
+    const double b = (1.0 - 2.0 * ad) / (1.0 - ad);
+    LogitK k;
+    k.a = a;
+    k.c1 = (float)((1.0 - ad) * b);
+    k.lo = logf((float)(ad / (1.0 - ad)));
+    const float hi = logf((float)((1.0 - ad) / ad));
+    k.span = hi - k.lo;
+    k.inv_bc = (float)(1.0 / (b * (1.0 - ad)));
+    return k;
+}
+
+// preprocess_dataset_class._preprocess_for_logit / _logit / _scale_logit (:198-212)
+__global__ __launch_bounds__(256) void k_logit(const float* __restrict__ x, float* __restrict__ out, long long n,
+                                               LogitK k, int inverse) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const float v = x[i];
+        float r;
+        if (!inverse) {
+            const float e = k.a + k.c1 * v;
+            r = (logf(e / (1.f - e)) - k.lo) / k.span;
+        } else {   // de_logitify (:306-318): (logistic(v span + lo) - a) / (b (1 - a))
+            const float z = v * k.span + k.lo;
+            r = (1.f / (1.f + expf(-z)) - k.a) * k.inv_bc;
+        }
+        out[i] = r;
+    }
+}
+
+// mean of the 2^L x 2^L block of `in` ([H][W][C] image) whose top-left corner is (r0, c0), as
+// nested 2x2 means (down applied L times, :111-116: reduce_mean over each 2x2 block)
+__device__ float nested_mean(const float* __restrict__ in, int W, int C, int r0, int c0, int c, int L) {
+    if (L == 0) return in[((size_t)r0 * W + c0) * C + c];
+    const int h = 1 << (L - 1);
+    const float m00 = nested_mean(in, W, C, r0, c0, c, L - 1);
+    const float m01 = nested_mean(in, W, C, r0, c0 + h, c, L - 1);
+    const float m10 = nested_mean(in, W, C, r0 + h, c0, c, L - 1);
+    const float m11 = nested_mean(in, W, C, r0 + h, c0 + h, c, L - 1);
+    return ((m00 + m01) + (m10 + m11)) * 0.25f;
+}
+
+// preprocess_dataset_SR._preprocess_* (:252-273): one thread per (pixel, channel) of x
+__global__ __launch_bounds__(256) void k_sr(const float* __restrict__ hi, float* __restrict__ xy, int B, int H, int W,
+                                            int C, int xd, int yl, int residual) {
+    const int Ho = H >> xd, Wo = W >> xd;
+    const long long n = (long long)B * Ho * Wo * C;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % C);
+        const long long p = e / C;
+        const int j = (int)(p % Wo);
+        const long long q = p / Wo;
+        const int i = (int)(q % Ho);
+        const int b = (int)(q / Ho);
+        const float* img = hi + (size_t)b * H * W * C;
+        const int s = 1 << xd;
+        const float x0 = nested_mean(img, W, C, i * s, j * s, c, xd);
+        const int m = 1 << yl;
+        const int bi = (i / m) * m, bj = (j / m) * m;   // y block of x0 containing (i, j)
+        const float y = nested_mean(img, W, C, bi * s, bj * s, c, xd + yl);
+        float* o = xy + (size_t)p * 2 * C;
+        o[c] = residual ? x0 - y : x0;
+        o[C + c] = y;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_down(const float* __restrict__ in, float* __restrict__ out, int B, int H,
+                                              int W, int C) {
+    const int Ho = H / 2, Wo = W / 2;
+    const long long n = (long long)B * Ho * Wo * C;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % C);
+        const long long p = e / C;
+        const int j = (int)(p % Wo);
+        const long long q = p / Wo;
+        const int i = (int)(q % Ho);
+        const int b = (int)(q / Ho);
+        out[e] = nested_mean(in + (size_t)b * H * W * C, W, C, 2 * i, 2 * j, c, 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_up(const float* __restrict__ in, float* __restrict__ out, int B, int H, int W,
+                                            int C) {
+    const int Ho = 2 * H, Wo = 2 * W;
+    const long long n = (long long)B * Ho * Wo * C;
+    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int c = (int)(e % C);
+        const long long p = e / C;
+        const int j = (int)(p % Wo);
+        const long long q = p / Wo;
+        const int i = (int)(q % Ho);
+        const int b = (int)(q / Ho);
+        out[e] = in[(((size_t)b * H + i / 2) * W + j / 2) * C + c];
+    }
+}
+
+// Philox4x32-10 (Salmon et al. 2011): counter (offset + i / 4 as 64 bits, 0, 0), key = seed
+__device__ inline void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+// instance_noise (:635-654) / renew_noise (:660-676); Box-Muller on Philox words, 4 normals per
+// counter value (element i uses normal i % 4 of counter (offset + i) / 4)
+__global__ __launch_bounds__(256) void k_noise(const float* __restrict__ x, float* __restrict__ out, long long n,
+                                               float alpha, uint64_t seed, uint64_t offset) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const uint64_t g = offset + (uint64_t)i;
+        uint32_t c[4] = {(uint32_t)(g >> 2), (uint32_t)(g >> 34), 0u, 0u};
+        philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const int w = (int)(g & 3);
+        const int pair = w >> 1;
+        // uniform in (0, 1] and [0, 1)
+        const float u1 = ((float)(c[2 * pair] >> 8) + 1.f) * (1.f / 16777216.f);
+        const float u2 = (float)(c[2 * pair + 1] >> 8) * (1.f / 16777216.f);
+        const float rad = sqrtf(-2.f * logf(u1));
+        const float th = 6.283185307179586f * u2;
+        const float z = (w & 1) ? rad * sinf(th) : rad * cosf(th);
+        out[i] = x != nullptr ? alpha * x[i] + (1.f - alpha) * z : z;
+    }
+}
+
+int grid_for(long long n) {
+    long long g = (n + 255) / 256;
+    return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
+}
+
+int finish(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(CNF_E_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+    return CNF_OK;
+}
+
+}  // namespace
+}  // namespace cnf
+
+extern "C" {
+
+int cnf_logit(const float* x, float* out, int64_t n, float a, int inverse, void* stream) {
+    if (!x || !out || n < 0 || !(a > 0.f && a < 0.5f))
+        return cnf::set_error(CNF_E_INVALID, "cnf_logit: null pointer, n < 0 or a outside (0, 0.5)");
+    if (n == 0) return CNF_OK;
+    hipLaunchKernelGGL(cnf::k_logit, dim3(cnf::grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, out, (long long)n,
+                       cnf::logit_consts(a), inverse);
+    return cnf::finish("k_logit");
+}
+
+int cnf_sr_preprocess(const float* hires, float* xy, int B, int H, int W, int C, int x_down, int y_levels,
+                      int residual, void* stream) {
+    if (!hires || !xy || B <= 0 || H <= 0 || W <= 0 || C <= 0 || x_down < 0 || y_levels < 0 || x_down + y_levels > 8)
+        return cnf::set_error(CNF_E_INVALID, "cnf_sr_preprocess: bad shape or levels");
+    const int m = 1 << (x_down + y_levels);
+    if (H % m || W % m) return cnf::set_error(CNF_E_INVALID, "cnf_sr_preprocess: H and W must be divisible by 2^(x_down + y_levels)");
+    const long long n = (long long)B * (H >> x_down) * (W >> x_down) * C;
+    hipLaunchKernelGGL(cnf::k_sr, dim3(cnf::grid_for(n)), dim3(256), 0, (hipStream_t)stream, hires, xy, B, H, W, C,
+                       x_down, y_levels, residual);
+    return cnf::finish("k_sr");
+}
+
+int cnf_down(const float* in, float* out, int B, int H, int W, int C, void* stream) {
+    if (!in || !out || B <= 0 || H < 2 || W < 2 || C <= 0) return cnf::set_error(CNF_E_INVALID, "cnf_down: bad shape");
+    const long long n = (long long)B * (H / 2) * (W / 2) * C;
+    hipLaunchKernelGGL(cnf::k_down, dim3(cnf::grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, B, H, W, C);
+    return cnf::finish("k_down");
+}
+
+int cnf_up(const float* in, float* out, int B, int H, int W, int C, void* stream) {
+    if (!in || !out || B <= 0 || H <= 0 || W <= 0 || C <= 0) return cnf::set_error(CNF_E_INVALID, "cnf_up: bad shape");
+    const long long n = (long long)B * 4 * H * W * C;
+    hipLaunchKernelGGL(cnf::k_up, dim3(cnf::grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, B, H, W, C);
+    return cnf::finish("k_up");
+}
+
+int cnf_instance_noise(const float* x, float* out, int64_t n, float alpha, uint64_t seed, uint64_t offset,
+                       void* stream) {
+    if (!out || n < 0) return cnf::set_error(CNF_E_INVALID, "cnf_instance_noise: null output or n < 0");
+    if (n == 0) return CNF_OK;
+    hipLaunchKernelGGL(cnf::k_noise, dim3(cnf::grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, out, (long long)n,
+                       alpha, seed, offset);
+    return cnf::finish("k_noise");
+}
+
+}  // extern "C"

@@ -208,6 +208,33 @@ int cnf_toy_call(const cnf_toy_desc* d, const float* params, const float* u, flo
  * sum -log_detJ_i); divide by B for the reference's 4-tuple. */
 int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream);
 
+/* ---- input transforms (the step before the path; conv_cINN_base_functions.py) ----------- */
+
+/* Logit preprocessing of preprocess_dataset_class(LOGITS=True) (:174-231), elementwise over n
+ * values in [0, 1]: x -> (logit(a + (1-a) b x) - logit(a)) / (logit(1-a) - logit(a)),
+ * b = (1-2a)/(1-a). inverse != 0 applies de_logitify (:287-318) instead. out may alias x. */
+int cnf_logit(const float* x, float* out, int64_t n, float a, int inverse, void* stream);
+
+/* Super-resolution preprocessing (preprocess_dataset_SR :233-279 with down/up :74-164):
+ * hires [B][H][W][C] -> xy [B][H>>x_down][W>>x_down][2C] with x0 = down^x_down(hires),
+ * y = up^y_levels(down^y_levels(x0)) (nested 2x2 means, then 2x2 repeats) and x = x0 - y when
+ * residual (RESIDUAL=True), else x0; xy = concat(x, y). 'SR2,1': x_down 0, y_levels 1;
+ * 'SR4,2': x_down 1, y_levels 1; the 4x / 8x benchmark configs: y_levels 2 / 3. H and W must be
+ * divisible by 2^(x_down + y_levels). */
+int cnf_sr_preprocess(const float* hires, float* xy, int B, int H, int W, int C, int x_down, int y_levels,
+                      int residual, void* stream);
+
+/* 2x2 average-pool down (:74-125) / 2x2 repeat up (:127-160) of [B][H][W][C]. */
+int cnf_down(const float* in, float* out, int B, int H, int W, int C, void* stream);
+int cnf_up(const float* in, float* out, int B, int H, int W, int C, void* stream);
+
+/* instance_noise (:635-654): out = alpha x + (1 - alpha) N(0, 1), and renew_noise (:660-676)
+ * with x == NULL: out = N(0, 1). Normals from a counter-based generator (Philox4x32-10 +
+ * Box-Muller): element i of a call depends only on (seed, offset + i), so results are
+ * reproducible and independent of the launch shape. out may alias x. */
+int cnf_instance_noise(const float* x, float* out, int64_t n, float alpha, uint64_t seed, uint64_t offset,
+                       void* stream);
+
 /* Measurement hooks (bench.py): number of kernel launches recorded by the last
  * forward/inverse call on this plan, their kernel symbol names, and a re-launch
  * of one recorded launch with identical arguments (same buffers). */
