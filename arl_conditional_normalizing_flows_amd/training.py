@@ -1,0 +1,201 @@
+"""Training driver: the reference's model.fit loop with its callbacks and
+the annealed instance-noise schedule, over the HIP train_step / test_step.
+
+  fit(...)                       keras Model.fit as conv_cINN.py:617-631 calls it (epochs,
+                                 initial_epoch, validation_data, callbacks)
+  EarlyStopping                  tf.keras.callbacks.EarlyStopping(monitor='val_loss', patience)
+                                 (conv_cINN.py:140-141)
+  CSVLogger                      tf.keras.callbacks.CSVLogger(path, separator=',', append=True)
+                                 (:533-536): header 'epoch' + sorted metric names
+  ModelCheckpoint                save_weights_only every save_freq batches, '{epoch:02d}' in the
+                                 name (:522-527); weights as .npz (no h5py here)
+  anneal_and_fit(...)            conv_cINN.py:583-636: num_annealing_epochs one-epoch fits on
+                                 instance_noise(xy, alpha = i / num_annealing_epochs), then the
+                                 clean fit up to num_epochs
+  save_weights / load_weights    {canonical name: array} .npz (np.load with allow_pickle=False)
+
+Datasets are iterables of device batches (torch tensors [B, H, W, D]); `callable` datasets are
+re-invoked each epoch (the tf.data re-iteration of the reference).
+"""
+from __future__ import annotations
+
+import csv
+import math
+import os
+from typing import Callable, Iterable, List, Optional
+
+import numpy as np
+
+from .base_functions import instance_noise
+
+
+def save_weights(model, path):
+    """model.save_weights (conv_cINN.py:636-641) as {canonical parameter name: array} .npz."""
+    np.savez(path, **model.get_weights())
+
+
+def load_weights(model, path):
+    """model.load_weights (conv_cINN.py:579) from save_weights' .npz (no pickles)."""
+    with np.load(path, allow_pickle=False) as z:
+        model.set_weights({k: z[k] for k in z.files})
+
+
+class Callback:
+    def set_model(self, model):
+        self.model = model
+
+    def on_train_begin(self, logs=None):
+        pass
+
+    def on_train_batch_end(self, batch, logs=None):
+        pass
+
+    def on_epoch_end(self, epoch, logs=None):
+        pass
+
+
+class EarlyStopping(Callback):
+    """monitor='val_loss', mode min, min_delta 0: stop once `patience` epochs pass without an
+    improvement (keras semantics: wait resets on improvement; checked from the second epoch)."""
+
+    def __init__(self, monitor='val_loss', patience=0, min_delta=0.0):
+        self.monitor, self.patience, self.min_delta = monitor, int(patience), abs(float(min_delta))
+        self.best, self.wait, self.stopped_epoch = math.inf, 0, None
+
+    def on_train_begin(self, logs=None):
+        self.best, self.wait, self.stopped_epoch = math.inf, 0, None
+
+    def on_epoch_end(self, epoch, logs=None):
+        cur = (logs or {}).get(self.monitor)
+        if cur is None:
+            return
+        self.wait += 1
+        if cur < self.best - self.min_delta:
+            self.best, self.wait = cur, 0
+        if self.wait >= self.patience and epoch > 0:
+            self.stopped_epoch = epoch
+            self.model.stop_training = True
+
+
+class CSVLogger(Callback):
+    def __init__(self, filename, separator=',', append=False):
+        self.filename, self.sep, self.append = filename, separator, append
+        self.keys = None
+
+    def on_train_begin(self, logs=None):
+        self._has_header = self.append and os.path.exists(self.filename) and os.path.getsize(self.filename) > 0
+        if not self.append:
+            open(self.filename, 'w').close()
+
+    def on_epoch_end(self, epoch, logs=None):
+        logs = dict(logs or {})
+        if self.keys is None:
+            self.keys = sorted(logs)
+        with open(self.filename, 'a', newline='') as f:
+            w = csv.writer(f, delimiter=self.sep)
+            if not self._has_header:
+                w.writerow(['epoch'] + self.keys)
+                self._has_header = True
+            w.writerow([epoch] + [logs.get(k, 'NA') for k in self.keys])
+
+
+class ModelCheckpoint(Callback):
+    def __init__(self, filepath, save_weights_only=True, save_freq='epoch'):
+        if not save_weights_only:
+            raise NotImplementedError('only save_weights_only=True (the reference never saves whole models)')
+        self.filepath, self.save_freq = filepath, save_freq
+        self._batches, self._epoch = 0, 0
+        self.saved: List[str] = []
+
+    def _save(self, epoch):
+        path = self.filepath.format(epoch=epoch + 1)
+        save_weights(self.model, path)
+        self.saved.append(path)
+
+    def on_train_batch_end(self, batch, logs=None):
+        self._batches += 1
+        if self.save_freq != 'epoch' and self._batches % int(self.save_freq) == 0:
+            self._save(self._epoch)
+
+    def on_epoch_end(self, epoch, logs=None):
+        self._epoch = epoch + 1
+        if self.save_freq == 'epoch':
+            self._save(epoch)
+
+
+class History(Callback):
+    def on_train_begin(self, logs=None):
+        self.epoch, self.history = [], {}
+
+    def on_epoch_end(self, epoch, logs=None):
+        self.epoch.append(epoch)
+        for k, v in (logs or {}).items():
+            self.history.setdefault(k, []).append(v)
+
+
+def _batches(data):
+    return data() if callable(data) else data
+
+
+def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Optional[List[Callback]] = None,
+        verbose=0, process_group=None):
+    """keras Model.fit over train_step / test_step. Logs per epoch: loss, z_loss, y_loss, detJ_loss
+    (+ val_ prefixed on validation_data); returns a History."""
+    hist = History()
+    cbs = list(callbacks or []) + [hist]
+    for cb in cbs:
+        cb.set_model(model)
+        cb.on_train_begin()
+    model.stop_training = False
+    for epoch in range(initial_epoch, epochs):
+        for t in model.metrics:
+            t.reset_state()
+        logs = {}
+        for i, xy in enumerate(_batches(x)):
+            logs = model.train_step(xy, process_group=process_group)
+            for cb in cbs:
+                cb.on_train_batch_end(i, logs)
+        logs = dict(logs)
+        if validation_data is not None:
+            for t in model.metrics:
+                t.reset_state()
+            vlogs = {}
+            for xy in _batches(validation_data):
+                vlogs = model.test_step(xy)
+            logs.update({'val_' + k: v for k, v in vlogs.items()})
+        if verbose:
+            print(f'Epoch {epoch + 1}/{epochs} ' + ' - '.join(f'{k}: {v:.4f}' for k, v in logs.items()))
+        for cb in cbs:
+            cb.on_epoch_end(epoch, logs)
+        if model.stop_training:
+            break
+    return hist
+
+
+def anneal_and_fit(model, xy_train: Iterable, xy_val: Optional[Iterable], num_annealing_epochs: int, num_epochs: int,
+                   callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0):
+    """conv_cINN.py:583-636: anneal instance noise from pure noise (alpha = 0) towards clean data
+    over num_annealing_epochs one-epoch fits, then fit the clean data up to num_epochs. Noise is
+    redrawn every epoch (counter offsets advance per batch)."""
+    completed = 0
+    hist = None
+    for i in range(int(num_annealing_epochs)):
+        alpha = i / num_annealing_epochs
+        if verbose:
+            print(f'Annealing instance noise, alpha={alpha}, annealing epoch {i} of {num_annealing_epochs}.')
+
+        def noisy(data, tag):
+            def gen():
+                off = 0
+                for xy in _batches(data):
+                    yield instance_noise(xy, alpha, seed=seed * 1000003 + 7919 * i + tag, offset=off)
+                    off += xy.numel()
+            return gen
+        hist = fit(model, noisy(xy_train, 0), epochs=completed + 1, initial_epoch=completed,
+                   validation_data=noisy(xy_val, 1) if xy_val is not None else None, callbacks=callbacks,
+                   verbose=verbose)
+        completed += 1
+        if getattr(model, 'stop_training', False):
+            return hist
+    return fit(model, xy_train, epochs=num_epochs, initial_epoch=completed, validation_data=xy_val,
+               callbacks=callbacks, verbose=verbose)
