@@ -169,15 +169,7 @@ struct Plan {
     bool record = true;
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     std::vector<Recorded> recorded;
-    // batch groups: the forward splits the batch into `groups` slices, each run on its own
-    // plan-owned stream (forked from / joined to the caller's stream by events), so the
-    // latency-bound LDS-resident layers of one slice overlap the streamed layers of another
-    int groups = 1;
-    std::vector<hipStream_t> gstreams;
-    std::vector<hipEvent_t> gevents;   // [0] fork, [1..groups] joins
-
     WsLayout layout(int B) const;
-    size_t forward_ws_bytes(int B) const;   // max(layout(B), groups x layout(ceil(B / groups)))
     TrainLayout train_layout(int B) const;
 };
 

@@ -748,7 +748,6 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     CNF_TRY
     Plan* p = build_plan(desc);
     if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CNF_GROUPS")) p->groups = std::max(1, std::min(8, std::atoi(e)));
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     *out = new cnf_plan{p};
@@ -762,8 +761,6 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->dev_table) (void)hipFree(plan->p->dev_table);
         if (plan->p->dev_aux_map) (void)hipFree(plan->p->dev_aux_map);
         if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
-        for (hipStream_t st : plan->p->gstreams) (void)hipStreamDestroy(st);
-        for (hipEvent_t ev : plan->p->gevents) (void)hipEventDestroy(ev);
         delete plan->p;
     }
     delete plan;
@@ -835,68 +832,17 @@ int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* strea
 
 size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
     if (!plan || B <= 0) return 0;
-    return plan->p->forward_ws_bytes(B);
+    return plan->p->layout(B).total;
 }
 
 }  // extern "C"
 
-size_t cnf::Plan::forward_ws_bytes(int B) const {
-    size_t t = layout(B).total;
-    const int G = std::min(groups, B);
-    if (G > 1) {
-        const int Bg = (B + G - 1) / G;
-        t = std::max(t, (size_t)G * align_up(layout(Bg).total, 256));
-    }
-    return t;
-}
-
 // the forward schedule; save_inputs: also copy every coupling layer's input into the training
 // workspace (cnf_flow_forward_train)
-static void flow_forward_one(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
-                             float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs);
-
 static void flow_forward(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
                          float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs) {
     ensure_tables(p);
     p.recorded.clear();
-    const int G = save_inputs ? 1 : std::min(p.groups, B);
-    if (G <= 1) {
-        flow_forward_one(p, params, aux, xy, zy, logdet_per_image, workspace, B, stream, save_inputs);
-        return;
-    }
-    // batch groups on plan-owned streams: fork from the caller's stream, join back into it (both
-    // are events, so a hipGraph capture of the caller's stream captures every group as a branch)
-    if ((int)p.gstreams.size() < G) {
-        for (int g = (int)p.gstreams.size(); g < G; g++) {
-            hipStream_t s;
-            hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate(group)");
-            p.gstreams.push_back(s);
-        }
-    }
-    while ((int)p.gevents.size() < G + 1) {
-        hipEvent_t e;
-        hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(group)");
-        p.gevents.push_back(e);
-    }
-    const int Bg = (B + G - 1) / G;
-    const size_t wsg = align_up(p.layout(Bg).total, 256);
-    const int64_t nuv = (int64_t)p.desc.io_h * p.desc.io_w * p.desc.io_d;
-    hip_check(hipEventRecord(p.gevents[0], stream), "hipEventRecord(fork)");
-    int b0 = 0;
-    for (int g = 0; g < G && b0 < B; g++) {
-        const int nb = std::min(Bg, B - b0);
-        hipStream_t s = p.gstreams[g];
-        hip_check(hipStreamWaitEvent(s, p.gevents[0], 0), "hipStreamWaitEvent(fork)");
-        flow_forward_one(p, params, aux, xy + (size_t)b0 * nuv, zy + (size_t)b0 * nuv, logdet_per_image + b0,
-                         (char*)workspace + (size_t)g * wsg, nb, s, false);
-        hip_check(hipEventRecord(p.gevents[1 + g], s), "hipEventRecord(join)");
-        hip_check(hipStreamWaitEvent(stream, p.gevents[1 + g], 0), "hipStreamWaitEvent(join)");
-        b0 += nb;
-    }
-}
-
-static void flow_forward_one(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
-                             float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs) {
     Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
     TrainLayout TL;
     if (save_inputs) TL = p.train_layout(B);
