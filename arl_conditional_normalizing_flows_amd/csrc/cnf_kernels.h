@@ -125,6 +125,7 @@ void launch_toy(const ToyArgs& a, int lds_floats, hipStream_t st);
 void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st);
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
 int read_stamps(long long* host, int n);
+int read_cycles(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);

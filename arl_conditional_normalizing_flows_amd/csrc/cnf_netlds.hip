@@ -626,12 +626,16 @@ __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int
 
 // Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs).
 __device__ long long g_stamps[256];
+__device__ long long g_cycles[256];   // s_memtime (shader clock) at the same stamps
 #define STAMP(i)                                                                            \
     do {                                                                                     \
         if (STAMPS) {                                                                        \
             __syncthreads();                                                                 \
-            if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0)                      \
-                g_stamps[(i)] = (long long)__builtin_amdgcn_s_memrealtime();                \
+            const int si_ = (i);                                                             \
+            if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                    \
+                g_stamps[si_] = (long long)__builtin_amdgcn_s_memrealtime();                 \
+                g_cycles[si_] = (long long)__builtin_amdgcn_s_memtime();                     \
+            }                                                                                \
         }                                                                                    \
     } while (0)
 
@@ -840,6 +844,10 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         hipLaunchKernelGGL(k_net_lds<true>, dim3(B, 2), dim3(NT), lds, st, a);
     else
         hipLaunchKernelGGL(k_net_lds<false>, dim3(B, 2), dim3(NT), lds, st, a);
+}
+
+int read_cycles(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cycles), sizeof(long long) * (n > 256 ? 256 : n)) == hipSuccess ? 0 : -1;
 }
 
 int read_stamps(long long* host, int n) {

@@ -1198,6 +1198,7 @@ int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream) 
 }
 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
+int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }
 int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }
 
 int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)plan->p->recorded.size() : -1; }
