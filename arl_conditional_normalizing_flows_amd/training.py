@@ -199,3 +199,27 @@ def anneal_and_fit(model, xy_train: Iterable, xy_val: Optional[Iterable], num_an
             return hist
     return fit(model, xy_train, epochs=num_epochs, initial_epoch=completed, validation_data=xy_val,
                callbacks=callbacks, verbose=verbose)
+
+
+def pretrain_on_noise(model, batch_size: int, num_epochs: int, batches_per_epoch: int = 20,
+                      callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0):
+    """conv_pre_training_cINN_on_noise.py:100-147: condition the model on pure N(0, 1) inputs of its
+    io_shape, `batches_per_epoch` batches per epoch (the reference's 20 * batch_size examples),
+    fresh noise on every call (renew_noise); returns the History."""
+    import torch
+    shape = (batch_size,) + tuple(model.io_shape)
+    n_el = int(np.prod(shape))
+    proto = torch.empty(shape, device=model.device, dtype=torch.float32)
+    state = {'calls': 0}
+
+    def epoch_batches():
+        c = state['calls']
+        state['calls'] += 1
+        for j in range(batches_per_epoch):
+            yield renew_noise_like(proto, seed, (c * batches_per_epoch + j) * n_el)
+    return fit(model, epoch_batches, epochs=num_epochs, callbacks=callbacks, verbose=verbose)
+
+
+def renew_noise_like(t, seed, offset):
+    from .base_functions import renew_noise
+    return renew_noise(t, seed=seed, offset=offset)

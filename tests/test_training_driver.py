@@ -120,3 +120,18 @@ def test_anneal_and_fit_end_to_end(gpu, tmp_path):
     w_before = flow.params.detach().clone()
     T.load_weights(flow, ck.saved[-1])
     assert torch.equal(flow.params, w_before)
+
+
+@pytest.mark.gpu
+def test_pretrain_on_noise(gpu):
+    from arl_conditional_normalizing_flows_amd.config import PRESETS
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    from arl_conditional_normalizing_flows_amd.optimizers import Adam
+    cfg = PRESETS['tiny']
+    flow = cFlow(**cfg.kwargs(), device=gpu)
+    flow.set_weights(flow.initial_weights(1))
+    flow.compile(optimizer=Adam(learning_rate=1e-3))
+    hist = T.pretrain_on_noise(flow, batch_size=4, num_epochs=3, batches_per_epoch=4)
+    losses = hist.history['loss']
+    assert len(losses) == 3 and all(math.isfinite(v) for v in losses)
+    assert losses[-1] < losses[0]
