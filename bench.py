@@ -177,12 +177,20 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # rehearsal knobs (one-GPU boxes): CNF_BENCH_DEVICE pins every rank to one device,
+    # CNF_BENCH_BACKEND=gloo replaces RCCL; the driver's multi-GPU runs use neither
+    if os.environ.get('CNF_BENCH_DEVICE') is not None:
+        local = int(os.environ['CNF_BENCH_DEVICE'])
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        backend = os.environ.get('CNF_BENCH_BACKEND', 'nccl')
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     cfg = PRESETS[args.config]
     B = args.batch or cfg.batch
@@ -200,17 +208,31 @@ def main():
     ws = flow._workspace(B)
     lib = _lib.load()
 
-    def step():
+    def local_step():
         st = torch.cuda.current_stream().cuda_stream
         _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(), xy.data_ptr(),
                                         zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
         _lib.check(lib.cnf_nll(flow._plan, xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
                                sums.data_ptr(), B, st), 'nll')
+
+    def exchange():
+        # the path's one exchange step, issued eagerly after the (graph-replayed) local work: RCCL
+        # collectives are never captured into the graph
         if dist is not None:
             pack_nll_sums(sums, B, red)
             dist.all_reduce(red)
 
+    def step():
+        local_step()
+        exchange()
+
+    def note(msg):
+        if os.environ.get('CNF_BENCH_VERBOSE'):
+            print(f'# rank {rank}: {msg}', file=sys.stderr, flush=True)
+
+    note('first step')
     step()
+    note('first step done')
     torch.cuda.synchronize()
     graph = None
     if not args.no_graph:
@@ -218,17 +240,22 @@ def main():
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                step()
+                local_step()
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                step()
+                local_step()
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover
             print(f'# graph capture failed, eager: {e}', file=sys.stderr)
             graph = None
-    run = graph.replay if graph is not None else step
+
+    def replay():
+        graph.replay()
+        exchange()
+    run = replay if graph is not None else step
+    note(f'graph {graph is not None}; warmup')
 
     for _ in range(args.warmup):
         run()
@@ -244,6 +271,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    note('timed steps done')
     if dist is not None:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -256,7 +284,7 @@ def main():
     if rank == 0:
         roof = None
         if not args.no_roofline:
-            step()   # eager forward records its launches for the measurement hooks
+            local_step()   # eager forward records its launches (no collective: rank 0 only)
             torch.cuda.synchronize()
             per_k = measure_dominant_kernel(flow, torch.cuda.current_stream().cuda_stream)
             roof = roofline_for(per_k)
