@@ -80,6 +80,7 @@ struct NetLdsArgs {
     LdsConv ci, ca, cb, co, gcv[NETLDS_MAXBR];   // packed images of conv_in, conv_a, conv_b, conv_out, branches
     const float* zero_bias;                      // >= 128 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
+    int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
 };
 // k_gc (cnf_stream.hip): every grouped dilated branch of one residual block for a tile of TH
 // image rows of one net, `ipw` images per workgroup. Branch input windows are staged into LDS

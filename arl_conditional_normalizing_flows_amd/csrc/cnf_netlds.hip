@@ -421,14 +421,23 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
     if (stats) lst_flush(st, slots);
 }
 
+// MAXNR: the widest output block count the instantiation supports (wider is compiled out, which
+// keeps the narrow instantiation's register allocation small; the host picks MAXNR per layer)
+template <int MAXNR>
 __device__ __forceinline__ void conv1_any(const float* in, int istride, int cin, int HW, const float* wl, float* out,
                                           int ostride, int cout, const float* bias, bool residual, double* slots) {
-    switch ((cout + 15) / 16) {
-        case 1: conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        case 2: conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        case 3: conv1_lds<3>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        case 4: conv1_lds<4>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        default: conv1_lds<5>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+    const int nr = (cout + 15) / 16;
+    if (MAXNR <= 2 || nr <= 2) {
+        if (nr == 1)
+            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots);
+        else
+            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots);
+        return;
+    }
+    switch (nr) {
+        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
     }
 }
 
@@ -503,15 +512,22 @@ __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, 
     if (stats) lst_flush(st, slots);
 }
 
+template <int MAXNR>
 __device__ __forceinline__ void conv3q_any(const float* in, int istride, int G, int H, int W, const float* wl,
                                            const int* qt, float* out, int ostride, int cout, const float* bias,
                                            double* slots) {
-    switch ((cout + 15) / 16) {
-        case 1: conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
-        case 2: conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
-        case 3: conv3q_lds<3>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
-        default: conv3q_lds<4>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots); break;
+    const int nr = (cout + 15) / 16;
+    if (MAXNR <= 2 || nr <= 2) {
+        if (nr == 1)
+            conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+        else
+            conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+        return;
     }
+    if (nr == 3)
+        conv3q_lds<MAXNR >= 3 ? 3 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+    else
+        conv3q_lds<MAXNR >= 4 ? 4 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
 }
 
 // k -> (dr, dc, c) table of a PK_KN conv over cin channels from channel ic0; -1 beyond K
@@ -578,15 +594,22 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
     if (stats) lst_flush(st, slots);
 }
 
+template <int MAXNR>
 __device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
                                            const float* bias, double* slots) {
-    switch ((cout + 15) / 16) {
-        case 1: conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
-        case 2: conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
-        case 3: conv3k_lds<3>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
-        default: conv3k_lds<4>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots); break;
+    const int nr = (cout + 15) / 16;
+    if (MAXNR <= 2 || nr <= 2) {
+        if (nr == 1)
+            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+        else
+            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+        return;
     }
+    if (nr == 3)
+        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+    else
+        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
 }
 
 // entries of the tap (PK_KN) / quad (PK_Q4) table of a 3x3 conv, rounded to 4
@@ -599,13 +622,14 @@ __device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin
     else
         build_ktab(tab, cin, ic0, d, cv.kpad);
 }
+template <int MAXNR>
 __device__ __forceinline__ void conv3_run(const LdsConv& cv, const float* in, int istride, int H, int W,
                                           const float* wl, const int* tab, float* out, int ostride, int cout,
                                           const float* bias, double* slots) {
     if (cv.fmt == PK_Q4)
-        conv3q_any(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, slots);
+        conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, slots);
     else
-        conv3k_any(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, slots);
+        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, slots);
 }
 
 // position in u of element (pixel p, channel c) of the compressed u1c (mask compress, :720-759)
@@ -639,7 +663,7 @@ __device__ long long g_cycles[256];   // s_memtime (shader clock) at the same st
         }                                                                                    \
     } while (0)
 
-template <bool STAMPS>
+template <bool STAMPS, int MAXNR>
 __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int img = blockIdx.x, net = blockIdx.y;
@@ -699,7 +723,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
         if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
-        conv3_run(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, sl);
+        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, sl);
         lds_barrier();
         STAMP(sti++);
     }
@@ -716,7 +740,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         lst_zero(slots);
         wpf_load(pf, X + o[10], brw(o));
         STAMP(sti++);
-        conv1_any(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
+        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
         lds_barrier();
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
@@ -750,7 +774,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             for (int bi = 0; bi < a.nbr; bi++) {
                 const LdsConv& cv = a.gcv[bi];
                 const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
-                conv3_run(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
+                conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
                           WL + (o[11 + 2 * bi] - o[10]), sl);
                 kto += ktab_len(cv);
             }
@@ -774,7 +798,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
                      HW * nk / 4);
         STAMP(sti++);
-        conv1_any(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, sl);
+        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, sl);
         lds_barrier();
         STAMP(sti++);
     }
@@ -798,7 +822,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv1_any(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, nullptr);
+            conv1_any<MAXNR>(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, nullptr);
             lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -822,7 +846,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             conv3_table(a.co, KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv3_run(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, nullptr);
+            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, nullptr);
             lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -840,10 +864,17 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         const char* e = std::getenv("CNF_STAMPS");
         return e && std::atoi(e) != 0;
     }();
+    static const bool wide = [] {   // A/B knob: always the generic instantiation
+        const char* e = std::getenv("CNF_NETLDS_WIDE");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool narrow = a.maxnr <= 2 && !wide;
     if (stamps)
-        hipLaunchKernelGGL(k_net_lds<true>, dim3(B, 2), dim3(NT), lds, st, a);
+        hipLaunchKernelGGL((k_net_lds<true, 5>), dim3(B, 2), dim3(NT), lds, st, a);
+    else if (narrow)
+        hipLaunchKernelGGL((k_net_lds<false, 2>), dim3(B, 2), dim3(NT), lds, st, a);
     else
-        hipLaunchKernelGGL(k_net_lds<false>, dim3(B, 2), dim3(NT), lds, st, a);
+        hipLaunchKernelGGL((k_net_lds<false, 5>), dim3(B, 2), dim3(NT), lds, st, a);
 }
 
 int read_cycles(long long* host, int n) {

@@ -360,8 +360,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.use_lds = false;
                 if (!allow) continue;
                 const int ci9 = c.dc1 % 4 == 0 ? PK_Q4 : PK_KN;
-                // k_net_lds runs the tap-decomposed conv_out up to 80 tap columns (NR = 5)
-                const int co9 = 9 * c.dc2 <= 80 ? PK_TAP : (c.nk % 4 == 0 ? PK_Q4 : PK_KN);
+                // tap-decomposed conv_out only up to 32 tap columns (NR <= 2)
+                int tapmax = 32;   // wider conv_outs take the PK_Q4 3x3 path (narrow instantiation)
+                if (const char* e = std::getenv("CNF_CO_TAPMAX")) tapmax = std::atoi(e);   // tuning
+                const int co9 = 9 * c.dc2 <= tapmax ? PK_TAP : (c.nk % 4 == 0 ? PK_Q4 : PK_KN);
                 std::vector<int> gc9;
                 for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_Q4 : PK_KN);
                 NetLdsGeom g;

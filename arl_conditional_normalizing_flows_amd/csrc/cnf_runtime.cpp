@@ -490,6 +490,12 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     a.off_t2 = g.off_t2;
     a.off_w = g.off_w;
     a.off_k = g.off_k;
+    auto nr = [](int cout) { return (cout + 15) / 16; };
+    a.maxnr = std::max(nr(c.nk), nr(c.co_fmt == PK_TAP ? 9 * c.dc2 : c.dc2));
+    for (const Branch& b : c.br) a.maxnr = std::max(a.maxnr, nr(b.cout));
+    if (const char* e = std::getenv("CNF_NETLDS_VERBOSE"))
+        if (std::atoi(e)) std::fprintf(stderr, "netlds layer hc=%d wc=%d nk=%d dc2=%d co_fmt=%d maxnr=%d\n", c.hc, c.wc,
+                                       c.nk, c.dc2, c.co_fmt, a.maxnr);
     return (size_t)g.bytes;
 }
 
