@@ -12,7 +12,8 @@ the annealed instance-noise schedule, over the HIP train_step / test_step.
   anneal_and_fit(...)            conv_cINN.py:583-636: num_annealing_epochs one-epoch fits on
                                  instance_noise(xy, alpha = i / num_annealing_epochs), then the
                                  clean fit up to num_epochs
-  save_weights / load_weights    {canonical name: array} .npz (np.load with allow_pickle=False)
+  save_weights / load_weights    Keras-layout .h5 (keras_h5.py) or {canonical name: array} .npz
+                                 (np.load with allow_pickle=False)
 
 Datasets are iterables of device batches (torch tensors [B, H, W, D]); `callable` datasets are
 re-invoked each epoch (the tf.data re-iteration of the reference).
@@ -30,12 +31,25 @@ from .base_functions import instance_noise
 
 
 def save_weights(model, path):
-    """model.save_weights (conv_cINN.py:636-641) as {canonical parameter name: array} .npz."""
-    np.savez(path, **model.get_weights())
+    """model.save_weights (conv_cINN.py:636-641). A path ending in .h5 / .hdf5 / .keras writes the
+    Keras HDF5 layout the reference's files have (keras_h5.py); anything else a
+    {canonical parameter name: array} .npz."""
+    if str(path).endswith(('.h5', '.hdf5', '.keras')):
+        from .keras_h5 import save_weights_h5
+        save_weights_h5(model, path)
+    else:
+        np.savez(path, **model.get_weights())
 
 
 def load_weights(model, path):
-    """model.load_weights (conv_cINN.py:579) from save_weights' .npz (no pickles)."""
+    """model.load_weights (conv_cINN.py:579): a Keras .h5 weight file (including one the
+    reference wrote) or save_weights' .npz (no pickles)."""
+    with open(path, 'rb') as fh:
+        is_h5 = fh.read(8) == b'\x89HDF\r\n\x1a\n'
+    if is_h5:
+        from .keras_h5 import load_weights_h5
+        load_weights_h5(model, path)
+        return
     with np.load(path, allow_pickle=False) as z:
         model.set_weights({k: z[k] for k in z.files})
 
