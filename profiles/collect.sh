@@ -4,6 +4,8 @@
 #  2-4. separate --pmc passes (never combined with sys/runtime traces): FETCH_SIZE, WRITE_SIZE,
 #     SQ issue/wait counters, each with --kernel-trace only, on the eager (no-graph) bench path
 # then profiles/pmc_summary.py folds them into profiles/TAG_summary.json (+ the stats CSV copy).
+# Only gpurun_out/ comes back from the box: re-run the fold in the container afterwards,
+#   python3 profiles/pmc_summary.py gpurun_out/prof_TAG TAG
 set -o pipefail
 tag=${1:-r01}
 root=$PWD
