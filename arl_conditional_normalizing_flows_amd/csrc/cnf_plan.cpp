@@ -359,6 +359,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.gc_fmt.assign(c.br.size(), PK_KN);
                 c.use_lds = false;
                 if (!allow) continue;
+                if (const char* e = std::getenv("CNF_NETLDS_MAXHW"))   // tuning: stream layers above this size
+                    if (c.hc * c.wc > std::atoi(e)) continue;
                 const int ci9 = c.dc1 % 4 == 0 ? PK_Q4 : PK_KN;
                 // tap-decomposed conv_out only up to 32 tap columns (NR <= 2)
                 int tapmax = 32;   // wider conv_outs take the PK_Q4 3x3 path (narrow instantiation)

@@ -339,6 +339,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = 0;
         const int64_t units = (int64_t)tiles * a.nprob * E.B;
         a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+        if (const char* e = std::getenv(resf ? "CNF_PW_IPW_RES" : "CNF_PW_IPW"))   // tuning override
+            a.ipw = std::max(1, std::min(16, std::atoi(e)));
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool lnf = probs[0].in_st.part != nullptr;
