@@ -55,6 +55,12 @@ struct CoupArgs {
     const float* tanh_w;     // device scalar
     double* ld_part;         // [B][gridDim.x] or null
     int H, W, D, mask, mask_c, hc, wc, dc1, dc2, dir;
+    // tap mode (tc[0] != null): s_pre / t are the 3x3 conv_out finished here from the tap GEMM
+    // C[img][p][(tap, o)] (row stride 9*dc2) of each net, plus bias, and also written to
+    // so_w[net] (the raw conv_out the training path reads)
+    const float* tc[2];
+    const float* tbias[2];
+    float* so_w[2];
 };
 
 // Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).

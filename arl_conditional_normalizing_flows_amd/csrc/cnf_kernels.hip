@@ -473,8 +473,35 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
         if (e < n2) {
             const int p = e / a.dc2, c = e - p * a.dc2;
             const int q = mask_pos(a.mask_c, p, c, a.wc, a.W, a.D);
-            const float s = w * tanhf(sb[e]);
-            const float t = tb[e];
+            float sp, t;
+            if (a.tc[0] != nullptr) {
+                // out[p][c] = b[c] + sum_tap C[p + off(tap)][(tap, c)], taps in (kh, kw) order
+                const int pr = p / a.wc, pc = p - pr * a.wc;
+                const int ncol = 9 * a.dc2;
+                const float* c0 = a.tc[0] + (size_t)img * npx * ncol;
+                const float* c1 = a.tc[1] + (size_t)img * npx * ncol;
+                sp = a.tbias[0][c];
+                t = a.tbias[1][c];
+#pragma unroll
+                for (int kh = 0; kh < 3; kh++) {
+                    const int sr = pr + kh - 1;
+                    if (sr < 0 || sr >= a.hc) continue;
+#pragma unroll
+                    for (int kw = 0; kw < 3; kw++) {
+                        const int sc = pc + kw - 1;
+                        if (sc < 0 || sc >= a.wc) continue;
+                        const size_t ci = (size_t)(sr * a.wc + sc) * ncol + (kh * 3 + kw) * a.dc2 + c;
+                        sp += c0[ci];
+                        t += c1[ci];
+                    }
+                }
+                a.so_w[0][(size_t)img * npx * a.dc2 + e] = sp;
+                a.so_w[1][(size_t)img * npx * a.dc2 + e] = t;
+            } else {
+                sp = sb[e];
+                t = tb[e];
+            }
+            const float s = w * tanhf(sp);
             const float x = ub[q];
             float y;
             if (a.dir > 0) {

@@ -168,6 +168,7 @@ struct Plan {
     // launch recording
     bool record = true;
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
+    bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
     std::vector<Recorded> recorded;
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;

@@ -521,6 +521,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     const bool ln = E.p.desc.layer_norm != 0;
     float* so0 = E.at<float>(L.so[0]);
     float* so1 = E.at<float>(L.so[1]);
+    const float* tap_c[2] = {nullptr, nullptr};   // streamed tap-GEMM conv_out (finished in k_coupling)
+    const float* tap_b[2] = {nullptr, nullptr};
     NetLdsArgs na;
     const size_t nlds = c.use_lds ? netlds_setup(E.p, c, na) : 0;
     if (c.use_lds && nlds == 0) throw std::runtime_error("layer planned for k_net_lds does not fit its LDS budget");
@@ -679,10 +681,24 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                   ln ? P + np.ln_out_b : none, 1, X + np.co.w, X + np.co.b, so[n], c.dc2, 0, c.dc2,
                                   none, Slab{}, 0, 1});
         }
-        if (c.net[0].co.fmt == PK_TAP)
+        if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2) {
+            // tap GEMM C = LN_out(LReLU(y)) . W_tap as a streamed 1x1 conv into the dead t1 buffer;
+            // k_coupling finishes the 3x3 (tap sums + bias) where it reads s and t
+            for (int n = 0; n < 2; n++) {
+                ProbSpec& q = pr[n];
+                q.bias = X + E.p.aux_zero;
+                q.out = t1[n];
+                q.out_cs = q.cout = 9 * c.dc2;
+                q.out_off = 0;
+                tap_c[n] = t1[n];
+                tap_b[n] = X + c.net[n].co.b;
+            }
+            conv_launch(E, 1, ROLE_CONV_OUT, c.hc, c.wc, pr);
+        } else if (c.net[0].co.fmt == PK_TAP) {
             convtap_launch(E, c.hc, c.wc, pr);
-        else
+        } else {
             conv_launch(E, 3, ROLE_CONV_OUT, c.hc, c.wc, pr);
+        }
     }
     }  // streamed path
     // affine coupling law + decompress + log-det partials
@@ -704,6 +720,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         ca.dc1 = c.dc1;
         ca.dc2 = c.dc2;
         ca.dir = dir;
+        for (int n = 0; n < 2; n++) {
+            ca.tc[n] = tap_c[n];
+            ca.tbias[n] = tap_b[n];
+            ca.so_w[n] = n == 0 ? so0 : so1;
+        }
         const int np = E.L.ld_parts;
         E.record("k_coupling", 0, 4.0 * B * c.H * c.W * c.D * 2 + 8.0 * B * c.hc * c.wc * c.dc2,
                  [ca, B, np](void* st) { launch_coupling(ca, B, np, (hipStream_t)st); });
@@ -756,6 +777,7 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     CNF_TRY
     Plan* p = build_plan(desc);
     if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
+    if (const char* e = std::getenv("CNF_TAP_PW")) p->tap_pw = std::atoi(e) != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     *out = new cnf_plan{p};
