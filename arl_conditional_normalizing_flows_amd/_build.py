@@ -34,6 +34,7 @@ def needs_build() -> bool:
 def _compile(src: Path, obj: Path, verbose: bool) -> None:
     cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wno-pass-failed', '-c',
            '-o', str(obj), str(src)]
+    cmd[1:1] = os.environ.get('CNF_EXTRA_FLAGS', '').split()   # diagnostics, e.g. -DCNF_GC_STAMPS
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
