@@ -355,29 +355,31 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
             e -= nq;
         }
     }
-    auto load_q = [&](const float* __restrict__ base, int u) -> f4 {
-        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+    // one staged quad through a buffer resource (out-of-range offset BUF_OOB reads 0). The vector
+    // / scalar choice is made per wave (ballot), never per lane: a lane-divergent choice makes both
+    // paths write the same VGPRs, and the compiler then drains every load (vmcnt(0)) before the next
+    // one — the gathers of a band would run one round trip at a time.
+    auto load_q = [&](__amdgpu_buffer_rsrc_t r, int u) -> f4 {
         const int n = nv[u] & 7;
-        if (nv[u] & 8) {
-            v = *reinterpret_cast<const f4*>(base + soff[u]);
-        } else if (n > 0) {
+        const uint32_t o = (uint32_t)soff[u] * 4u;
+        if (__all(n == 0 || (nv[u] & 8) != 0)) return buf_load4(r, n == 0 ? BUF_OOB : o);
+        f4 v;
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if (j < n) v[j] = base[soff[u] + j];
-        }
+        for (int j = 0; j < 4; j++) v[j] = buf_load1(r, j < n ? o + 4u * j : BUF_OOB);
         return v;
     };
+    const uint32_t img_bytes = (uint32_t)HW * a.in_cs * 4u;
     // tile LN2 gamma/beta (image-independent) and the first image's raw quads, all in flight together
     f4 gq[GC_GQ], bq[GC_GQ], xq[GC_GQ];
 #pragma unroll
     for (int u = 0; u < GC_GQ; u++) {
-        gq[u] = ln ? load_q(a.gamma[net], u) : f4{1.f, 1.f, 1.f, 1.f};
-        bq[u] = ln ? load_q(a.beta[net], u) : f4{0.f, 0.f, 0.f, 0.f};
+        gq[u] = ln ? load_q(buf_rsrc(a.gamma[net], img_bytes), u) : f4{1.f, 1.f, 1.f, 1.f};
+        bq[u] = ln ? load_q(buf_rsrc(a.beta[net], img_bytes), u) : f4{0.f, 0.f, 0.f, 0.f};
     }
     auto load_img = [&](int ii) {
-        const float* __restrict__ src = a.in[net] + (size_t)(img0 + ii) * HW * a.in_cs;
+        const auto r = buf_rsrc(a.in[net] + (size_t)(img0 + ii) * HW * a.in_cs, img_bytes);
 #pragma unroll
-        for (int u = 0; u < GC_GQ; u++) xq[u] = load_q(src, u);
+        for (int u = 0; u < GC_GQ; u++) xq[u] = load_q(r, u);
     };
     // LN2(LeakyReLU(t1)) of the quads in xq -> band buffer (ii & 1); zero outside the image / window
     auto store_img = [&](int ii) {
