@@ -97,7 +97,7 @@ struct GcBranch {
     int cin_off, cin, cinp, cout, out_off, dil;   // input window, padded channels, outputs
     int G;                                        // quad groups of the PK_Q4 image
     int band_off, BW, BH, S;                      // LDS band: byte offset, width, height, pixel stride
-    int w_off, q_off;                             // LDS byte offsets: packed weights, quad offsets
+    int w_off, q_off, b_off;                      // LDS byte offsets: packed weights, quad offsets, bias
     uint32_t cpq_mag, bw_mag;                     // x / (cinp/4) == umulhi(x, cpq_mag) (cinp > 4), x / BW likewise
 };
 struct GcArgs {

@@ -418,6 +418,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 // two band buffers: the next image is staged while the current one is computed
                 const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
                 off += band_bytes;
+                for (GcBranch& g : gb) {   // biases (read from LDS in the epilogue: no global load there)
+                    g.b_off = (int)off;
+                    off = align16(off + 4LL * g.cout);
+                }
                 if (!ok || off > 160 * 1024 || quads > 4 * 512 || !allow_gc) continue;
                 c.gc_fused = true;
                 c.gc_TH = TH;

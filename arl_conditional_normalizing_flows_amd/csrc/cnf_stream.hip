@@ -192,7 +192,7 @@ constexpr int GC_NT = 64 * GC_NW;   // threads
 
 template <int NR>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, const unsigned char* smem,
-                                          const float* __restrict__ bias, float* __restrict__ outp, int npx,
+                                          const float* bias, float* __restrict__ outp, int npx,
                                           int px0, LnAcc& st, bool& first, bool stats, int boff) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
@@ -406,6 +406,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         const GcBranch& br = a.br[bi];
         const int nr = (br.cout + 15) >> 4;
         copy_to_lds<GC_NT>(a.w[net][bi], reinterpret_cast<float*>(smem + br.w_off), br.G * 16 * 16 * nr);
+        for (int i = tid; i < br.cout; i += GC_NT) reinterpret_cast<float*>(smem + br.b_off)[i] = a.b[net][bi][i];
         int* qo = reinterpret_cast<int*>(smem + br.q_off);
         const int cpq = br.cinp >> 2, nq = 9 * cpq;
         for (int qd = tid; qd < 4 * br.G; qd += GC_NT) {
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         const int boff = (ii & 1) * a.band_bytes;
         for (int bi = 0; bi < a.nbr; bi++) {
             const GcBranch& br = a.br[bi];
-            const float* bias = a.b[net][bi];
+            const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
             switch ((br.cout + 15) >> 4) {
                 case 1: gc_branch<1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
                 case 2: gc_branch<2>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
