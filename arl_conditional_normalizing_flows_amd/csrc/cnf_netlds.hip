@@ -678,7 +678,13 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     int* KT = reinterpret_cast<int*>(smem + a.off_k);
     const float* P = a.params;
     const float* X = a.aux;
-    const int* off = a.offs + net * a.offs_per_net;   // see NetLdsArgs
+    // this net's parameter-offset table (see NetLdsArgs) copied to LDS [192, ...): every later read
+    // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
+    static_assert(NW * 3 * 8 <= 192, "LN slots overlap the offset table");
+    int* otab = reinterpret_cast<int*>(smem + 192);
+    for (int i = threadIdx.x; i < a.offs_per_net; i += NT) otab[i] = a.offs[net * a.offs_per_net + i];
+    lds_barrier();
+    const int* off = otab;
     const bool ln = a.ln != 0;
     double* sl = ln ? slots : nullptr;
     float mu = 0.f, rstd = 1.f;

@@ -119,7 +119,10 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
         wmax = std::max(wmax, wsum);
         kmax = std::max(kmax, ksum);
     }
-    int64_t off = 512;   // LN-statistics slots (NW x 3 doubles, NW <= 16)
+    // [0, 192): LN-statistics slots (8 waves x 3 doubles); [192, ...): this net's parameter-offset
+    // table (2 + R*(10 + 2*nbr) + 4 ints), read from LDS so no phase waits on a global load of it
+    const int64_t opn = 2 + (int64_t)c.R * (10 + 2 * (int64_t)c.br.size()) + 4;
+    int64_t off = std::max<int64_t>(512, align16(192 + 4 * opn));
     g.off_y = (int)off;
     off = align16(off + HW * g.sy * 4);
     g.off_t1 = (int)off;
