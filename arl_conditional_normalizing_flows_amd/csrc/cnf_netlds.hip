@@ -338,7 +338,8 @@ struct Epi {
         for (int n = 0; n < NR; n++) {
             const int ch = n * 16 + i16;
             chv[n] = ch < cout;
-            bz[n] = chv[n] ? bias[ch] : 0.f;
+            const float b = bias[chv[n] ? ch : 0];   // unconditional LDS read: no divergent block
+            bz[n] = chv[n] ? b : 0.f;
         }
     }
     // write subtile sb of acc; out points at channel oc0 of pixel 0
