@@ -108,6 +108,25 @@ def test_roundtrip_cfg2_full_batch(gpu):
     assert torch.isfinite(ld).all()
 
 
+@pytest.mark.parametrize('netlds', [True, False])
+def test_ragged_large_batch_matches_small_batches(gpu, netlds):
+    """Every op is per image, so an image's result must not depend on the batch it rides in: a
+    ragged batch of 67 (the image-looping kernels' last workgroups get partial image sets) against
+    the same images in batches of 5, on the LDS and the streamed paths (tolerance: fp32 ordering
+    of the LN partial merges, 1e-6 relative)."""
+    from oracle.cflow_np import synthetic_class_batch
+    flow, ora, P, _ = _setup('cfg2', 2, netlds=netlds)
+    xy = synthetic_class_batch(67, 32, 32, 3, seed=5)
+    x = torch.from_numpy(xy).to(gpu)
+    zy, ld = flow(x, 1, per_image_logdet=True)
+    for s in range(0, 67, 5):
+        zs, ls = flow(x[s:s + 5], 1, per_image_logdet=True)
+        e = (zs - zy[s:s + 5]).abs().max().item() / zy[s:s + 5].abs().max().item()
+        assert e < 1e-6, (s, e)
+        assert torch.allclose(ls, ld[s:s + 5], rtol=1e-6, atol=1e-4)
+    torch.cuda.synchronize()
+
+
 def test_nll_matches_oracle(gpu):
     flow, ora, P, xy = _setup('cfg2', 2)
     ref = ora.log_loss(xy, P)
