@@ -23,8 +23,28 @@ def _hipcc() -> str:
     raise RuntimeError('hipcc not found')
 
 
+def _extra_flags() -> list:
+    return os.environ.get('CNF_EXTRA_FLAGS', '').split()   # diagnostics, e.g. -DCNF_GC_STAMPS
+
+
+def _flags_file() -> Path:
+    return LIB.with_suffix('.so.flags')
+
+
+def _objdir() -> Path:
+    """Objects live in a directory per flag set, so a diagnostic build (CNF_EXTRA_FLAGS) never
+    leaves instrumented objects for a later normal build to reuse."""
+    import hashlib
+    fl = ' '.join(_extra_flags())
+    return PKG / 'build' / ('default' if not fl else 'x' + hashlib.sha1(fl.encode()).hexdigest()[:12])
+
+
 def needs_build() -> bool:
     if not LIB.exists():
+        return True
+    ff = _flags_file()
+    built_with = ff.read_text() if ff.exists() else ''
+    if built_with != ' '.join(_extra_flags()):
         return True
     t = LIB.stat().st_mtime
     deps = [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / 'include' / 'cnf.h']
@@ -34,7 +54,7 @@ def needs_build() -> bool:
 def _compile(src: Path, obj: Path, verbose: bool) -> None:
     cmd = [_hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wno-pass-failed', '-c',
            '-o', str(obj), str(src)]
-    cmd[1:1] = os.environ.get('CNF_EXTRA_FLAGS', '').split()   # diagnostics, e.g. -DCNF_GC_STAMPS
+    cmd[1:1] = _extra_flags()
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -49,8 +69,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         return LIB
     from concurrent.futures import ThreadPoolExecutor
     LIB.parent.mkdir(parents=True, exist_ok=True)
-    objdir = PKG / 'build'
-    objdir.mkdir(exist_ok=True)
+    objdir = _objdir()
+    objdir.mkdir(parents=True, exist_ok=True)
     hdr_t = max((CSRC / h).stat().st_mtime for h in HEADERS)
     hdr_t = max(hdr_t, (PKG.parent / 'include' / 'cnf.h').stat().st_mtime)
     jobs = []
@@ -70,6 +90,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f'link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')
     os.replace(tmp, LIB)
+    _flags_file().write_text(' '.join(_extra_flags()))
     return LIB
 
 

@@ -571,9 +571,10 @@ class cFlow:
             t.update_state(v)
         return {t.name: t.result() for t in self.metrics}
 
-    def test_step(self, xy):
-        """:1882-1904 — loss without a weight update; updates the Mean trackers."""
-        loss, lz, ly, ld = self.log_loss(xy)
+    def test_step(self, xy, process_group=None):
+        """:1882-1904 — loss without a weight update; updates the Mean trackers. With
+        process_group the loss terms are global-batch means (log_loss), the same on every rank."""
+        loss, lz, ly, ld = self.log_loss(xy, process_group=process_group)
         vals = torch.stack([loss, lz, ly, ld]).cpu().tolist()
         for t, v in zip(self.metrics, vals):
             t.update_state(v)

@@ -38,7 +38,10 @@ def save_weights(model, path):
         from .keras_h5 import save_weights_h5
         save_weights_h5(model, path)
     else:
-        np.savez(path, **model.get_weights())
+        # through an open handle: np.savez would append '.npz' to a bare path, and the file the
+        # caller named (ModelCheckpoint.saved, load_weights) would not exist
+        with open(path, 'wb') as fh:
+            np.savez(fh, **model.get_weights())
 
 
 def load_weights(model, path):
@@ -55,10 +58,16 @@ def load_weights(model, path):
 
 
 class Callback:
+    # callbacks that write files run on rank 0 only in a data-parallel fit
+    writes_files = False
+
     def set_model(self, model):
         self.model = model
 
     def on_train_begin(self, logs=None):
+        pass
+
+    def on_epoch_begin(self, epoch, logs=None):
         pass
 
     def on_train_batch_end(self, batch, logs=None):
@@ -92,6 +101,8 @@ class EarlyStopping(Callback):
 
 
 class CSVLogger(Callback):
+    writes_files = True
+
     def __init__(self, filename, separator=',', append=False):
         self.filename, self.sep, self.append = filename, separator, append
         self.keys = None
@@ -114,6 +125,8 @@ class CSVLogger(Callback):
 
 
 class ModelCheckpoint(Callback):
+    writes_files = True
+
     def __init__(self, filepath, save_weights_only=True, save_freq='epoch'):
         if not save_weights_only:
             raise NotImplementedError('only save_weights_only=True (the reference never saves whole models)')
@@ -126,13 +139,17 @@ class ModelCheckpoint(Callback):
         save_weights(self.model, path)
         self.saved.append(path)
 
+    def on_epoch_begin(self, epoch, logs=None):
+        # keras sets the epoch used for '{epoch:02d}' at on_epoch_begin, so a fresh callback in a
+        # fit(initial_epoch > 0) names its batch-count saves after the current epoch
+        self._epoch = epoch
+
     def on_train_batch_end(self, batch, logs=None):
         self._batches += 1
         if self.save_freq != 'epoch' and self._batches % int(self.save_freq) == 0:
             self._save(self._epoch)
 
     def on_epoch_end(self, epoch, logs=None):
-        self._epoch = epoch + 1
         if self.save_freq == 'epoch':
             self._save(epoch)
 
@@ -151,17 +168,55 @@ def _batches(data):
     return data() if callable(data) else data
 
 
+def _rank(process_group):
+    if process_group is None:
+        return 0
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    grp = None if process_group is True else process_group
+    return dist.get_rank(grp)
+
+
+def _agree_stop(model, process_group):
+    """Rank 0's stop_training decision on every rank (one broadcast of one int): a rank that
+    stopped alone would leave the others blocked in the next train_step all-reduce."""
+    if process_group is None:
+        return
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    grp = None if process_group is True else process_group
+    dev = getattr(model, 'device', None)
+    if dist.get_backend(grp) == 'gloo' or dev is None:
+        dev = torch.device('cpu')
+    flag = torch.tensor([1 if getattr(model, 'stop_training', False) else 0], dtype=torch.int32, device=dev)
+    src = dist.get_global_rank(grp, 0) if grp is not None else 0
+    dist.broadcast(flag, src=src, group=grp)
+    model.stop_training = bool(int(flag.item()))
+
+
 def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Optional[List[Callback]] = None,
         verbose=0, process_group=None):
     """keras Model.fit over train_step / test_step. Logs per epoch: loss, z_loss, y_loss, detJ_loss
-    (+ val_ prefixed on validation_data); returns a History."""
+    (+ val_ prefixed on validation_data); returns a History.
+
+    Data-parallel (process_group given, True = the default group): every rank passes its own
+    shard of the batches; train_step and test_step all-reduce over the global batch, so the
+    logged losses (and EarlyStopping's val_loss) are the same on every rank; rank 0's
+    stop_training decision is broadcast after each epoch, and callbacks that write files
+    (CSVLogger, ModelCheckpoint) run on rank 0 only."""
     hist = History()
-    cbs = list(callbacks or []) + [hist]
+    rank = _rank(process_group)
+    cbs = [cb for cb in list(callbacks or []) if rank == 0 or not cb.writes_files] + [hist]
     for cb in cbs:
         cb.set_model(model)
         cb.on_train_begin()
     model.stop_training = False
     for epoch in range(initial_epoch, epochs):
+        for cb in cbs:
+            cb.on_epoch_begin(epoch)
         for t in model.metrics:
             t.reset_state()
         logs = {}
@@ -175,24 +230,29 @@ def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Op
                 t.reset_state()
             vlogs = {}
             for xy in _batches(validation_data):
-                vlogs = model.test_step(xy)
+                vlogs = model.test_step(xy, process_group=process_group)
             logs.update({'val_' + k: v for k, v in vlogs.items()})
-        if verbose:
+        if verbose and rank == 0:
             print(f'Epoch {epoch + 1}/{epochs} ' + ' - '.join(f'{k}: {v:.4f}' for k, v in logs.items()))
         for cb in cbs:
             cb.on_epoch_end(epoch, logs)
+        _agree_stop(model, process_group)
         if model.stop_training:
             break
     return hist
 
 
 def anneal_and_fit(model, xy_train: Iterable, xy_val: Optional[Iterable], num_annealing_epochs: int, num_epochs: int,
-                   callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0):
+                   callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0, process_group=None):
     """conv_cINN.py:583-636: anneal instance noise from pure noise (alpha = 0) towards clean data
     over num_annealing_epochs one-epoch fits, then fit the clean data up to num_epochs. Noise is
-    redrawn every epoch (counter offsets advance per batch)."""
+    redrawn every epoch (counter offsets advance per batch). As in the reference, each fit()
+    starts with stop_training reset (keras), so an EarlyStopping that fires during annealing
+    ends that one-epoch fit only and the schedule carries on. process_group: see fit (each rank
+    passes its own shard; the noise is seeded per rank so shards draw independent noise)."""
     completed = 0
     hist = None
+    rank = _rank(process_group)
     for i in range(int(num_annealing_epochs)):
         alpha = i / num_annealing_epochs
         if verbose:
@@ -202,36 +262,37 @@ def anneal_and_fit(model, xy_train: Iterable, xy_val: Optional[Iterable], num_an
             def gen():
                 off = 0
                 for xy in _batches(data):
-                    yield instance_noise(xy, alpha, seed=seed * 1000003 + 7919 * i + tag, offset=off)
+                    yield instance_noise(xy, alpha, seed=seed * 1000003 + 7919 * i + tag + 104729 * rank, offset=off)
                     off += xy.numel()
             return gen
         hist = fit(model, noisy(xy_train, 0), epochs=completed + 1, initial_epoch=completed,
                    validation_data=noisy(xy_val, 1) if xy_val is not None else None, callbacks=callbacks,
-                   verbose=verbose)
+                   verbose=verbose, process_group=process_group)
         completed += 1
-        if getattr(model, 'stop_training', False):
-            return hist
     return fit(model, xy_train, epochs=num_epochs, initial_epoch=completed, validation_data=xy_val,
-               callbacks=callbacks, verbose=verbose)
+               callbacks=callbacks, verbose=verbose, process_group=process_group)
 
 
 def pretrain_on_noise(model, batch_size: int, num_epochs: int, batches_per_epoch: int = 20,
-                      callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0):
+                      callbacks: Optional[List[Callback]] = None, seed: int = 0, verbose=0, process_group=None):
     """conv_pre_training_cINN_on_noise.py:100-147: condition the model on pure N(0, 1) inputs of its
     io_shape, `batches_per_epoch` batches per epoch (the reference's 20 * batch_size examples),
-    fresh noise on every call (renew_noise); returns the History."""
+    fresh noise on every call (renew_noise); returns the History. process_group: data-parallel as
+    in fit, batch_size images per rank, the noise seeded per rank."""
     import torch
     shape = (batch_size,) + tuple(model.io_shape)
     n_el = int(np.prod(shape))
     proto = torch.empty(shape, device=model.device, dtype=torch.float32)
     state = {'calls': 0}
+    seed = seed + 104729 * _rank(process_group)
 
     def epoch_batches():
         c = state['calls']
         state['calls'] += 1
         for j in range(batches_per_epoch):
             yield renew_noise_like(proto, seed, (c * batches_per_epoch + j) * n_el)
-    return fit(model, epoch_batches, epochs=num_epochs, callbacks=callbacks, verbose=verbose)
+    return fit(model, epoch_batches, epochs=num_epochs, callbacks=callbacks, verbose=verbose,
+               process_group=process_group)
 
 
 def renew_noise_like(t, seed, offset):

@@ -34,7 +34,7 @@ class _Stub:
         self.steps += 1
         return {'loss': 1.0}
 
-    def test_step(self, xy):
+    def test_step(self, xy, process_group=None):
         return {'loss': self.val[self.epoch]}
 
     def get_weights(self):
@@ -91,6 +91,95 @@ def test_model_checkpoint_batch_frequency(tmp_path):
     assert [os.path.basename(p) for p in ck.saved] == ['ck.e01.npz', 'ck.e02.npz', 'ck.e03.npz']
     with np.load(ck.saved[0], allow_pickle=False) as z:
         assert np.array_equal(z['w'], np.arange(3.0))
+
+
+def test_model_checkpoint_names_current_epoch_on_resume(tmp_path):
+    """A fresh ModelCheckpoint in fit(initial_epoch=2) with a batch-count save_freq names its
+    file after the current epoch (keras sets it at on_epoch_begin), and a path without the .npz
+    suffix is written exactly as named."""
+    stub = _Stub([1.0] * 4)
+
+    def data():
+        stub.epoch += 1
+        return [0, 0]
+    ck = T.ModelCheckpoint(str(tmp_path / 'ck.e{epoch:02d}'), save_weights_only=True, save_freq=2)
+    T.fit(stub, data, epochs=4, initial_epoch=2, callbacks=[ck])
+    assert [os.path.basename(p) for p in ck.saved] == ['ck.e03', 'ck.e04']
+    assert all(os.path.exists(p) for p in ck.saved)
+    with np.load(ck.saved[-1], allow_pickle=False) as z:
+        assert np.array_equal(z['w'], np.arange(3.0))
+
+
+def test_anneal_keeps_going_after_early_stop(monkeypatch):
+    """EarlyStopping firing inside an annealing epoch ends that one-epoch fit only: the schedule
+    runs the remaining annealing epochs and the clean fit (conv_cINN.py:583-631; keras resets
+    stop_training at every fit call)."""
+    calls = []
+
+    def fake_fit(model, x, epochs=1, initial_epoch=0, **kw):
+        calls.append((initial_epoch, epochs))
+        model.stop_training = True
+        return 'h'
+    monkeypatch.setattr(T, 'fit', fake_fit)
+
+    class M:
+        stop_training = False
+    T.anneal_and_fit(M(), [], None, num_annealing_epochs=3, num_epochs=6)
+    assert calls == [(0, 1), (1, 2), (2, 3), (3, 6)]
+
+
+class _DPStub(_Stub):
+    """Rank-dependent validation losses and an all-reduce in every train_step: without the
+    broadcast stop decision rank 1 (earlier plateau) would leave fit while rank 0 blocks in the
+    next all-reduce."""
+
+    def __init__(self, val_losses):
+        super().__init__(val_losses)
+
+    def train_step(self, xy, process_group=None):
+        import torch.distributed as dist
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        self.steps += 1
+        return {'loss': float(t.item())}
+
+
+def _dp_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        vals = [5.0, 4.0, 4.5, 4.2, 3.0, 2.0] if rank == 0 else [5.0, 5.5, 5.6, 5.7, 5.8, 5.9]
+        stub = _DPStub(vals)
+
+        def data():
+            stub.epoch += 1
+            return [0, 0]
+        csvp = os.path.join(out_dir, f'h{rank}.csv')
+        ck = T.ModelCheckpoint(os.path.join(out_dir, f'w{rank}.e{{epoch:02d}}.npz'), save_freq='epoch')
+        es = T.EarlyStopping(monitor='val_loss', patience=2)
+        hist = T.fit(stub, data, epochs=6, validation_data=[0], callbacks=[T.CSVLogger(csvp), ck, es],
+                     process_group=True)
+        np.save(os.path.join(out_dir, f'ep{rank}.npy'), np.array(hist.epoch))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_fit_agrees_on_early_stop(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_dp_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    e0, e1 = np.load(tmp_path / 'ep0.npy'), np.load(tmp_path / 'ep1.npy')
+    # rank 0's schedule (best 4.0 at epoch 1, no improvement in 2, 3 -> stop after epoch 3) on both
+    assert e0.tolist() == [0, 1, 2, 3] and e1.tolist() == e0.tolist()
+    # files from rank 0 only
+    assert os.path.exists(tmp_path / 'h0.csv') and not os.path.exists(tmp_path / 'h1.csv')
+    assert os.path.exists(tmp_path / 'w0.e04.npz') and not any(p.name.startswith('w1') for p in tmp_path.iterdir())
 
 
 @pytest.mark.gpu
