@@ -87,6 +87,7 @@ struct NetLdsArgs {
     const float* zero_bias;                      // >= 128 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
     int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
+    int stamp_off;                               // diagnostic stamp builds: LDS byte offset of the stamp array
 };
 // k_gc (cnf_stream.hip): every grouped dilated branch of one residual block for a tile of TH
 // image rows of one net, `ipw` images per workgroup. Branch input windows are staged into LDS

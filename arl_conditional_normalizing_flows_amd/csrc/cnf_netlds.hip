@@ -10,9 +10,9 @@
 // floats so the channel-quad ds_read_b128 A reads are bank-conflict free.
 //
 // LayerNorm statistics (per image over H*W*C, conv_cINN_base_functions.py:357) are produced in
-// the epilogue of the conv that writes the tensor: every lane accumulates shifted fp32 sums of
-// LeakyReLU(out) (shift = a wave-uniform sample value), each wave reduces and Chan-merges into its
-// fp64 LDS slot, and after the conv's barrier every wave merges the NW slots — no extra pass.
+// the epilogue of the conv(s) that write the tensor: every lane accumulates shifted fp32 sums of
+// LeakyReLU(out) (shift = a wave-uniform sample value), each wave reduces them once per tensor into
+// its LDS slot, and after the producer's barrier every wave merges the NW slots — no extra pass.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -33,6 +33,9 @@ constexpr int NW = CNF_NETLDS_NW;   // waves per workgroup (one workgroup per CU
 #endif
 constexpr bool PAIR = CNF_NETLDS_PAIR != 0;   // two 16-pixel subtiles per wave and pass
 constexpr int NT = NW * 64;         // threads
+#ifndef CNF_CQ
+#define CNF_CQ 2   // 3x3 groups per chunk (conv3q_lds)
+#endif
 
 // LeakyReLU(0.3) as max(x, 0.3x) (2 VALU ops; equal to the select form for every finite x)
 __device__ __forceinline__ float lrelu_(float x) { return __builtin_fmaxf(x, LRELU_ALPHA * x); }
@@ -45,80 +48,79 @@ __device__ __forceinline__ double wsum_d(double v) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// LN statistics produced in conv epilogues
+// LN statistics produced in conv epilogues. Every lane accumulates fp32 sums of LeakyReLU(out) - K,
+// K a wave-uniform sample value of the tensor (so sum (x-K)^2 does not cancel), across every conv
+// that produces the tensor (the grouped branches share one LStat); the value count is kept as a
+// wave-uniform scalar. Once per tensor each wave reduces its sums (DPP) and lane 0 writes
+// (K, S1, S2, n) to the wave's 16-byte LDS slot: no read-modify-write, no fp64.
 // ---------------------------------------------------------------------------------------------
 struct LStat {
-    float K, s1, s2, c;
+    float K, s1, s2;
+    int cnt;     // values added (wave-uniform)
+    bool kset;   // K chosen (wave-uniform)
 };
 __device__ __forceinline__ void lst_reset(LStat& a) {
     a.K = 0.f;
     a.s1 = 0.f;
     a.s2 = 0.f;
-    a.c = 0.f;
+    a.cnt = 0;
+    a.kset = false;
 }
-// shift = LeakyReLU of lane 0's value (call in wave-uniform control flow)
+// shift = LeakyReLU of lane 0's value at the wave's first output (call in wave-uniform control flow)
 __device__ __forceinline__ void lst_setk(LStat& a, float v) {
+    if (a.kset) return;
     a.K = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lrelu_(v))));
+    a.kset = true;
 }
 __device__ __forceinline__ void lst_add(LStat& a, float v) {
     const float d = lrelu_(v) - a.K;
     a.s1 += d;
     a.s2 = fmaf(d, d, a.s2);
-    a.c += 1.f;
 }
-// each wave zeroes its own slot before the producing conv(s) of a tensor
-__device__ __forceinline__ void lst_zero(double* slots) {
-    if ((threadIdx.x & 63) == 0) {
-        double* q = slots + 3 * (threadIdx.x >> 6);
-        q[0] = 0.0;
-        q[1] = 0.0;
-        q[2] = 0.0;
-    }
+// wave-reduce the lane sums and write (K, S1, S2, n) to this wave's slot (every wave, once per tensor)
+__device__ __forceinline__ void lst_flush(const LStat& a, float* slots) {
+#ifdef CNF_ABL_NOSTATS
+    return;
+#endif
+    const float s1 = wsum_f(a.s1), s2 = wsum_f(a.s2);
+    if ((threadIdx.x & 63) == 0)
+        *reinterpret_cast<f4*>(slots + 4 * (threadIdx.x >> 6)) = f4{a.K, s1, s2, (float)a.cnt};
 }
-// wave-reduce the lane sums and Chan-merge (n, mean, M2) into this wave's slot
-__device__ __forceinline__ void lst_flush(const LStat& a, double* slots) {
-    const float s1 = wsum_f(a.s1), s2 = wsum_f(a.s2), c = wsum_f(a.c);
-    if ((threadIdx.x & 63) == 0 && c > 0.f) {
-        const double nb = c, S1 = s1;
-        const double mb = S1 / nb;
-        double M2b = (double)s2 - S1 * mb;
-        if (M2b < 0.0) M2b = 0.0;
-        double* q = slots + 3 * (threadIdx.x >> 6);
-        const double na = q[0], ma = q[1];
-        const double mbx = (double)a.K + mb;
-        if (na == 0.0) {
-            q[0] = nb;
-            q[1] = mbx;
-            q[2] = M2b;
-        } else {
-            const double nn = na + nb, dl = mbx - ma;
-            q[1] = ma + dl * (nb / nn);
-            q[2] = q[2] + M2b + dl * dl * (na * nb / nn);
-            q[0] = nn;
-        }
-    }
-}
-// (mean, rstd) of the tensor from the NW slots (every wave, after the producer's barrier). Every
-// lane reads all slots (uniform-address LDS broadcasts) and merges them in the same fixed order:
-// one LDS round trip and a short fp64 chain, no cross-lane shuffles. Single-pass fp64 form
-// (M2 = sum(M2_i + n_i m_i^2) - N mean^2): fp64 keeps > 1e-10 relative even at |mean| = 1e3 std.
-__device__ __forceinline__ void lst_final(const double* slots, float& mu, float& rstd) {
-    double q[3 * NW];
+// (mean, rstd) of the tensor from the NW slots (every wave, after the producer's barrier): every
+// lane reads all slots (uniform-address LDS broadcasts, one round trip) and merges them in the same
+// fixed order, so every lane of every wave gets bitwise the same pair. Per wave n_w, mean_w,
+// M2_w = S2 - S1^2/n; then mean = sum n_w mean_w / N, M2 = sum M2_w + n_w (mean_w - mean)^2 (fp32;
+// the shifted per-wave sums keep it well conditioned).
+__device__ __forceinline__ void lst_final(const float* slots, float& mu, float& rstd) {
+#ifdef CNF_ABL_NOSTATS
+    mu = 0.f;
+    rstd = 1.f;
+    return;
+#endif
+    f4 q[NW];
 #pragma unroll
-    for (int i = 0; i < 3 * NW; i++) q[i] = slots[i];
-    double N = 0.0, S = 0.0, Q = 0.0;
+    for (int w = 0; w < NW; w++) q[w] = *reinterpret_cast<const f4*>(slots + 4 * w);
+    float n[NW], m[NW], M2[NW];
+    float N = 0.f, S = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-        const double n = q[3 * w], m = q[3 * w + 1];
-        N += n;
-        S = fma(n, m, S);
-        Q += fma(n * m, m, q[3 * w + 2]);
+        n[w] = q[w][3];
+        const float r = n[w] > 0.f ? q[w][1] * __builtin_amdgcn_rcpf(n[w]) : 0.f;
+        m[w] = q[w][0] + r;
+        M2[w] = fmaxf(fmaf(-q[w][1], r, q[w][2]), 0.f);
+        N += n[w];
+        S = fmaf(n[w], m[w], S);
     }
-    const double mean = S / N;
-    double var = Q / N - mean * mean;
-    if (var < 0.0) var = 0.0;
-    mu = (float)mean;
-    rstd = (float)(1.0 / sqrt(var + (double)LN_EPS));
+    const float iN = __builtin_amdgcn_rcpf(N);
+    const float mean = S * iN;
+    float M = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const float d = m[w] - mean;
+        M += fmaf(n[w] * d, d, M2[w]);
+    }
+    mu = mean;
+    rstd = __builtin_amdgcn_rsqf(fmaf(M, iN, LN_EPS));
 }
 
 // dst[p][c] = LN(LeakyReLU(src[p][c])) for channels [c0, c0+nc) of a C_ln-channel LN tensor;
@@ -332,7 +334,9 @@ template <int NR>
 struct Epi {
     float bz[NR];
     bool chv[NR];
-    __device__ __forceinline__ void init(const float* __restrict__ bias, int cout) {
+    int cout;
+    __device__ __forceinline__ void init(const float* __restrict__ bias, int cout_) {
+        cout = cout_;
         const int i16 = threadIdx.x & 15;
 #pragma unroll
         for (int n = 0; n < NR; n++) {
@@ -345,6 +349,13 @@ struct Epi {
     // write subtile sb of acc; out points at channel oc0 of pixel 0
     __device__ __forceinline__ void store(const f4 (&acc)[NR], int sb, int HW, float* out, int ostride, bool residual,
                                           bool stats, LStat& st) {
+#ifdef CNF_ABL_NOEPI
+        if (sb >= 0) return;
+#endif
+#ifdef CNF_ABL_NOSTATS
+        stats = false;
+#endif
+        if (stats) st.cnt += min(16, HW - sb * 16) * cout;
         const int i16 = threadIdx.x & 15, kq = (threadIdx.x & 63) >> 4;
 #pragma unroll
         for (int n = 0; n < NR; n++) {
@@ -368,7 +379,7 @@ struct Epi {
 template <int NR>
 __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl, float* out,
                                           int ostride, int cout, const float* __restrict__ bias, bool residual,
-                                          double* slots) {
+                                          LStat& st, bool stats) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int nsub = (HW + 15) >> 4;
@@ -376,9 +387,6 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
     constexpr int NSJ = 16 * NR;
     Epi<NR> ep;
     ep.init(bias, cout);
-    LStat st;
-    lst_reset(st);
-    const bool stats = slots != nullptr;
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -415,30 +423,29 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
                     acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bq[n][s], acc1[n], 0, 0, 0);
                 }
         }
-        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        if (stats) lst_setk(st, acc0[0][0] + ep.bz[0]);
         ep.store(acc0, s0, HW, out, ostride, residual, stats, st);
         if (v1) ep.store(acc1, s1, HW, out, ostride, residual, stats, st);
     }
-    if (stats) lst_flush(st, slots);
 }
 
 // MAXNR: the widest output block count the instantiation supports (wider is compiled out, which
 // keeps the narrow instantiation's register allocation small; the host picks MAXNR per layer)
 template <int MAXNR>
 __device__ __forceinline__ void conv1_any(const float* in, int istride, int cin, int HW, const float* wl, float* out,
-                                          int ostride, int cout, const float* bias, bool residual, double* slots) {
+                                          int ostride, int cout, const float* bias, bool residual, LStat& st, bool stats) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots);
+            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats);
         else
-            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots);
+            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats);
         return;
     }
     switch (nr) {
-        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
-        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, slots); break;
+        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
+        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
+        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
     }
 }
 
@@ -458,21 +465,22 @@ __device__ __forceinline__ void build_qtab(int* qt, int cin, int ic0, int d) {
 }
 
 // 3x3 dilated conv, PK_Q4: per group g each lane reads one channel quad (tap, cq) of its shifted
-// pixel with a ds_read_b128 (zero outside the image) -> 4*NR MFMAs per subtile.
+// pixel with a ds_read_b128 -> 4*NR MFMAs per subtile. Groups are taken in chunks of CQ: the chunk's
+// quad-table entries, then every A quad of both subtiles, are issued before its MFMAs, so the two
+// dependent LDS round trips are paid once per chunk instead of once per group. Quads outside the
+// image read the 16-byte zero slot zq (branch-free).
 template <int NR>
 __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, int H, int W, const float* wl,
                                            const int* qt, float* out, int ostride, int cout,
-                                           const float* __restrict__ bias, double* slots) {
+                                           const float* __restrict__ bias, LStat& st, bool stats, const float* zq) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
     const int nsub = (HW + 15) >> 4;
     constexpr int NSJ = 16 * NR;
+    constexpr int CQ = CNF_CQ;
     Epi<NR> ep;
     ep.init(bias, cout);
-    LStat st;
-    lst_reset(st);
-    const bool stats = slots != nullptr;
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -486,49 +494,60 @@ __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, 
             acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
             acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
         }
-        for (int g = 0; g < G; g++) {
-            const int t = qt[4 * g + kq];
-            const int dr = (t & 63) - 32, dc = ((t >> 6) & 63) - 32, c = t >> 12;
-            const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
-            const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
-            const bool okb = t >= 0 && (unsigned)yb < (unsigned)H && (unsigned)xb < (unsigned)W;
-            const f4 a0 = oka ? *reinterpret_cast<const f4*>(in + (ya * W + xa) * istride + c) : f4{0.f, 0.f, 0.f, 0.f};
-            const f4 a1 = okb ? *reinterpret_cast<const f4*>(in + (yb * W + xb) * istride + c) : f4{0.f, 0.f, 0.f, 0.f};
-            const float* brow = wl + ((g * 4 + kq) * NSJ + i16) * 4;
-            f4 bq[NR];
+        for (int g0 = 0; g0 < G; g0 += CQ) {
+            int tq[CQ];
 #pragma unroll
-            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+            for (int j = 0; j < CQ; j++) tq[j] = qt[4 * min(g0 + j, G - 1) + kq];
+            f4 a0[CQ], a1[CQ];
 #pragma unroll
-            for (int s = 0; s < 4; s++)
+            for (int j = 0; j < CQ; j++) {
+                const int t = tq[j];
+                const int dr = (t & 63) - 32, dc = ((t >> 6) & 63) - 32, c = t >> 12;
+                const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
+                const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
+                const bool okb = t >= 0 && (unsigned)yb < (unsigned)H && (unsigned)xb < (unsigned)W;
+                a0[j] = *reinterpret_cast<const f4*>(oka ? in + (ya * W + xa) * istride + c : zq);
+                a1[j] = *reinterpret_cast<const f4*>(okb ? in + (yb * W + xb) * istride + c : zq);
+            }
 #pragma unroll
-                for (int n = 0; n < NR; n++) {
-                    acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s], bq[n][s], acc0[n], 0, 0, 0);
-                    acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], bq[n][s], acc1[n], 0, 0, 0);
+            for (int j = 0; j < CQ; j++) {
+                if (g0 + j < G) {
+                    const float* brow = wl + (((g0 + j) * 4 + kq) * NSJ + i16) * 4;
+                    f4 bq[NR];
+#pragma unroll
+                    for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+#pragma unroll
+                    for (int s = 0; s < 4; s++)
+#pragma unroll
+                        for (int n = 0; n < NR; n++) {
+                            acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j][s], bq[n][s], acc0[n], 0, 0, 0);
+                            acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j][s], bq[n][s], acc1[n], 0, 0, 0);
+                        }
                 }
+            }
         }
-        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        if (stats) lst_setk(st, acc0[0][0] + ep.bz[0]);
         ep.store(acc0, s0, HW, out, ostride, false, stats, st);
         if (v1) ep.store(acc1, s1, HW, out, ostride, false, stats, st);
     }
-    if (stats) lst_flush(st, slots);
 }
 
 template <int MAXNR>
 __device__ __forceinline__ void conv3q_any(const float* in, int istride, int G, int H, int W, const float* wl,
                                            const int* qt, float* out, int ostride, int cout, const float* bias,
-                                           double* slots) {
+                                           LStat& st, bool stats, const float* zq) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+            conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
         else
-            conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+            conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
         return;
     }
     if (nr == 3)
-        conv3q_lds<MAXNR >= 3 ? 3 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+        conv3q_lds<MAXNR >= 3 ? 3 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
     else
-        conv3q_lds<MAXNR >= 4 ? 4 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, slots);
+        conv3q_lds<MAXNR >= 4 ? 4 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
 }
 
 // k -> (dr, dc, c) table of a PK_KN conv over cin channels from channel ic0; -1 beyond K
@@ -547,16 +566,13 @@ __device__ __forceinline__ void build_ktab(int* ktab, int cin, int ic0, int d, i
 template <int NR>
 __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* __restrict__ bias, double* slots) {
+                                           const float* __restrict__ bias, LStat& st, bool stats) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
     const int nsub = (HW + 15) >> 4;
     Epi<NR> ep;
     ep.init(bias, cout);
-    LStat st;
-    lst_reset(st);
-    const bool stats = slots != nullptr;
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -588,29 +604,28 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
                 acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc1[n], 0, 0, 0);
             }
         }
-        if (stats && s0 == wave) lst_setk(st, acc0[0][0] + ep.bz[0]);
+        if (stats) lst_setk(st, acc0[0][0] + ep.bz[0]);
         ep.store(acc0, s0, HW, out, ostride, false, stats, st);
         if (v1) ep.store(acc1, s1, HW, out, ostride, false, stats, st);
     }
-    if (stats) lst_flush(st, slots);
 }
 
 template <int MAXNR>
 __device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* bias, double* slots) {
+                                           const float* bias, LStat& st, bool stats) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
         else
-            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
         return;
     }
     if (nr == 3)
-        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
     else
-        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, slots);
+        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
 }
 
 // entries of the tap (PK_KN) / quad (PK_Q4) table of a 3x3 conv, rounded to 4
@@ -626,11 +641,11 @@ __device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin
 template <int MAXNR>
 __device__ __forceinline__ void conv3_run(const LdsConv& cv, const float* in, int istride, int H, int W,
                                           const float* wl, const int* tab, float* out, int ostride, int cout,
-                                          const float* bias, double* slots) {
+                                          const float* bias, LStat& st, bool stats, const float* zq) {
     if (cv.fmt == PK_Q4)
-        conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, slots);
+        conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, st, stats, zq);
     else
-        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, slots);
+        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, st, stats);
 }
 
 // position in u of element (pixel p, channel c) of the compressed u1c (mask compress, :720-759)
@@ -649,19 +664,19 @@ __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int
 
 }  // namespace
 
-// Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs).
+// Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs):
+// thread 0 of every workgroup records the shader clock (s_memtime) into an LDS array at each
+// stamp point, with no barrier or memory wait of its own, so the stamps see wave 0's own timeline
+// as the timed kernel runs it; workgroup (0, 0) copies its array to g_cycles at the end (with the
+// realtime clock at both ends in g_stamps[0..1] for the cycle -> time scale).
 __device__ long long g_stamps[256];
-__device__ long long g_cycles[256];   // s_memtime (shader clock) at the same stamps
-#define STAMP(i)                                                                            \
-    do {                                                                                     \
-        if (STAMPS) {                                                                        \
-            __syncthreads();                                                                 \
-            const int si_ = (i);                                                             \
-            if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                    \
-                g_stamps[si_] = (long long)__builtin_amdgcn_s_memrealtime();                 \
-                g_cycles[si_] = (long long)__builtin_amdgcn_s_memtime();                     \
-            }                                                                                \
-        }                                                                                    \
+__device__ long long g_cycles[256];
+#define STAMP(i)                                                                             \
+    do {                                                                                      \
+        if (STAMPS && threadIdx.x == 0) {                                                     \
+            const int si_ = (i);                                                              \
+            if (si_ < 128) stamp_lds[si_] = (long long)__builtin_amdgcn_s_memtime();          \
+        }                                                                                     \
     } while (0)
 
 template <bool STAMPS, int MAXNR>
@@ -671,7 +686,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const int H = a.hc, W = a.wc, HW = H * W;
     const int nk = a.nk, gc = a.gc;
     const int SY = a.sy, S1 = a.s1, S2 = a.s2, SU = a.su;   // S2 covers max(gc, nk, dc2) channels
-    double* slots = reinterpret_cast<double*>(smem);         // NW x (n, mean, M2)
+    float* slots = reinterpret_cast<float*>(smem);           // NW x (K, S1, S2, n)
     float* Y = reinterpret_cast<float*>(smem + a.off_y);
     float* T1 = reinterpret_cast<float*>(smem + a.off_t1);
     float* T2 = reinterpret_cast<float*>(smem + a.off_t2);
@@ -681,13 +696,16 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const float* X = a.aux;
     // this net's parameter-offset table (see NetLdsArgs) copied to LDS [192, ...): every later read
     // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
-    static_assert(NW * 3 * 8 <= 192, "LN slots overlap the offset table");
+    static_assert(NW * 4 * 4 <= 192, "LN slots overlap the offset table");
     int* otab = reinterpret_cast<int*>(smem + 192);
     for (int i = threadIdx.x; i < a.offs_per_net; i += NT) otab[i] = a.offs[net * a.offs_per_net + i];
+    // 16 zero bytes right below Y: the source of every 3x3 tap quad outside the image
+    float* ZQ = reinterpret_cast<float*>(smem + a.off_y - 16);
+    if (threadIdx.x < 4) ZQ[threadIdx.x] = 0.f;
     lds_barrier();
     const int* off = otab;
     const bool ln = a.ln != 0;
-    double* sl = ln ? slots : nullptr;
+    LStat st;   // LN statistics of the tensor being produced
     float mu = 0.f, rstd = 1.f;
     const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
     const int per_rb = 10 + 2 * a.nbr;
@@ -699,6 +717,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const bool yq = ln && (nk & 3) == 0, tq = ln && (gc & 3) == 0;
 
     int sti = 0;
+    long long* stamp_lds = reinterpret_cast<long long*>(smem + a.stamp_off);
+    long long rt0 = 0;
+    if (STAMPS && threadIdx.x == 0) rt0 = (long long)__builtin_amdgcn_s_memrealtime();
     STAMP(sti++);
     // packed conv images carry their bias right behind the weights (cnf_plan.cpp pack()): one
     // copy stages both, and every conv reads its bias from LDS
@@ -722,7 +743,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     {
         conv3_table(a.ci, KT, a.dc1, 0, 1);
         wpf_store(pf, WL, X + off[0]);
-        lst_zero(slots);
+        lst_reset(st);
         lds_barrier();
         if (a.R > 0)
             wpf_load(pf, X + rbo(0)[2], wb(a.ca, nk));
@@ -730,7 +751,8 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
         if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
-        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, sl);
+        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, st, ln, ZQ);
+        if (ln) lst_flush(st, slots);
         lds_barrier();
         STAMP(sti++);
     }
@@ -738,32 +760,44 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const int* o = rbo(r);
         // LN1(LReLU(y)) -> T2, conv_a (1x1 nk->nk) -> T1 (+ LN2 stats)
         if (ln) lst_final(slots, mu, rstd);
+        STAMP(sti++);
         if (yq)
             ln_full(Y, SY, T2, S2, HW, nk, mu, rstd, lp, P + o[0], P + o[1]);
         else
             ln_apply(Y, SY, T2, S2, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
-        wpf_store(pf, WL, X + o[2]);
-        lds_barrier();   // every wave has read the Y slots; T2 and W are complete
-        lst_zero(slots);
-        wpf_load(pf, X + o[10], brw(o));
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, sl);
+        wpf_store(pf, WL, X + o[2]);
+        STAMP(sti++);
+        lds_barrier();   // every wave has read the Y slots; T2 and W are complete
+        lst_reset(st);
+        wpf_load(pf, X + o[10], brw(o));
+        // LN2 over the whole of T1 when quad-shaped (vectorised, gamma/beta prefetched behind conv_a);
+        // the branches read only their windows of it
+        if (yq) lnp_load(lp, P + o[4], P + o[5], HW * nk / 4);
+        STAMP(sti++);
+        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, st, ln);
+        if (ln) lst_flush(st, slots);
+        STAMP(sti++);
         lds_barrier();
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
         if (ln) lst_final(slots, mu, rstd);
-        if (a.nwin == 1)
+        STAMP(sti++);
+        if (yq)
+            ln_full(T1, S1, T1, S1, HW, nk, mu, rstd, lp, P + o[4], P + o[5]);
+        else if (a.nwin == 1)
             ln_apply(T1, S1, T1, S1, HW, a.win_off[0], a.win_len[0], nk, mu, rstd, ln ? P + o[4] : nullptr,
                      ln ? P + o[5] : nullptr, ln);
         else
             ln_windows(T1, S1, HW, nk, a.nwin, a.win_off, a.win_len, mu, rstd, ln ? P + o[4] : nullptr,
                        ln ? P + o[5] : nullptr, ln);
+        STAMP(sti++);
         if (tq) lnp_load(lp, P + o[6], P + o[7], HW * gc / 4);
         // grouped dilated branches -> T2[:, out_off : out_off + cout] (+ LN3 stats over all of them)
         // every branch's packed image (contiguous in aux: weights + bias per branch) and tap / quad
         // table staged at once: the branches run back to back without barriers between them (they
         // read T1 and write disjoint T2 slices), each wave merging its LN3 partials across them
-        {
+        if (r == 0) {   // the same for every residual block (conv_out builds its own after the loop)
             int kto = 0;
             for (int bi = 0; bi < a.nbr; bi++) {
                 const LdsConv& cv = a.gcv[bi];
@@ -771,9 +805,11 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                 kto += ktab_len(cv);
             }
         }
+        STAMP(sti++);
         wpf_store(pf, WL, X + o[10]);
+        STAMP(sti++);
         lds_barrier();   // LN2 applied, slots read, branch images and tables complete
-        lst_zero(slots);
+        lst_reset(st);
         wpf_load(pf, X + o[8], wb(a.cb, nk));
         STAMP(sti++);
         {
@@ -782,21 +818,26 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                 const LdsConv& cv = a.gcv[bi];
                 const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
                 conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
-                          WL + (o[11 + 2 * bi] - o[10]), sl);
+                          WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ);
                 kto += ktab_len(cv);
             }
         }
+        if (ln) lst_flush(st, slots);
         STAMP(sti++);
         lds_barrier();
+        STAMP(sti++);
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
         if (ln) lst_final(slots, mu, rstd);
+        STAMP(sti++);
         if (tq)
             ln_full(T2, S2, T2, S2, HW, gc, mu, rstd, lp, P + o[6], P + o[7]);
         else
             ln_apply(T2, S2, T2, S2, HW, 0, gc, gc, mu, rstd, ln ? P + o[6] : nullptr, ln ? P + o[7] : nullptr, ln);
+        STAMP(sti++);
         wpf_store(pf, WL, X + o[8]);
+        STAMP(sti++);
         lds_barrier();
-        lst_zero(slots);
+        lst_reset(st);
         if (r + 1 < a.R)
             wpf_load(pf, X + rbo(r + 1)[2], wb(a.ca, nk));
         else
@@ -805,7 +846,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
                      HW * nk / 4);
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, sl);
+        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, st, ln);
+        if (ln) lst_flush(st, slots);
+        STAMP(sti++);
         lds_barrier();
         STAMP(sti++);
     }
@@ -829,7 +872,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv1_any<MAXNR>(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, nullptr);
+            conv1_any<MAXNR>(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, st, false);
             lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -853,7 +896,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             conv3_table(a.co, KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, nullptr);
+            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, st, false, ZQ);
             lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -863,7 +906,12 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         }
     }
     STAMP(sti++);
-    if (STAMPS && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_stamps[255] = sti;
+    if (STAMPS && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        g_stamps[0] = rt0;
+        g_stamps[1] = (long long)__builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < sti && i < 128; i++) g_cycles[i] = stamp_lds[i];
+        g_stamps[255] = sti;
+    }
 }
 
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
@@ -876,8 +924,14 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         return e && std::atoi(e) != 0;
     }();
     const bool narrow = a.maxnr <= 2 && !wide;
-    if (stamps)
-        hipLaunchKernelGGL((k_net_lds<true, 5>), dim3(B, 2), dim3(NT), lds, st, a);
+    if (stamps) {
+        NetLdsArgs b = a;
+        b.stamp_off = (lds + 15) & ~15;
+        if (narrow)
+            hipLaunchKernelGGL((k_net_lds<true, 2>), dim3(B, 2), dim3(NT), b.stamp_off + 1024, st, b);
+        else
+            hipLaunchKernelGGL((k_net_lds<true, 5>), dim3(B, 2), dim3(NT), b.stamp_off + 1024, st, b);
+    }
     else if (narrow)
         hipLaunchKernelGGL((k_net_lds<false, 2>), dim3(B, 2), dim3(NT), lds, st, a);
     else
