@@ -342,7 +342,7 @@ struct Epi {
         for (int n = 0; n < NR; n++) {
             const int ch = n * 16 + i16;
             chv[n] = ch < cout;
-            const float b = bias[chv[n] ? ch : 0];   // unconditional LDS read: no divergent block
+            const float b = bias != nullptr ? bias[chv[n] ? ch : 0] : 0.f;   // unconditional LDS read
             bz[n] = chv[n] ? b : 0.f;
         }
     }
@@ -375,16 +375,16 @@ struct Epi {
 };
 
 // 1x1 conv: A = in[p][0..cin) (pixel stride == 8 mod 16), PK_1X1 image wl ([g][q][j][s], lane
-// (i, q) holds channels 16g + 4q + s at k-step s); out[p][n] (+)= bias + A.B
+// (i, q) holds channels 16g + 4q + s at k-step s); out[p][n] (+)= bias + A.B. nsj / nb0: column
+// count of the packed image and first 16-column block this call computes (column-chunked calls).
 template <int NR>
 __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl, float* out,
                                           int ostride, int cout, const float* __restrict__ bias, bool residual,
-                                          LStat& st, bool stats) {
+                                          LStat& st, bool stats, int nsj, int nb0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int nsub = (HW + 15) >> 4;
     const int G = (cin + 15) >> 4;
-    constexpr int NSJ = 16 * NR;
     Epi<NR> ep;
     ep.init(bias, cout);
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
@@ -411,7 +411,7 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
                         a1[j] = 0.f;
                     }
             }
-            const float* brow = wl + ((g * 4 + kq) * NSJ + i16) * 4;
+            const float* brow = wl + ((g * 4 + kq) * nsj + i16) * 4 + nb0 * 64;
             f4 bq[NR];
 #pragma unroll
             for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
@@ -433,19 +433,21 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
 // keeps the narrow instantiation's register allocation small; the host picks MAXNR per layer)
 template <int MAXNR>
 __device__ __forceinline__ void conv1_any(const float* in, int istride, int cin, int HW, const float* wl, float* out,
-                                          int ostride, int cout, const float* bias, bool residual, LStat& st, bool stats) {
+                                          int ostride, int cout, const float* bias, bool residual, LStat& st, bool stats,
+                                          int nsj = 0, int nb0 = 0) {
     const int nr = (cout + 15) / 16;
+    if (nsj == 0) nsj = 16 * nr;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats);
+            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0);
         else
-            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats);
+            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0);
         return;
     }
     switch (nr) {
-        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
-        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
-        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats); break;
+        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
+        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
+        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
     }
 }
 
@@ -868,29 +870,57 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             // out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]
             const int ncol = 9 * a.dc2;
             const int co_nr = (ncol + 15) / 16;
-            const int CS = 16 * co_nr + 1;
+            const bool vq = (a.dc2 & 3) == 0;   // quad-shaped output: 16-byte tap-sum reads
+            const int CS = 16 * co_nr + (vq ? 4 : 1);
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv1_any<MAXNR>(Y, SY, nk, HW, WL, C, CS, ncol, a.zero_bias, false, st, false);
+            // in chunks of CB 16-column blocks (the narrow instantiation computes at most two at once)
+            constexpr int CB = MAXNR >= 5 ? 5 : 2;
+            STAMP(sti++);
+            for (int nb = 0; nb < co_nr; nb += CB)
+                conv1_any<MAXNR>(Y, SY, nk, HW, WL, C + 16 * nb, CS, min(16 * CB, ncol - 16 * nb), nullptr, false, st,
+                                 false, 16 * co_nr, nb);
+            STAMP(sti++);
             lds_barrier();
-            const int n = HW * a.dc2;
-            for (int e = threadIdx.x; e < n; e += NT) {
-                const int p = e / a.dc2, oc = e - p * a.dc2;
-                const int pr = p / W, pc = p - pr * W;
-                float acc = bias[oc];
+            STAMP(sti++);
+            if (vq) {
+                // one output quad per item: 9 tap quads issued together (outside the image: ZQ)
+                const int nq = a.dc2 >> 2, n = HW * nq;
+                for (int e = threadIdx.x; e < n; e += NT) {
+                    const int p = e / nq, oq = (e - p * nq) << 2;
+                    const int pr = p / W, pc = p - pr * W;
+                    f4 t[9];
 #pragma unroll
-                for (int kh = 0; kh < 3; kh++) {
-                    const int sr = pr + kh - 1;
-                    if (sr < 0 || sr >= H) continue;
-#pragma unroll
-                    for (int kw = 0; kw < 3; kw++) {
-                        const int sc = pc + kw - 1;
-                        if (sc < 0 || sc >= W) continue;
-                        acc += C[(sr * W + sc) * CS + (kh * 3 + kw) * a.dc2 + oc];
+                    for (int k = 0; k < 9; k++) {
+                        const int sr = pr + k / 3 - 1, sc = pc + k % 3 - 1;
+                        const bool ok = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+                        t[k] = *reinterpret_cast<const f4*>(ok ? C + (sr * W + sc) * CS + k * a.dc2 + oq : ZQ);
                     }
+                    f4 acc = *reinterpret_cast<const f4*>(bias + oq);
+#pragma unroll
+                    for (int k = 0; k < 9; k++) acc += t[k];
+                    *reinterpret_cast<f4*>(dst + p * a.dc2 + oq) = acc;
                 }
-                dst[e] = acc;
+            } else {
+                const int n = HW * a.dc2;
+                for (int e = threadIdx.x; e < n; e += NT) {
+                    const int p = e / a.dc2, oc = e - p * a.dc2;
+                    const int pr = p / W, pc = p - pr * W;
+                    float acc = bias[oc];
+#pragma unroll
+                    for (int kh = 0; kh < 3; kh++) {
+                        const int sr = pr + kh - 1;
+                        if (sr < 0 || sr >= H) continue;
+#pragma unroll
+                        for (int kw = 0; kw < 3; kw++) {
+                            const int sc = pc + kw - 1;
+                            if (sc < 0 || sc >= W) continue;
+                            acc += C[(sr * W + sc) * CS + (kh * 3 + kw) * a.dc2 + oc];
+                        }
+                    }
+                    dst[e] = acc;
+                }
             }
         } else {
             conv3_table(a.co, KT, nk, 0, 1);

@@ -94,7 +94,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     g.su = ci_fmt == PK_Q4 ? stride8(c.dc1) : stride2(c.dc1);
     g.s2r = std::max(g.s2, g.su);
     if (co_fmt == PK_TAP)   // tap-decomposed conv_out scratch (stride 16*nr+1) spans T1..T2
-        g.s2r = std::max(g.s2r, 16 * ((9 * c.dc2 + 15) / 16) + 1 - g.s1);
+        g.s2r = std::max(g.s2r, 16 * ((9 * c.dc2 + 15) / 16) + (c.dc2 % 4 == 0 ? 4 : 1) - g.s1);
     int64_t wmax = 0, sz;
     int kmax = 4, kp;
     auto acc = [&](int fmt, int ks, int cin, int cout) {
@@ -366,14 +366,24 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 if (const char* e = std::getenv("CNF_NETLDS_MAXHW"))   // tuning: stream layers above this size
                     if (c.hc * c.wc > std::atoi(e)) continue;
                 const int ci9 = c.dc1 % 4 == 0 ? PK_Q4 : PK_KN;
-                // tap-decomposed conv_out only up to 32 tap columns (NR <= 2)
-                int tapmax = 32;   // wider conv_outs take the PK_Q4 3x3 path (narrow instantiation)
-                if (const char* e = std::getenv("CNF_CO_TAPMAX")) tapmax = std::atoi(e);   // tuning
-                const int co9 = 9 * c.dc2 <= tapmax ? PK_TAP : (c.nk % 4 == 0 ? PK_Q4 : PK_KN);
+                // conv_out: the tap-decomposed form (1x1 GEMM to 9*dc2 columns, computed in 32-column
+                // chunks, + a 9-point shifted sum) when it needs fewer MFMAs than the quad-packed 3x3
+                // (ceil(nk/16) * ceil(9 dc2/16) against ceil(9 nk/16) * ceil(dc2/16) 16x16 blocks)
+                const int tap_cost = (c.nk + 15) / 16 * ((9 * c.dc2 + 15) / 16);
+                const int q4_cost = (9 * c.nk + 15) / 16 * ((c.dc2 + 15) / 16);
+                bool tap = tap_cost < q4_cost;
+                if (const char* e = std::getenv("CNF_CO_TAPMAX")) tap = 9 * c.dc2 <= std::atoi(e);   // tuning
+                const int coq = c.nk % 4 == 0 ? PK_Q4 : PK_KN;
                 std::vector<int> gc9;
                 for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_Q4 : PK_KN);
                 NetLdsGeom g;
-                if (netlds_geometry(c, ci9, co9, gc9, g)) {
+                int co9 = tap ? PK_TAP : coq;
+                bool fit = netlds_geometry(c, ci9, co9, gc9, g);
+                if (!fit && co9 == PK_TAP) {   // the tap scratch did not fit: quad-packed conv_out
+                    co9 = coq;
+                    fit = netlds_geometry(c, ci9, co9, gc9, g);
+                }
+                if (fit) {
                     c.ci_fmt = ci9;
                     c.co_fmt = co9;
                     c.gc_fmt = gc9;

@@ -493,7 +493,8 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     a.off_w = g.off_w;
     a.off_k = g.off_k;
     auto nr = [](int cout) { return (cout + 15) / 16; };
-    a.maxnr = std::max(nr(c.nk), nr(c.co_fmt == PK_TAP ? 9 * c.dc2 : c.dc2));
+    // the tap-decomposed conv_out runs in chunks of at most two 16-column blocks
+    a.maxnr = std::max(nr(c.nk), c.co_fmt == PK_TAP ? std::min(2, nr(9 * c.dc2)) : nr(c.dc2));
     for (const Branch& b : c.br) a.maxnr = std::max(a.maxnr, nr(b.cout));
     if (const char* e = std::getenv("CNF_NETLDS_VERBOSE"))
         if (std::atoi(e)) std::fprintf(stderr, "netlds layer hc=%d wc=%d nk=%d dc2=%d co_fmt=%d maxnr=%d\n", c.hc, c.wc,

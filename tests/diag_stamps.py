@@ -46,5 +46,5 @@ for li, layer in enumerate(flow.layers_list):
     R = (n - 5) // len(RB)
     for r in range(R):
         labels += [f'{x}' for x in RB]
-    labels += ['LN_out', 'conv_out']
+    labels += ['LN_out', 'co.W+bar', 'co.gemm', 'co.bar', 'co.sum+end'] if n - 5 - R * len(RB) == 3 else ['LN_out', 'conv_out']
     print('   ' + '  '.join(f'{lab}={v:.2f}' for lab, v in zip(labels, d)))

@@ -14,7 +14,7 @@ kink and the gradient of whole tensors moves by a DISCRETE amount (cfg2 B=2: flo
 itself moves by 7.5e-3 relative in layer c11, 2e-1 in c5, when xy is perturbed by 1e-7..1e-6
 relative, while each layer's own VJP at the float64 activations matches to ~1e-6). The bar is
 therefore, per parameter tensor, with g_ref the float64 gradient, g32 torch fp32 autograd and
-spread = max over 4 float64 gradients at xy * (1 + eps * N(0,1)), eps in PERTURB, of |g_pert - g_ref|:
+spread = max over 9 float64 gradients at xy * (1 + eps * N(0,1)), eps in PERTURB, of |g_pert - g_ref|:
   max|g - g_ref| <= K * max|g32 - g_ref| + KP * max(spread)
                     + GRAD_RTOL * max|g_ref| + GRAD_ATOL * max_all|g_ref|,
 K = K32_LAYER for one coupling layer's backward (no perturbation term: the strict per-layer bar of
@@ -32,7 +32,10 @@ from oracle.cflow_torch_cpu import TorchCPUFlow
 
 K32 = 10.0        # whole flow: 16 layers of fp32 rounding compound differently than torch's
 K32_LAYER = 4.0   # one coupling layer
-PERTURB = (1e-7, 1e-6)   # relative input perturbations ~ the fp32 forward's own rounding (2 seeds each)
+# relative input perturbations ~ the fp32 forward's own rounding, which compounds over the 16
+# layers: by c7 the HIP forward's activations sit a few 1e-6 from the float64 ones
+PERTURB = (1e-7, 1e-6, 4e-6)
+PERTURB_SEEDS = 3         # seeds per eps: the spread is a sampled estimate
 PERTURB_CASES = ('cfg2',)  # deep enough for kink flips (the small presets pass without the term)
 KP = 2.0          # whole flow: multiple of the float64 gradient's spread under PERTURB
 GRAD_RTOL = 1e-4
@@ -158,7 +161,7 @@ def test_gradients_match_oracle(gpu, name, B, extra):
     if name in PERTURB_CASES:
         rng = np.random.default_rng(11)
         for eps in PERTURB:
-            for _ in range(2):
+            for _ in range(PERTURB_SEEDS):
                 Gp, _ = oracle_grads(kw, P, np.asarray(xy, np.float64) * (1.0 + eps * rng.standard_normal(xy.shape)))
                 for k in G_spread:
                     G_spread[k] = np.maximum(G_spread[k], np.abs(Gp[k].reshape(-1) - G_ref[k].reshape(-1)))
