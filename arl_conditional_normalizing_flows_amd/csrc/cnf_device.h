@@ -64,11 +64,14 @@ __device__ __forceinline__ bool stored(const ConvProb& P, int ch) {
 }
 
 // LN statistics of a conv output, produced in the conv's epilogue (no extra pass, no barrier):
-// each wave writes the partial (n, mean, M2) of the LeakyReLU'd values its lanes hold. Sums are
-// fp32 shifted by a wave-uniform sample value K (readfirstlane), so sum (x-K)^2 does not cancel;
-// the (n, mean, M2) conversion and every cross-wave merge are fp64.
+// each wave writes the partial (K, S1, S2, n) of the LeakyReLU'd values its lanes hold — fp32 sums
+// shifted by a wave-uniform sample value K (readfirstlane), so sum (x-K)^2 does not cancel — as
+// one 16-byte store by lane 0 (DPP reductions, no division, no fp64).
 template <int N>
-__device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&valid)[N], double* __restrict__ dst) {
+__device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&valid)[N], float* __restrict__ dst) {
+#ifdef CNF_ABL_NOPART
+    return;
+#endif
     const float K = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, vals[0])));
     float s1 = 0.f, s2 = 0.f, c = 0.f;
 #pragma unroll
@@ -81,18 +84,11 @@ __device__ __forceinline__ void ln_partial(const float (&vals)[N], const bool (&
     s1 = wave_sum_f(s1);
     s2 = wave_sum_f(s2);
     c = wave_sum_f(c);
-    if ((threadIdx.x & 63) == 0) {
-        const double n = c, S1 = s1, S2 = s2;
-        const double m = n > 0.0 ? S1 / n : 0.0;
-        double M2 = S2 - S1 * m;
-        dst[0] = n;
-        dst[1] = n > 0.0 ? (double)K + m : 0.0;
-        dst[2] = M2 > 0.0 ? M2 : 0.0;
-    }
+    if ((threadIdx.x & 63) == 0) *reinterpret_cast<f4*>(dst) = f4{K, s1, s2, c};
 }
 
 // Streaming form of ln_partial for epilogues that produce their values in several steps: lanes
-// accumulate shifted fp32 sums; write() reduces over the wave and stores (n, mean, M2) in fp64.
+// accumulate shifted fp32 sums; write() reduces over the wave and stores (K, S1, S2, n).
 struct LnAcc {
     float K, s1, s2, c;
     __device__ __forceinline__ void reset() { K = s1 = s2 = c = 0.f; }
@@ -106,43 +102,47 @@ struct LnAcc {
         s2 = fmaf(d, d, s2);
         c += valid ? 1.f : 0.f;
     }
-    __device__ __forceinline__ void write(double* __restrict__ dst) const {
-        const float S1f = wave_sum_f(s1), S2f = wave_sum_f(s2), cf = wave_sum_f(c);
-        if ((threadIdx.x & 63) == 0) {
-            const double n = cf, S1 = S1f;
-            const double m = n > 0.0 ? S1 / n : 0.0;
-            const double M2 = (double)S2f - S1 * m;
-            dst[0] = n;
-            dst[1] = n > 0.0 ? (double)K + m : 0.0;
-            dst[2] = M2 > 0.0 ? M2 : 0.0;
-        }
+    __device__ __forceinline__ void write(float* __restrict__ dst) const {
+#ifdef CNF_ABL_NOPART
+        return;
+#endif
+        const float S1 = wave_sum_f(s1), S2 = wave_sum_f(s2), C = wave_sum_f(c);
+        if ((threadIdx.x & 63) == 0) *reinterpret_cast<f4*>(dst) = f4{K, S1, S2, C};
     }
 };
 
 // (mean, rstd) of the input LayerNorm of image img from the producer's partials, merged by every
-// wave on its own (parallel-axis form: one division, fixed order, no barrier); identity without LN.
+// wave on its own (no barrier); identity without LN. Each lane folds its partials (Chan merge when
+// it holds more than one), then the wave merges per-lane (n, mean, M2) in the parallel-axis form
+// (N = sum n, mean = sum n m / N, M2 = sum M2 + n (m - mean)^2) with DPP sums: fixed order, fp32.
 __device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
     mu = 0.f;
     rstd = 1.f;
     if (P.in_part == nullptr) return;
+#ifdef CNF_ABL_NOINLN
+    return;
+#endif
     const int lane = threadIdx.x & 63;
-    const double* __restrict__ q = P.in_part + (size_t)img * P.part_stride * 3;
-    double ln = 0.0, ls = 0.0;
+    const float* __restrict__ q = P.in_part + (size_t)img * P.part_stride * LNP;
+    float n = 0.f, m = 0.f, M2 = 0.f;
     for (int i = lane; i < P.in_nparts; i += 64) {
-        const double n = q[3 * i];
-        ln += n;
-        ls += n * q[3 * i + 1];
+        const f4 v = *reinterpret_cast<const f4*>(q + (size_t)LNP * i);
+        if (v[3] > 0.f) {
+            const float r = v[1] * __builtin_amdgcn_rcpf(v[3]);
+            const float mi = v[0] + r, M2i = fmaxf(fmaf(-v[1], r, v[2]), 0.f);
+            const float nn = n + v[3], dl = mi - m, f = v[3] * __builtin_amdgcn_rcpf(nn);
+            m = fmaf(dl, f, m);
+            M2 = M2 + M2i + dl * dl * n * f;
+            n = nn;
+        }
     }
-    const double nt = wave_sum(ln);
-    const double mt = wave_sum(ls) / nt;
-    double lm = 0.0;
-    for (int i = lane; i < P.in_nparts; i += 64) {
-        const double d = q[3 * i + 1] - mt;
-        lm += q[3 * i + 2] + q[3 * i] * d * d;
-    }
-    const double M2 = wave_sum(lm);
-    mu = (float)mt;
-    rstd = (float)(1.0 / sqrt(M2 / nt + (double)LN_EPS));
+    const float N = wave_sum_f(n);
+    const float iN = __builtin_amdgcn_rcpf(N);
+    const float mean = wave_sum_f(n * m) * iN;
+    const float d = m - mean;
+    const float M = wave_sum_f(fmaf(n * d, d, M2));
+    mu = mean;
+    rstd = __builtin_amdgcn_rsqf(fmaf(M, iN, LN_EPS));
 }
 
 // Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.

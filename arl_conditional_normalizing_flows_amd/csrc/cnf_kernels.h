@@ -10,6 +10,9 @@ namespace cnf {
 constexpr float LRELU_ALPHA = 0.3f;      // keras.layers.LeakyReLU() default
 constexpr float LN_EPS = 1e-3f;          // keras.layers.LayerNormalization() default
 constexpr double LOG_2PI_D = 1.8378770664093453;
+// LayerNorm statistics partial of one producing wave: (K, S1, S2, n) with S1 = sum(x - K),
+// S2 = sum((x - K)^2) over its n values of LeakyReLU(out), K a sample of them (fp32, 16 bytes)
+constexpr int LNP = 4;
 
 constexpr int MAXPROB = 12;
 
@@ -22,7 +25,7 @@ enum { ROLE_CONV_IN = 0, ROLE_CONV_A = 1, ROLE_GC = 2, ROLE_CONV_B = 3, ROLE_CON
 // One convolution problem of a k_conv launch (blockIdx.y selects the problem).
 struct ConvProb {
     const float* in;          // NHWC, image 0
-    const double* in_part;    // LN partials (n, mean, M2) of the input tensor [B][part_stride][3] (first
+    const float* in_part;     // LN partials (K, S1, S2, n) of the input tensor [B][part_stride][LNP] (first
                               // in_nparts slots valid), or null (no LN)
     const float* gamma;       // LN gamma over the full in_cs-channel tensor (per h,w,c)
     const float* beta;
@@ -30,7 +33,7 @@ struct ConvProb {
     const float* bias;        // [cout]
     const float* res;         // residual, same layout as out, or null
     float* out;
-    double* out_part;         // per-wave LN partials of LeakyReLU(out) [B][part_stride][3], or null
+    float* out_part;          // per-wave LN partials of LeakyReLU(out) [B][part_stride][LNP], or null
     int in_cs, in_off, cin, in_nparts;
     int out_cs, out_off, cout, part_stride, out_part_base;
     int dil, act;
@@ -86,6 +89,7 @@ struct NetLdsArgs {
     LdsConv ci, ca, cb, co, gcv[NETLDS_MAXBR];   // packed images of conv_in, conv_a, conv_b, conv_out, branches
     const float* zero_bias;                      // >= 128 zeros (tap GEMM has no bias)
     int off_y, off_t1, off_t2, off_w, off_k;     // LDS byte offsets
+    int off_ks;                                  // K-split partial buffers (0: the image has > 4 subtiles)
     int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
     int stamp_off;                               // diagnostic stamp builds: LDS byte offset of the stamp array
 };
@@ -104,8 +108,8 @@ struct GcBranch {
 struct GcArgs {
     const float* in[2];          // t1 per net [B][HW][in_cs]
     float* out[2];               // t2 per net [B][HW][out_cs]
-    const double* in_part[2];    // LN2 partials of t1 (null: no LN)
-    double* out_part[2];         // LN3 partials of LeakyReLU(t2)
+    const float* in_part[2];     // LN2 partials of t1 (null: no LN)
+    float* out_part[2];          // LN3 partials of LeakyReLU(t2)
     const float* gamma[2];       // LN2 gamma/beta [HW][in_cs]
     const float* beta[2];
     const float* w[2][GC_MAXBR];

@@ -91,7 +91,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvProb& P, f4 (&acc)[MR][N
                     valid[(m * NR + n) * 4 + r] = pv[m][r] && chv[n];
                 }
         ln_partial(vals, valid,
-                   P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tr * 4 + (threadIdx.x >> 6)) * 3);
+                   P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tr * 4 + (threadIdx.x >> 6)) * LNP);
     }
 }
 

@@ -374,19 +374,92 @@ struct Epi {
     }
 };
 
+// K-split for images of at most NW/2 subtiles (4x4 .. 8x8 compressed images): instead of leaving
+// most waves idle, wave w takes subtile w % nsub and K slice w / nsub of KS = NW / nsub; slices
+// 1..KS-1 park their partial accumulators in LDS, and after one barrier slice 0 sums them in a fixed
+// order (bitwise reproducible) and runs the epilogue. Two buffers alternate (par), so a conv that
+// follows without a barrier of its own (the grouped branches, the tap-GEMM chunks) never overwrites
+// partials still being read.
+struct KSplit {
+    float* buf;   // two buffers of (NW - 1) x 5 blocks x 64 lanes x 4 floats (null: no K-split)
+    int par;
+};
+constexpr int KS_BUF = (NW - 1) * 5 * 64 * 4;   // floats per buffer
+// the K-split pays when at least half the waves would idle and there are K groups to split
+__device__ __forceinline__ bool ks_on(const KSplit& ks, int nsub, int G) {
+    return ks.buf != nullptr && 2 * nsub <= NW && G >= 2;
+}
+__device__ __forceinline__ void ks_slice(int nsub, int G, int& s, int& k, int& KS, int& glo, int& ghi) {
+    const int wave = threadIdx.x >> 6;
+    KS = min(NW / nsub, G);
+    s = wave % nsub;
+    k = wave / nsub;
+    glo = k < KS ? (k * G) / KS : 0;
+    ghi = k < KS ? ((k + 1) * G) / KS : 0;
+}
+template <int NR>
+__device__ __forceinline__ void ks_finish(f4 (&acc)[NR], int s, int k, int KS, int nsub, const KSplit& ks,
+                                          Epi<NR>& ep, int HW, float* out, int ostride, bool residual, bool stats,
+                                          LStat& st) {
+    const int lane = threadIdx.x & 63;
+    float* b = ks.buf + ks.par * KS_BUF;
+    if (k > 0 && k < KS) {
+#pragma unroll
+        for (int n = 0; n < NR; n++)
+            *reinterpret_cast<f4*>(b + ((((k - 1) * nsub + s) * NR + n) * 64 + lane) * 4) = acc[n];
+    }
+    lds_barrier();
+    if (k == 0) {
+        for (int kk = 1; kk < KS; kk++)
+#pragma unroll
+            for (int n = 0; n < NR; n++)
+                acc[n] += *reinterpret_cast<const f4*>(b + ((((kk - 1) * nsub + s) * NR + n) * 64 + lane) * 4);
+        if (stats) lst_setk(st, acc[0][0] + ep.bz[0]);
+        ep.store(acc, s, HW, out, ostride, residual, stats, st);
+    }
+}
+
 // 1x1 conv: A = in[p][0..cin) (pixel stride == 8 mod 16), PK_1X1 image wl ([g][q][j][s], lane
 // (i, q) holds channels 16g + 4q + s at k-step s); out[p][n] (+)= bias + A.B. nsj / nb0: column
 // count of the packed image and first 16-column block this call computes (column-chunked calls).
 template <int NR>
 __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin, int HW, const float* wl, float* out,
                                           int ostride, int cout, const float* __restrict__ bias, bool residual,
-                                          LStat& st, bool stats, int nsj, int nb0) {
+                                          LStat& st, bool stats, int nsj, int nb0, const KSplit& ks) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int nsub = (HW + 15) >> 4;
     const int G = (cin + 15) >> 4;
     Epi<NR> ep;
     ep.init(bias, cout);
+    if (ks_on(ks, nsub, G)) {
+        int s, k, KS, glo, ghi;
+        ks_slice(nsub, G, s, k, KS, glo, ghi);
+        f4 acc[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+        const int pa = s * 16 + i16;
+        const bool pva = pa < HW;
+        for (int g = glo; g < ghi; g++) {
+            const int c0 = 16 * g + 4 * kq;
+            f4 a0 = (pva && c0 < cin) ? *reinterpret_cast<const f4*>(in + pa * istride + c0) : f4{0.f, 0.f, 0.f, 0.f};
+            if (c0 + 4 > cin) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (c0 + j >= cin) a0[j] = 0.f;
+            }
+            const float* brow = wl + ((g * 4 + kq) * nsj + i16) * 4 + nb0 * 64;
+            f4 bq[NR];
+#pragma unroll
+            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int n = 0; n < NR; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s4], bq[n][s4], acc[n], 0, 0, 0);
+        }
+        ks_finish<NR>(acc, s, k, KS, nsub, ks, ep, HW, out, ostride, residual, stats, st);
+        return;
+    }
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -434,20 +507,20 @@ __device__ __forceinline__ void conv1_lds(const float* in, int istride, int cin,
 template <int MAXNR>
 __device__ __forceinline__ void conv1_any(const float* in, int istride, int cin, int HW, const float* wl, float* out,
                                           int ostride, int cout, const float* bias, bool residual, LStat& st, bool stats,
-                                          int nsj = 0, int nb0 = 0) {
+                                          const KSplit& ks, int nsj = 0, int nb0 = 0) {
     const int nr = (cout + 15) / 16;
     if (nsj == 0) nsj = 16 * nr;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0);
+            conv1_lds<1>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0, ks);
         else
-            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0);
+            conv1_lds<2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0, ks);
         return;
     }
     switch (nr) {
-        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
-        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
-        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0); break;
+        case 3: conv1_lds<MAXNR >= 3 ? 3 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0, ks); break;
+        case 4: conv1_lds<MAXNR >= 4 ? 4 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0, ks); break;
+        default: conv1_lds<MAXNR >= 5 ? 5 : 2>(in, istride, cin, HW, wl, out, ostride, cout, bias, residual, st, stats, nsj, nb0, ks); break;
     }
 }
 
@@ -474,7 +547,8 @@ __device__ __forceinline__ void build_qtab(int* qt, int cin, int ic0, int d) {
 template <int NR>
 __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, int H, int W, const float* wl,
                                            const int* qt, float* out, int ostride, int cout,
-                                           const float* __restrict__ bias, LStat& st, bool stats, const float* zq) {
+                                           const float* __restrict__ bias, LStat& st, bool stats, const float* zq,
+                                           const KSplit& ks) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
@@ -483,6 +557,33 @@ __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, 
     constexpr int CQ = CNF_CQ;
     Epi<NR> ep;
     ep.init(bias, cout);
+    if (ks_on(ks, nsub, G)) {
+        int s, k, KS, glo, ghi;
+        ks_slice(nsub, G, s, k, KS, glo, ghi);
+        f4 acc[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+        const int pa = s * 16 + i16;
+        const bool pva = pa < HW;
+        const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
+        for (int g = glo; g < ghi; g++) {
+            const int t = qt[4 * g + kq];
+            const int dr = (t & 63) - 32, dc = ((t >> 6) & 63) - 32, c = t >> 12;
+            const int ya = ra + dr, xa = ca + dc;
+            const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
+            const f4 a0 = *reinterpret_cast<const f4*>(oka ? in + (ya * W + xa) * istride + c : zq);
+            const float* brow = wl + ((g * 4 + kq) * NSJ + i16) * 4;
+            f4 bq[NR];
+#pragma unroll
+            for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + n * 64);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+                for (int n = 0; n < NR; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[s4], bq[n][s4], acc[n], 0, 0, 0);
+        }
+        ks_finish<NR>(acc, s, k, KS, nsub, ks, ep, HW, out, ostride, false, stats, st);
+        return;
+    }
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -537,19 +638,19 @@ __device__ __forceinline__ void conv3q_lds(const float* in, int istride, int G, 
 template <int MAXNR>
 __device__ __forceinline__ void conv3q_any(const float* in, int istride, int G, int H, int W, const float* wl,
                                            const int* qt, float* out, int ostride, int cout, const float* bias,
-                                           LStat& st, bool stats, const float* zq) {
+                                           LStat& st, bool stats, const float* zq, const KSplit& ks) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
+            conv3q_lds<1>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq, ks);
         else
-            conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
+            conv3q_lds<2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq, ks);
         return;
     }
     if (nr == 3)
-        conv3q_lds<MAXNR >= 3 ? 3 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
+        conv3q_lds<MAXNR >= 3 ? 3 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq, ks);
     else
-        conv3q_lds<MAXNR >= 4 ? 4 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq);
+        conv3q_lds<MAXNR >= 4 ? 4 : 2>(in, istride, G, H, W, wl, qt, out, ostride, cout, bias, st, stats, zq, ks);
 }
 
 // k -> (dr, dc, c) table of a PK_KN conv over cin channels from channel ic0; -1 beyond K
@@ -568,13 +669,36 @@ __device__ __forceinline__ void build_ktab(int* ktab, int cin, int ic0, int d, i
 template <int NR>
 __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* __restrict__ bias, LStat& st, bool stats) {
+                                           const float* __restrict__ bias, LStat& st, bool stats, const KSplit& ks) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
     const int nsub = (HW + 15) >> 4;
     Epi<NR> ep;
     ep.init(bias, cout);
+    if (ks_on(ks, nsub, Kpad >> 2)) {
+        int s, k, KS, glo, ghi;
+        ks_slice(nsub, Kpad >> 2, s, k, KS, glo, ghi);
+        f4 acc[NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+        const int pa = s * 16 + i16;
+        const bool pva = pa < HW;
+        const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
+        for (int k0 = 4 * glo; k0 < 4 * ghi; k0 += 4) {
+            const int t = ktab[k0 + kq];
+            const int c = t & 0xffff;
+            const int dr = ((t >> 24) & 0xff) - 32, dc = ((t >> 16) & 0xff) - 32;
+            const int ya = ra + dr, xa = ca + dc;
+            const bool oka = t >= 0 && (unsigned)ya < (unsigned)H && (unsigned)xa < (unsigned)W;
+            const float a0 = oka ? in[(ya * W + xa) * istride + c] : 0.f;
+            const float* wrow = wl + (k0 + kq) * NS + i16;
+#pragma unroll
+            for (int n = 0; n < NR; n++) acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wrow[n * 16], acc[n], 0, 0, 0);
+        }
+        ks_finish<NR>(acc, s, k, KS, nsub, ks, ep, HW, out, ostride, false, stats, st);
+        return;
+    }
     for (int s0 = wave; s0 < nsub; s0 += (PAIR ? 2 : 1) * NW) {
         const int s1 = s0 + NW;
         const bool v1 = PAIR && s1 < nsub;
@@ -615,19 +739,19 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
 template <int MAXNR>
 __device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* bias, LStat& st, bool stats) {
+                                           const float* bias, LStat& st, bool stats, const KSplit& ks) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
+            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
         else
-            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
+            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
         return;
     }
     if (nr == 3)
-        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
+        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
     else
-        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats);
+        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
 }
 
 // entries of the tap (PK_KN) / quad (PK_Q4) table of a 3x3 conv, rounded to 4
@@ -643,11 +767,11 @@ __device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin
 template <int MAXNR>
 __device__ __forceinline__ void conv3_run(const LdsConv& cv, const float* in, int istride, int H, int W,
                                           const float* wl, const int* tab, float* out, int ostride, int cout,
-                                          const float* bias, LStat& st, bool stats, const float* zq) {
+                                          const float* bias, LStat& st, bool stats, const float* zq, const KSplit& ks) {
     if (cv.fmt == PK_Q4)
-        conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, st, stats, zq);
+        conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, st, stats, zq, ks);
     else
-        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, st, stats);
+        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, st, stats, ks);
 }
 
 // position in u of element (pixel p, channel c) of the compressed u1c (mask compress, :720-759)
@@ -681,7 +805,7 @@ __device__ long long g_cycles[256];
         }                                                                                     \
     } while (0)
 
-template <bool STAMPS, int MAXNR>
+template <bool STAMPS, int MAXNR, bool KSP>
 __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int img = blockIdx.x, net = blockIdx.y;
@@ -708,6 +832,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const int* off = otab;
     const bool ln = a.ln != 0;
     LStat st;   // LN statistics of the tensor being produced
+    // K-split only in the instantiation for images of at most 4 subtiles (its extra registers stay
+    // out of the larger layers' kernel)
+    float* ksb = KSP ? reinterpret_cast<float*>(smem + a.off_ks) : nullptr;
+    const KSplit ks0{ksb, 0};
     float mu = 0.f, rstd = 1.f;
     const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
     const int per_rb = 10 + 2 * a.nbr;
@@ -753,7 +881,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
         if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
-        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, st, ln, ZQ);
+        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, st, ln, ZQ, ks0);
         if (ln) lst_flush(st, slots);
         lds_barrier();
         STAMP(sti++);
@@ -777,7 +905,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         // the branches read only their windows of it
         if (yq) lnp_load(lp, P + o[4], P + o[5], HW * nk / 4);
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, st, ln);
+        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, st, ln, ks0);
         if (ln) lst_flush(st, slots);
         STAMP(sti++);
         lds_barrier();
@@ -820,7 +948,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                 const LdsConv& cv = a.gcv[bi];
                 const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
                 conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
-                          WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ);
+                          WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ, KSplit{ksb, bi & 1});
                 kto += ktab_len(cv);
             }
         }
@@ -848,7 +976,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
                      HW * nk / 4);
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, st, ln);
+        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, st, ln, ks0);
         if (ln) lst_flush(st, slots);
         STAMP(sti++);
         lds_barrier();
@@ -880,7 +1008,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             STAMP(sti++);
             for (int nb = 0; nb < co_nr; nb += CB)
                 conv1_any<MAXNR>(Y, SY, nk, HW, WL, C + 16 * nb, CS, min(16 * CB, ncol - 16 * nb), nullptr, false, st,
-                                 false, 16 * co_nr, nb);
+                                 false, KSplit{ksb, (nb / CB) & 1}, 16 * co_nr, nb);
             STAMP(sti++);
             lds_barrier();
             STAMP(sti++);
@@ -926,7 +1054,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             conv3_table(a.co, KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, st, false, ZQ);
+            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, st, false, ZQ, ks0);
             lds_barrier();
             const int n = HW * a.dc2;
             for (int e = threadIdx.x; e < n; e += NT) {
@@ -954,18 +1082,25 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         return e && std::atoi(e) != 0;
     }();
     const bool narrow = a.maxnr <= 2 && !wide;
+    const bool ks = a.off_ks != 0;
+    const dim3 grid(B, 2), block(NT);
     if (stamps) {
         NetLdsArgs b = a;
         b.stamp_off = (lds + 15) & ~15;
-        if (narrow)
-            hipLaunchKernelGGL((k_net_lds<true, 2>), dim3(B, 2), dim3(NT), b.stamp_off + 1024, st, b);
+        const int l2 = b.stamp_off + 1024;
+        if (narrow && ks)
+            hipLaunchKernelGGL((k_net_lds<true, 2, true>), grid, block, l2, st, b);
+        else if (narrow)
+            hipLaunchKernelGGL((k_net_lds<true, 2, false>), grid, block, l2, st, b);
         else
-            hipLaunchKernelGGL((k_net_lds<true, 5>), dim3(B, 2), dim3(NT), b.stamp_off + 1024, st, b);
+            hipLaunchKernelGGL((k_net_lds<true, 5, false>), grid, block, l2, st, b);
+    } else if (narrow && ks) {
+        hipLaunchKernelGGL((k_net_lds<false, 2, true>), grid, block, lds, st, a);
+    } else if (narrow) {
+        hipLaunchKernelGGL((k_net_lds<false, 2, false>), grid, block, lds, st, a);
+    } else {
+        hipLaunchKernelGGL((k_net_lds<false, 5, false>), grid, block, lds, st, a);
     }
-    else if (narrow)
-        hipLaunchKernelGGL((k_net_lds<false, 2>), dim3(B, 2), dim3(NT), lds, st, a);
-    else
-        hipLaunchKernelGGL((k_net_lds<false, 5>), dim3(B, 2), dim3(NT), lds, st, a);
 }
 
 int read_cycles(long long* host, int n) {

@@ -134,6 +134,13 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     off = align16(off + wmax * 4);
     g.off_k = (int)off;
     off = align16(off + (int64_t)kmax * 4);
+    // images of at most 4 16-pixel subtiles leave k_net_lds waves idle: their convs split K over the
+    // waves and sum the slices through two alternating LDS buffers of (waves - 1) x 5 blocks x 1 KiB
+    g.off_ks = 0;
+    if ((HW + 15) / 16 <= 4) {
+        g.off_ks = (int)off;
+        off = align16(off + 2LL * 7 * 5 * 1024);
+    }
     g.bytes = (int)std::min<int64_t>(off, 1 << 30);
     return off <= 160 * 1024;
 }

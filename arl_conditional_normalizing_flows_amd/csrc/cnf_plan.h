@@ -58,6 +58,7 @@ struct NetParams {
 struct NetLdsGeom {
     int sy = 0, s1 = 0, s2 = 0, su = 0, s2r = 0;
     int off_y = 0, off_t1 = 0, off_t2 = 0, off_w = 0, off_k = 0, bytes = 0;
+    int off_ks = 0;   // images of at most 4 subtiles: K-split partial sums (0 = none)
 };
 
 struct Coupling {

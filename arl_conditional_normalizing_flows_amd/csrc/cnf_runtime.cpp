@@ -141,7 +141,7 @@ WsLayout Plan::layout(int B) const {
         L.t2[n] = take(Bz * n_t2 * 4);
         L.so[n] = take(Bz * n_so * 4);
         for (int k = 0; k < 3; k++) {   // LN slabs y, t1, t2: per-wave partials
-            L.st_part[n][k] = take(Bz * parts * 3 * 8);
+            L.st_part[n][k] = take(Bz * parts * LNP * 4);
         }
     }
 
@@ -180,10 +180,10 @@ struct Exec {
     }
 };
 
-// LN statistics slab of one tensor: per-wave partials [B][st_parts][3] of which the last producer
+// LN statistics slab of one tensor: per-wave partials [B][st_parts][LNP] of which the last producer
 // wrote the first nparts (see ConvProb)
 struct Slab {
-    double* part = nullptr;
+    float* part = nullptr;
     int nparts = 0;
 };
 
@@ -492,6 +492,7 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     a.off_t2 = g.off_t2;
     a.off_w = g.off_w;
     a.off_k = g.off_k;
+    a.off_ks = g.off_ks;
     auto nr = [](int cout) { return (cout + 15) / 16; };
     // the tap-decomposed conv_out runs in chunks of at most two 16-column blocks
     a.maxnr = std::max(nr(c.nk), c.co_fmt == PK_TAP ? std::min(2, nr(9 * c.dc2)) : nr(c.dc2));
@@ -560,7 +561,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     Slab sl[2][3];   // [net][y, t1, t2]
     for (int n = 0; n < 2; n++)
         for (int k = 0; k < 3; k++) {
-            sl[n][k].part = E.at<double>(L.st_part[n][k]);
+            sl[n][k].part = E.at<float>(L.st_part[n][k]);
         }
     // a producing launch reports the partial slots it wrote per image (set_parts); in_slab hands
     // that count on to the consumer

@@ -20,8 +20,11 @@ namespace cnf {
 constexpr int PW_LDS_STAT = 256;    // byte offset of the per-image (mean, rstd) table
 constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 
+#ifndef CNF_PW_MINW
+#define CNF_PW_MINW 2
+#endif
 template <int NR, int GM, bool LN, bool RES>
-__global__ __launch_bounds__(64 * PW_NW, 2) void k_pw(ConvArgs a) {
+__global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
     const ConvProb P = a.p[blockIdx.y];
@@ -126,7 +129,9 @@ __global__ __launch_bounds__(64 * PW_NW, 2) void k_pw(ConvArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) res[n][r] = rv[n][r];
         }
+#ifndef CNF_ABL_PW_NOLOAD
         if (ii + 1 < nimg) load_img(ii + 1);   // in flight during this image's MFMAs and stores
+#endif
         f4 acc[NR];
 #pragma unroll
         for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
@@ -152,12 +157,14 @@ __global__ __launch_bounds__(64 * PW_NW, 2) void k_pw(ConvArgs a) {
             for (int r = 0; r < 4; r++) {
                 float v = acc[n][r] + bias[n];
                 if (RES) v += res[n][r];
+#ifndef CNF_ABL_PW_NOSTORE
                 buf_store1(rout, oo[n][r] == BUF_OOB ? BUF_OOB : ob + oo[n][r], v);
+#endif
                 vals[n * 4 + r] = lrelu(v);
             }
         if (P.out_part != nullptr)
             ln_partial(vals, valid,
-                       P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tile * NW + wave) * 3);
+                       P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tile * NW + wave) * LNP);
     }
 }
 
@@ -457,7 +464,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
             }
             GSTAMP(gs++);
         }
-        if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * 3);
+        if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * LNP);
         if (ii + 1 < nimg) store_img(ii + 1);   // the other buffer: nobody reads it this iteration
         __syncthreads();
         GSTAMP(gs++);
