@@ -1,6 +1,8 @@
 // cnf_kernels.h — kernel argument blocks and launch helpers (host <-> device contract).
 #pragma once
 
+#include <cstddef>
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -93,6 +95,22 @@ struct NetLdsArgs {
     int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
     int stamp_off;                               // diagnostic stamp builds: LDS byte offset of the stamp array
 };
+// The launch-independent "shape" of a k_net_lds launch as int words: [offs_per_net, zero_bias) and
+// [off_y, stamp_off) of NetLdsArgs (the mask word inside is not part of it). Shape-specialised
+// instantiations take these words as compile-time constants (cnf_netlds_shapes.inc).
+constexpr int NETSHAPE_W1 = (int)((offsetof(NetLdsArgs, zero_bias) - offsetof(NetLdsArgs, offs_per_net)) / 4);
+constexpr int NETSHAPE_W2 = (int)((offsetof(NetLdsArgs, stamp_off) - offsetof(NetLdsArgs, off_y)) / 4);
+constexpr int NETSHAPE_WORDS = NETSHAPE_W1 + NETSHAPE_W2;
+static_assert(offsetof(NetLdsArgs, gcv) + sizeof(LdsConv) * NETLDS_MAXBR - offsetof(NetLdsArgs, offs_per_net) == 4 * 123,
+              "gen_netlds_shapes.py assumes 123 int members in [offs_per_net, zero_bias)");
+constexpr int NETSHAPE_MASK = (int)((offsetof(NetLdsArgs, mask) - offsetof(NetLdsArgs, offs_per_net)) / 4);
+inline void netshape_words(const NetLdsArgs& a, int* w) {
+    const int* p1 = &a.offs_per_net;
+    const int* p2 = &a.off_y;
+    for (int i = 0; i < NETSHAPE_W1; i++) w[i] = p1[i];
+    for (int i = 0; i < NETSHAPE_W2; i++) w[NETSHAPE_W1 + i] = p2[i];
+    w[NETSHAPE_MASK] = 0;
+}
 // k_gc (cnf_stream.hip): every grouped dilated branch of one residual block for a tile of TH
 // image rows of one net, `ipw` images per workgroup. Branch input windows are staged into LDS
 // bands with their own dilation halo (LN2 + LeakyReLU applied on the way in, zero padding), so
@@ -136,6 +154,7 @@ struct ToyArgs {
 void launch_toy(const ToyArgs& a, int lds_floats, hipStream_t st);
 void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st);
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st);
+int netlds_num_shapes();   // shape-specialised k_net_lds instantiations compiled in
 int read_stamps(long long* host, int n);
 int read_cycles(long long* host, int n);
 

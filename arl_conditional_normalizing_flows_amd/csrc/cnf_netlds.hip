@@ -22,6 +22,8 @@
 
 namespace cnf {
 
+#include "cnf_netlds_shapes.inc"   // shape-specialised instantiations (gen_netlds_shapes.py)
+
 namespace {
 
 #ifndef CNF_NETLDS_NW
@@ -805,42 +807,47 @@ __device__ long long g_cycles[256];
         }                                                                                     \
     } while (0)
 
-template <bool STAMPS, int MAXNR, bool KSP>
+// Shape-specialised instantiations (SID >= 0) read every shape field from the constexpr table entry
+// SID (the host picks SID only when the launch's shape words match it), so strides, trip counts,
+// formats and offsets are compile-time constants; SID < 0 reads them from the kernel arguments.
+#define SA(f) (SID >= 0 ? kNetShapes[SID >= 0 ? SID : 0].f : a.f)
+
+template <bool STAMPS, int MAXNR, bool KSP, int SID>
 __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int img = blockIdx.x, net = blockIdx.y;
-    const int H = a.hc, W = a.wc, HW = H * W;
-    const int nk = a.nk, gc = a.gc;
-    const int SY = a.sy, S1 = a.s1, S2 = a.s2, SU = a.su;   // S2 covers max(gc, nk, dc2) channels
+    const int H = SA(hc), W = SA(wc), HW = H * W;
+    const int nk = SA(nk), gc = SA(gc);
+    const int SY = SA(sy), S1 = SA(s1), S2 = SA(s2), SU = SA(su);   // S2 covers max(gc, nk, dc2) channels
     float* slots = reinterpret_cast<float*>(smem);           // NW x (K, S1, S2, n)
-    float* Y = reinterpret_cast<float*>(smem + a.off_y);
-    float* T1 = reinterpret_cast<float*>(smem + a.off_t1);
-    float* T2 = reinterpret_cast<float*>(smem + a.off_t2);
-    float* WL = reinterpret_cast<float*>(smem + a.off_w);
-    int* KT = reinterpret_cast<int*>(smem + a.off_k);
+    float* Y = reinterpret_cast<float*>(smem + SA(off_y));
+    float* T1 = reinterpret_cast<float*>(smem + SA(off_t1));
+    float* T2 = reinterpret_cast<float*>(smem + SA(off_t2));
+    float* WL = reinterpret_cast<float*>(smem + SA(off_w));
+    int* KT = reinterpret_cast<int*>(smem + SA(off_k));
     const float* P = a.params;
     const float* X = a.aux;
     // this net's parameter-offset table (see NetLdsArgs) copied to LDS [192, ...): every later read
     // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
     static_assert(NW * 4 * 4 <= 192, "LN slots overlap the offset table");
     int* otab = reinterpret_cast<int*>(smem + 192);
-    for (int i = threadIdx.x; i < a.offs_per_net; i += NT) otab[i] = a.offs[net * a.offs_per_net + i];
+    for (int i = threadIdx.x; i < SA(offs_per_net); i += NT) otab[i] = a.offs[net * SA(offs_per_net) + i];
     // 16 zero bytes right below Y: the source of every 3x3 tap quad outside the image
-    float* ZQ = reinterpret_cast<float*>(smem + a.off_y - 16);
+    float* ZQ = reinterpret_cast<float*>(smem + SA(off_y) - 16);
     if (threadIdx.x < 4) ZQ[threadIdx.x] = 0.f;
     lds_barrier();
     const int* off = otab;
-    const bool ln = a.ln != 0;
+    const bool ln = SA(ln) != 0;
     LStat st;   // LN statistics of the tensor being produced
     // K-split only in the instantiation for images of at most 4 subtiles (its extra registers stay
     // out of the larger layers' kernel)
-    float* ksb = KSP ? reinterpret_cast<float*>(smem + a.off_ks) : nullptr;
+    float* ksb = KSP ? reinterpret_cast<float*>(smem + SA(off_ks)) : nullptr;
     const KSplit ks0{ksb, 0};
     float mu = 0.f, rstd = 1.f;
     const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
-    const int per_rb = 10 + 2 * a.nbr;
+    const int per_rb = 10 + 2 * SA(nbr);
     auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
-    const int* oend = off + RB0 + a.R * per_rb;
+    const int* oend = off + RB0 + SA(R) * per_rb;
     WPre pf;
     LnPre lp;
     // full-width LNs (Y: nk channels, T2: gc channels) take the prefetched path when quad-shaped
@@ -856,37 +863,37 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     auto wb = [](const LdsConv& cv, int cout) { return cv.size + ((cout + 3) & ~3); };
     // floats of all branch images of a residual block (contiguous from offs[10])
     auto brw = [&](const int* o) {
-        const int l = a.nbr - 1;
-        return o[11 + 2 * l] + ((a.br_cout[l] + 3) & ~3) - o[10];
+        const int l = SA(nbr) - 1;
+        return o[11 + 2 * l] + ((SA(br_cout)[l] + 3) & ~3) - o[10];
     };
-    wpf_load(pf, X + off[0], wb(a.ci, nk));
+    wpf_load(pf, X + off[0], wb(SA(ci), nk));
     // gather u1c (mask compress) into T2 (stride SU)
     {
-        const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
-        const int n = HW * a.dc1;
+        const float* ub = a.u + (size_t)img * SA(H) * SA(W) * SA(D);
+        const int n = HW * SA(dc1);
         for (int e = threadIdx.x; e < n; e += NT) {
-            const int p = e / a.dc1, c = e - p * a.dc1;
-            T2[p * SU + c] = ub[mask_pos_(a.mask, p, c, W, a.W, a.D)];
+            const int p = e / SA(dc1), c = e - p * SA(dc1);
+            T2[p * SU + c] = ub[mask_pos_(a.mask, p, c, W, SA(W), SA(D))];
         }
     }
     // conv_in (3x3, dc1 -> nk) -> Y, LN stats of Y
     {
-        conv3_table(a.ci, KT, a.dc1, 0, 1);
+        conv3_table(SA(ci), KT, SA(dc1), 0, 1);
         wpf_store(pf, WL, X + off[0]);
         lst_reset(st);
         lds_barrier();
-        if (a.R > 0)
-            wpf_load(pf, X + rbo(0)[2], wb(a.ca, nk));
+        if (SA(R) > 0)
+            wpf_load(pf, X + rbo(0)[2], wb(SA(ca), nk));
         else
-            wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
-        if (yq) lnp_load(lp, P + (a.R > 0 ? rbo(0)[0] : oend[0]), P + (a.R > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
+            wpf_load(pf, X + oend[2], wb(SA(co), SA(dc2)));
+        if (yq) lnp_load(lp, P + (SA(R) > 0 ? rbo(0)[0] : oend[0]), P + (SA(R) > 0 ? rbo(0)[1] : oend[1]), HW * nk / 4);
         STAMP(sti++);
-        conv3_run<MAXNR>(a.ci, T2, SU, H, W, WL, KT, Y, SY, nk, WL + a.ci.size, st, ln, ZQ, ks0);
+        conv3_run<MAXNR>(SA(ci), T2, SU, H, W, WL, KT, Y, SY, nk, WL + SA(ci).size, st, ln, ZQ, ks0);
         if (ln) lst_flush(st, slots);
         lds_barrier();
         STAMP(sti++);
     }
-    for (int r = 0; r < a.R; r++) {
+    for (int r = 0; r < SA(R); r++) {
         const int* o = rbo(r);
         // LN1(LReLU(y)) -> T2, conv_a (1x1 nk->nk) -> T1 (+ LN2 stats)
         if (ln) lst_final(slots, mu, rstd);
@@ -905,7 +912,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         // the branches read only their windows of it
         if (yq) lnp_load(lp, P + o[4], P + o[5], HW * nk / 4);
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + a.ca.size, false, st, ln, ks0);
+        conv1_any<MAXNR>(T2, S2, nk, HW, WL, T1, S1, nk, WL + SA(ca).size, false, st, ln, ks0);
         if (ln) lst_flush(st, slots);
         STAMP(sti++);
         lds_barrier();
@@ -915,11 +922,11 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         if (yq)
             ln_full(T1, S1, T1, S1, HW, nk, mu, rstd, lp, P + o[4], P + o[5]);
-        else if (a.nwin == 1)
-            ln_apply(T1, S1, T1, S1, HW, a.win_off[0], a.win_len[0], nk, mu, rstd, ln ? P + o[4] : nullptr,
+        else if (SA(nwin) == 1)
+            ln_apply(T1, S1, T1, S1, HW, SA(win_off)[0], SA(win_len)[0], nk, mu, rstd, ln ? P + o[4] : nullptr,
                      ln ? P + o[5] : nullptr, ln);
         else
-            ln_windows(T1, S1, HW, nk, a.nwin, a.win_off, a.win_len, mu, rstd, ln ? P + o[4] : nullptr,
+            ln_windows(T1, S1, HW, nk, SA(nwin), SA(win_off), SA(win_len), mu, rstd, ln ? P + o[4] : nullptr,
                        ln ? P + o[5] : nullptr, ln);
         STAMP(sti++);
         if (tq) lnp_load(lp, P + o[6], P + o[7], HW * gc / 4);
@@ -929,9 +936,9 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         // read T1 and write disjoint T2 slices), each wave merging its LN3 partials across them
         if (r == 0) {   // the same for every residual block (conv_out builds its own after the loop)
             int kto = 0;
-            for (int bi = 0; bi < a.nbr; bi++) {
-                const LdsConv& cv = a.gcv[bi];
-                conv3_table(cv, KT + kto, a.br_cin[bi], a.br_cin_off[bi], a.br_dil[bi]);
+            for (int bi = 0; bi < SA(nbr); bi++) {
+                const LdsConv& cv = SA(gcv)[bi];
+                conv3_table(cv, KT + kto, SA(br_cin)[bi], SA(br_cin_off)[bi], SA(br_dil)[bi]);
                 kto += ktab_len(cv);
             }
         }
@@ -940,14 +947,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         lds_barrier();   // LN2 applied, slots read, branch images and tables complete
         lst_reset(st);
-        wpf_load(pf, X + o[8], wb(a.cb, nk));
+        wpf_load(pf, X + o[8], wb(SA(cb), nk));
         STAMP(sti++);
         {
             int kto = 0;
-            for (int bi = 0; bi < a.nbr; bi++) {
-                const LdsConv& cv = a.gcv[bi];
+            for (int bi = 0; bi < SA(nbr); bi++) {
+                const LdsConv& cv = SA(gcv)[bi];
                 const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
-                conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + a.br_out_off[bi], S2, a.br_cout[bi],
+                conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + SA(br_out_off)[bi], S2, SA(br_cout)[bi],
                           WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ, KSplit{ksb, bi & 1});
                 kto += ktab_len(cv);
             }
@@ -968,15 +975,15 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         lds_barrier();
         lst_reset(st);
-        if (r + 1 < a.R)
-            wpf_load(pf, X + rbo(r + 1)[2], wb(a.ca, nk));
+        if (r + 1 < SA(R))
+            wpf_load(pf, X + rbo(r + 1)[2], wb(SA(ca), nk));
         else
-            wpf_load(pf, X + oend[2], wb(a.co, a.dc2));
+            wpf_load(pf, X + oend[2], wb(SA(co), SA(dc2)));
         if (yq)
-            lnp_load(lp, P + (r + 1 < a.R ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < a.R ? rbo(r + 1)[1] : oend[1]),
+            lnp_load(lp, P + (r + 1 < SA(R) ? rbo(r + 1)[0] : oend[0]), P + (r + 1 < SA(R) ? rbo(r + 1)[1] : oend[1]),
                      HW * nk / 4);
         STAMP(sti++);
-        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + a.cb.size, true, st, ln, ks0);
+        conv1_any<MAXNR>(T2, S2, gc, HW, WL, Y, SY, nk, WL + SA(cb).size, true, st, ln, ks0);
         if (ln) lst_flush(st, slots);
         STAMP(sti++);
         lds_barrier();
@@ -991,14 +998,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         else
             ln_apply(Y, SY, Y, SY, HW, 0, nk, nk, mu, rstd, ln ? P + o[0] : nullptr, ln ? P + o[1] : nullptr, ln);
         STAMP(sti++);
-        float* dst = a.so[net] + (size_t)img * HW * a.dc2;
-        const float* bias = WL + a.co.size;
-        if (a.co.fmt == PK_TAP) {
+        float* dst = a.so[net] + (size_t)img * HW * SA(dc2);
+        const float* bias = WL + SA(co).size;
+        if (SA(co).fmt == PK_TAP) {
             // tap-decomposed: C[p][(tap, o)] = sum_c y[p][c] W[tap][c][o] (1x1 GEMM, scratch over T1..T2),
             // out[p][o] = b[o] + sum_tap C[p + off(tap)][(tap, o)]
-            const int ncol = 9 * a.dc2;
+            const int ncol = 9 * SA(dc2);
             const int co_nr = (ncol + 15) / 16;
-            const bool vq = (a.dc2 & 3) == 0;   // quad-shaped output: 16-byte tap-sum reads
+            const bool vq = (SA(dc2) & 3) == 0;   // quad-shaped output: 16-byte tap-sum reads
             const int CS = 16 * co_nr + (vq ? 4 : 1);
             float* C = T1;
             wpf_store(pf, WL, X + o[2]);
@@ -1014,7 +1021,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             STAMP(sti++);
             if (vq) {
                 // one output quad per item: 9 tap quads issued together (outside the image: ZQ)
-                const int nq = a.dc2 >> 2, n = HW * nq;
+                const int nq = SA(dc2) >> 2, n = HW * nq;
                 for (int e = threadIdx.x; e < n; e += NT) {
                     const int p = e / nq, oq = (e - p * nq) << 2;
                     const int pr = p / W, pc = p - pr * W;
@@ -1023,17 +1030,17 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                     for (int k = 0; k < 9; k++) {
                         const int sr = pr + k / 3 - 1, sc = pc + k % 3 - 1;
                         const bool ok = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
-                        t[k] = *reinterpret_cast<const f4*>(ok ? C + (sr * W + sc) * CS + k * a.dc2 + oq : ZQ);
+                        t[k] = *reinterpret_cast<const f4*>(ok ? C + (sr * W + sc) * CS + k * SA(dc2) + oq : ZQ);
                     }
                     f4 acc = *reinterpret_cast<const f4*>(bias + oq);
 #pragma unroll
                     for (int k = 0; k < 9; k++) acc += t[k];
-                    *reinterpret_cast<f4*>(dst + p * a.dc2 + oq) = acc;
+                    *reinterpret_cast<f4*>(dst + p * SA(dc2) + oq) = acc;
                 }
             } else {
-                const int n = HW * a.dc2;
+                const int n = HW * SA(dc2);
                 for (int e = threadIdx.x; e < n; e += NT) {
-                    const int p = e / a.dc2, oc = e - p * a.dc2;
+                    const int p = e / SA(dc2), oc = e - p * SA(dc2);
                     const int pr = p / W, pc = p - pr * W;
                     float acc = bias[oc];
 #pragma unroll
@@ -1044,21 +1051,21 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                         for (int kw = 0; kw < 3; kw++) {
                             const int sc = pc + kw - 1;
                             if (sc < 0 || sc >= W) continue;
-                            acc += C[(sr * W + sc) * CS + (kh * 3 + kw) * a.dc2 + oc];
+                            acc += C[(sr * W + sc) * CS + (kh * 3 + kw) * SA(dc2) + oc];
                         }
                     }
                     dst[e] = acc;
                 }
             }
         } else {
-            conv3_table(a.co, KT, nk, 0, 1);
+            conv3_table(SA(co), KT, nk, 0, 1);
             wpf_store(pf, WL, X + o[2]);
             lds_barrier();
-            conv3_run<MAXNR>(a.co, Y, SY, H, W, WL, KT, T2, S2, a.dc2, bias, st, false, ZQ, ks0);
+            conv3_run<MAXNR>(SA(co), Y, SY, H, W, WL, KT, T2, S2, SA(dc2), bias, st, false, ZQ, ks0);
             lds_barrier();
-            const int n = HW * a.dc2;
+            const int n = HW * SA(dc2);
             for (int e = threadIdx.x; e < n; e += NT) {
-                const int p = e / a.dc2, c = e - p * a.dc2;
+                const int p = e / SA(dc2), c = e - p * SA(dc2);
                 dst[e] = T2[p * S2 + c];
             }
         }
@@ -1072,6 +1079,26 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     }
 }
 
+// instantiation flags of table entry S: narrow (<= 2 output blocks) and K-split
+template <int S>
+constexpr bool shape_narrow() { return kNetShapeWords[S][NETSHAPE_W1 + NETSHAPE_W2 - 1] <= 2; }
+template <int S>
+constexpr bool shape_ks() { return kNetShapeWords[S][NETSHAPE_W1 + NETSHAPE_W2 - 2] != 0; }
+
+template <int S>
+bool launch_shape(int sid, const NetLdsArgs& a, dim3 grid, dim3 block, int lds, hipStream_t st) {
+    if constexpr (S < CNF_NETLDS_NSHAPES) {
+        if (sid == S) {
+            hipLaunchKernelGGL((k_net_lds<false, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block, lds, st, a);
+            return true;
+        }
+        return launch_shape<S + 1>(sid, a, grid, block, lds, st);
+    }
+    return false;
+}
+
+int netlds_num_shapes() { return CNF_NETLDS_NSHAPES; }
+
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
     static const bool stamps = [] {
         const char* e = std::getenv("CNF_STAMPS");
@@ -1079,6 +1106,10 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
     }();
     static const bool wide = [] {   // A/B knob: always the generic instantiation
         const char* e = std::getenv("CNF_NETLDS_WIDE");
+        return e && std::atoi(e) != 0;
+    }();
+    static const bool generic = [] {   // A/B knob: never the shape-specialised instantiations
+        const char* e = std::getenv("CNF_NETLDS_GENERIC");
         return e && std::atoi(e) != 0;
     }();
     const bool narrow = a.maxnr <= 2 && !wide;
@@ -1089,17 +1120,28 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         b.stamp_off = (lds + 15) & ~15;
         const int l2 = b.stamp_off + 1024;
         if (narrow && ks)
-            hipLaunchKernelGGL((k_net_lds<true, 2, true>), grid, block, l2, st, b);
+            hipLaunchKernelGGL((k_net_lds<true, 2, true, -1>), grid, block, l2, st, b);
         else if (narrow)
-            hipLaunchKernelGGL((k_net_lds<true, 2, false>), grid, block, l2, st, b);
+            hipLaunchKernelGGL((k_net_lds<true, 2, false, -1>), grid, block, l2, st, b);
         else
-            hipLaunchKernelGGL((k_net_lds<true, 5, false>), grid, block, l2, st, b);
-    } else if (narrow && ks) {
-        hipLaunchKernelGGL((k_net_lds<false, 2, true>), grid, block, lds, st, a);
+            hipLaunchKernelGGL((k_net_lds<true, 5, false, -1>), grid, block, l2, st, b);
+        return;
+    }
+    if (!generic && !wide) {
+        int w[NETSHAPE_WORDS];
+        netshape_words(a, w);
+        for (int sid = 0; sid < CNF_NETLDS_NSHAPES; sid++) {
+            bool eq = true;
+            for (int i = 0; i < NETSHAPE_WORDS && eq; i++) eq = w[i] == kNetShapeWords[sid][i];
+            if (eq && launch_shape<0>(sid, a, grid, block, lds, st)) return;
+        }
+    }
+    if (narrow && ks) {
+        hipLaunchKernelGGL((k_net_lds<false, 2, true, -1>), grid, block, lds, st, a);
     } else if (narrow) {
-        hipLaunchKernelGGL((k_net_lds<false, 2, false>), grid, block, lds, st, a);
+        hipLaunchKernelGGL((k_net_lds<false, 2, false, -1>), grid, block, lds, st, a);
     } else {
-        hipLaunchKernelGGL((k_net_lds<false, 5, false>), grid, block, lds, st, a);
+        hipLaunchKernelGGL((k_net_lds<false, 5, false, -1>), grid, block, lds, st, a);
     }
 }
 

@@ -497,6 +497,17 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     // the tap-decomposed conv_out runs in chunks of at most two 16-column blocks
     a.maxnr = std::max(nr(c.nk), c.co_fmt == PK_TAP ? std::min(2, nr(9 * c.dc2)) : nr(c.dc2));
     for (const Branch& b : c.br) a.maxnr = std::max(a.maxnr, nr(b.cout));
+    if (const char* e = std::getenv("CNF_NETLDS_DUMP")) {   // diagnostics: every shape field, as C
+        if (std::atoi(e)) {
+            const int* w = reinterpret_cast<const int*>(&a.offs_per_net);
+            const int n = (int)((reinterpret_cast<const char*>(&a.zero_bias) - reinterpret_cast<const char*>(w)) / 4);
+            std::fprintf(stderr, "NETSHAPE hc=%d wc=%d mask=%d:", c.hc, c.wc, c.mask);
+            for (int i = 0; i < n; i++) std::fprintf(stderr, " %d", w[i]);
+            const int* w2 = reinterpret_cast<const int*>(&a.off_y);
+            for (int i = 0; i < 7; i++) std::fprintf(stderr, " %d", w2[i]);
+            std::fprintf(stderr, "\n");
+        }
+    }
     if (const char* e = std::getenv("CNF_NETLDS_VERBOSE"))
         if (std::atoi(e)) std::fprintf(stderr, "netlds layer hc=%d wc=%d nk=%d dc2=%d co_fmt=%d maxnr=%d\n", c.hc, c.wc,
                                        c.nk, c.dc2, c.co_fmt, a.maxnr);
@@ -1228,6 +1239,21 @@ int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream) 
     return CNF_OK;
     CNF_CATCH
 }
+
+// shape words of coupling `coupling`'s k_net_lds launch (0 if the layer is streamed); host only, used
+// by csrc/gen_netlds_shapes.py to generate the shape-specialised instantiations' table
+int cnf_debug_netlds_shape(const cnf_plan* plan, int coupling, int* words, int cap) {
+    if (!plan || !words || cap < NETSHAPE_WORDS) return -1;
+    const Plan& p = *plan->p;
+    if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
+    const Coupling& c = p.couplings[coupling];
+    if (!c.use_lds) return 0;
+    NetLdsArgs a;
+    if (netlds_setup(p, c, a) == 0) return 0;
+    netshape_words(a, words);
+    return NETSHAPE_WORDS;
+}
+int cnf_debug_netlds_nshapes() { return netlds_num_shapes(); }
 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }

@@ -132,3 +132,15 @@ def test_fused_net_plan(lib):
         assert all(x[2] == 0 for x in fused())
     finally:
         os.environ.pop('CNF_NETLDS')
+
+
+def test_netlds_shape_table_is_current(lib):
+    """The shape-specialised k_net_lds instantiations are compiled from cnf_netlds_shapes.inc; the
+    table must equal the shapes the current plan produces for the benchmark configuration (a stale
+    table is not wrong, the launcher falls back to the generic kernel, but it loses the speed)."""
+    import subprocess
+    import sys
+    root = Path(__file__).resolve().parent.parent
+    gen = root / 'arl_conditional_normalizing_flows_amd' / 'csrc' / 'gen_netlds_shapes.py'
+    r = subprocess.run([sys.executable, str(gen), '--check'], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
