@@ -123,6 +123,12 @@ struct GcBranch {
     int w_off, q_off, b_off;                      // LDS byte offsets: packed weights, quad offsets, bias
     uint32_t cpq_mag, bw_mag;                     // x / (cinp/4) == umulhi(x, cpq_mag) (cinp > 4), x / BW likewise
 };
+struct GcShape {
+    GcBranch br[GC_MAXBR];
+    int nbr, H, W, in_cs, out_cs, TH, tiles_per_img;
+    int band_bytes;              // offset of the second band buffer (double-buffered staging)
+};
+constexpr int GCSHAPE_WORDS = (int)(sizeof(GcShape) / 4);
 struct GcArgs {
     const float* in[2];          // t1 per net [B][HW][in_cs]
     float* out[2];               // t2 per net [B][HW][out_cs]
@@ -132,12 +138,12 @@ struct GcArgs {
     const float* beta[2];
     const float* w[2][GC_MAXBR];
     const float* b[2][GC_MAXBR];
-    GcBranch br[GC_MAXBR];
-    int nbr, H, W, in_cs, out_cs, B, TH, tiles_per_img, ipw, in_nparts, part_stride;
-    int band_bytes;              // offset of the second band buffer (double-buffered staging)
+    GcShape s;                   // launch-independent part (compile-time in the shape-specialised kernels)
+    int B, ipw, in_nparts, part_stride;
 };
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st);
 int read_gc_stamps(long long* host, int n);
+int gc_num_shapes();   // shape-specialised k_gc instantiations compiled in
 // k_toy (cnf_toy.hip): TOYcINN dense flow, one thread per 3-dimensional sample
 constexpr int TOY_MAXL = 128;
 struct ToyArgs {

@@ -625,25 +625,25 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                     ga.b[n][bi] = X + rb.gc[bi].b;
                 }
             }
-            for (int bi = 0; bi < nbr; bi++) ga.br[bi] = c.gcb[bi];
-            ga.nbr = nbr;
-            ga.H = c.hc;
-            ga.W = c.wc;
-            ga.in_cs = c.nk;
-            ga.out_cs = c.gc;
+            for (int bi = 0; bi < nbr; bi++) ga.s.br[bi] = c.gcb[bi];
+            ga.s.nbr = nbr;
+            ga.s.H = c.hc;
+            ga.s.W = c.wc;
+            ga.s.in_cs = c.nk;
+            ga.s.out_cs = c.gc;
             ga.B = B;
-            ga.TH = c.gc_TH;
-            ga.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
+            ga.s.TH = c.gc_TH;
+            ga.s.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
             ga.in_nparts = sl[0][1].nparts;
             ga.part_stride = L.st_parts;
             // images per workgroup: one workgroup per CU, looping over its images with the next
             // image's band staged behind the current one's MFMAs
-            const int64_t units = (int64_t)ga.tiles_per_img * 2 * B;
+            const int64_t units = (int64_t)ga.s.tiles_per_img * 2 * B;
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
-            ga.band_bytes = c.gc_band_bytes;
+            ga.s.band_bytes = c.gc_band_bytes;
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
-            if (8 * ga.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
-            const int grid_x = ga.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
+            if (8 * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
+            const int grid_x = ga.s.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
             const int ilds = c.gc_lds;
             double fl = 0, by = 0;
             for (const Branch& b : c.br) fl += 2.0 * B * c.hc * c.wc * 9.0 * b.cin * b.cout * 2;
@@ -651,7 +651,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (const Branch& b : c.br) win += b.cin;
             by = 4.0 * B * c.hc * c.wc * (win + c.gc) * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
-            set_parts(2, 8 * ga.tiles_per_img);   // 8 waves per k_gc workgroup
+            set_parts(2, 8 * ga.s.tiles_per_img);   // 8 waves per k_gc workgroup
         } else {
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
@@ -1254,6 +1254,28 @@ int cnf_debug_netlds_shape(const cnf_plan* plan, int coupling, int* words, int c
     return NETSHAPE_WORDS;
 }
 int cnf_debug_netlds_nshapes() { return netlds_num_shapes(); }
+
+// shape words of coupling `coupling`'s k_gc launches (0 if it has none)
+int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) {
+    if (!plan || !words || cap < GCSHAPE_WORDS) return -1;
+    const Plan& p = *plan->p;
+    if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
+    const Coupling& c = p.couplings[coupling];
+    if (c.use_lds || !c.gc_fused) return 0;
+    GcShape s;
+    std::memset(&s, 0, sizeof(s));
+    for (size_t bi = 0; bi < c.br.size(); bi++) s.br[bi] = c.gcb[bi];
+    s.nbr = (int)c.br.size();
+    s.H = c.hc;
+    s.W = c.wc;
+    s.in_cs = c.nk;
+    s.out_cs = c.gc;
+    s.TH = c.gc_TH;
+    s.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
+    s.band_bytes = c.gc_band_bytes;
+    std::memcpy(words, &s, sizeof(s));
+    return GCSHAPE_WORDS;
+}
 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }

@@ -11,6 +11,8 @@
 // image's activations (and residual) are loaded into registers before the current image's MFMAs,
 // so HBM traffic and compute overlap inside the wave. The tile's LN gamma/beta are loaded once and
 // serve every image; weights and the per-image LN (mean, rstd) live in LDS.
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 #include "cnf_device.h"
@@ -189,6 +191,8 @@ void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x,
 
 namespace cnf {
 
+#include "cnf_gc_shapes.inc"   // shape-specialised k_gc instantiations (gen_netlds_shapes.py)
+
 // ---------------------------------------------------------------------------------------------
 // k_gc: the grouped dilated stage of a residual block (conv_cINN_base_functions.py:364-413,
 // 583-601) for the streamed layers — LN2(LeakyReLU(t1)) on the branch windows -> every branch's
@@ -197,7 +201,10 @@ namespace cnf {
 constexpr int GC_NW = 8;            // waves per k_gc workgroup
 constexpr int GC_NT = 64 * GC_NW;   // threads
 
-template <int NR>
+// shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
+#define GS(f) (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].f : a.s.f)
+
+template <int NR, int SID>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, const unsigned char* smem,
                                           const float* bias, float* __restrict__ outp, int npx,
                                           int px0, LnAcc& st, bool& first, bool stats, int boff) {
@@ -218,7 +225,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
 #pragma unroll
         for (int r = 0; r < 4; r++) bz[n][r] = r < nq[n] ? bias[c0 + r] : 0.f;
     }
-    const bool vq = ((a.out_cs | br.out_off) & 3) == 0;
+    const bool vq = ((GS(out_cs) | br.out_off) & 3) == 0;
     const int nsub = (npx + 15) >> 4;
     // two subtiles per wave and pass (s0, s0 + GC_NW) share every B read: two independent MFMA
     // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
@@ -233,7 +240,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
         for (int h = 0; h < 2; h++) {
             const int pt = (h ? s1 : s0) * 16 + i16;
             const int ptc = pt < npx ? pt : 0;
-            const int tr = ptc / a.W, tc = ptc - tr * a.W;
+            const int tr = ptc / GS(W), tc = ptc - tr * GS(W);
             base[h] = band + (tr * br.BW + tc) * br.S;
         }
         f4 acc0[NR], acc1[NR];
@@ -277,7 +284,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
             if (h == 1 && !v1) break;
             const int po = (h ? s1 : s0) * 16 + i16;
             const bool pv = po < npx;
-            float* orow = outp + (size_t)(px0 + po) * a.out_cs + br.out_off + 4 * kq;
+            float* orow = outp + (size_t)(px0 + po) * GS(out_cs) + br.out_off + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NR; n++) {
                 f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
@@ -316,16 +323,17 @@ __device__ long long g_gc_stamps[64];
 // double-buffered: the next image's t1 quads are loaded into registers before the current image's
 // MFMAs and written (LN2 + LeakyReLU applied) into the other buffer after them, so the staging
 // latency hides behind the compute; the tile's LN2 gamma/beta stay in registers for all images.
+template <int SID>
 __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
-    const int tile = blockIdx.x % a.tiles_per_img;
-    const int img0 = (blockIdx.x / a.tiles_per_img) * a.ipw;
+    const int tile = blockIdx.x % GS(tiles_per_img);
+    const int img0 = (blockIdx.x / GS(tiles_per_img)) * a.ipw;
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int H = a.H, W = a.W, HW = H * W;
-    const int r0 = tile * a.TH;
-    const int rows = min(a.TH, H - r0);
+    const int H = GS(H), W = GS(W), HW = H * W;
+    const int r0 = tile * GS(TH);
+    const int rows = min(GS(TH), H - r0);
     const int npx = rows * W, px0 = r0 * W;
     const bool ln = a.in_part[net] != nullptr;
     const bool stats = a.out_part[net] != nullptr;
@@ -343,8 +351,8 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         soff[u] = 0;
         loff[u] = -1;
         nv[u] = 0;
-        for (int bi = 0; bi < a.nbr; bi++) {
-            const GcBranch& br = a.br[bi];
+        for (int bi = 0; bi < GS(nbr); bi++) {
+            const GcBranch& br = GS(br)[bi];
             const int cpq = br.cinp >> 2, nq = br.BH * br.BW * cpq;
             if (e < nq) {
                 const int pix = cpq == 1 ? e : (int)__umulhi((unsigned)e, br.cpq_mag), cq = e - pix * cpq;
@@ -352,9 +360,9 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
                 const int y = r0 - br.dil + brr, x = bc - br.dil;
                 loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
                 if (y >= 0 && y < H && x >= 0 && x < W) {
-                    soff[u] = (y * W + x) * a.in_cs + br.cin_off + 4 * cq;
+                    soff[u] = (y * W + x) * GS(in_cs) + br.cin_off + 4 * cq;
                     const int v = min(4, br.cin - 4 * cq);
-                    const bool vec = v == 4 && ((br.cin_off | a.in_cs) & 3) == 0;
+                    const bool vec = v == 4 && ((br.cin_off | GS(in_cs)) & 3) == 0;
                     nv[u] = v | (vec ? 8 : 0);
                 }
                 break;
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         for (int j = 0; j < 4; j++) v[j] = buf_load1(r, j < n ? o + 4u * j : BUF_OOB);
         return v;
     };
-    const uint32_t img_bytes = (uint32_t)HW * a.in_cs * 4u;
+    const uint32_t img_bytes = (uint32_t)HW * GS(in_cs) * 4u;
     // tile LN2 gamma/beta (image-independent) and the first image's raw quads, all in flight together
     f4 gq[GC_GQ], bq[GC_GQ], xq[GC_GQ];
 #pragma unroll
@@ -384,7 +392,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         bq[u] = ln ? load_q(buf_rsrc(a.beta[net], img_bytes), u) : f4{0.f, 0.f, 0.f, 0.f};
     }
     auto load_img = [&](int ii) {
-        const auto r = buf_rsrc(a.in[net] + (size_t)(img0 + ii) * HW * a.in_cs, img_bytes);
+        const auto r = buf_rsrc(a.in[net] + (size_t)(img0 + ii) * HW * GS(in_cs), img_bytes);
 #pragma unroll
         for (int u = 0; u < GC_GQ; u++) xq[u] = load_q(r, u);
     };
@@ -392,7 +400,7 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
     auto store_img = [&](int ii) {
         const float rs = ln ? lstat[2 * ii + 1] : 1.f;
         const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
-        float* dst = lds_f + (ii & 1) * (a.band_bytes / 4);
+        float* dst = lds_f + (ii & 1) * (GS(band_bytes) / 4);
 #pragma unroll
         for (int u = 0; u < GC_GQ; u++) {
             if (loff[u] < 0) continue;
@@ -409,8 +417,8 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
     };
     load_img(0);
     // packed weights and quad-offset tables of every branch (once per workgroup)
-    for (int bi = 0; bi < a.nbr; bi++) {
-        const GcBranch& br = a.br[bi];
+    for (int bi = 0; bi < GS(nbr); bi++) {
+        const GcBranch& br = GS(br)[bi];
         const int nr = (br.cout + 15) >> 4;
         copy_to_lds<GC_NT>(a.w[net][bi], reinterpret_cast<float*>(smem + br.w_off), br.G * 16 * 16 * nr);
         for (int i = tid; i < br.cout; i += GC_NT) reinterpret_cast<float*>(smem + br.b_off)[i] = a.b[net][bi][i];
@@ -451,16 +459,16 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         LnAcc st;
         st.reset();
         bool first = true;
-        float* outp = a.out[net] + (size_t)img * HW * a.out_cs;
-        const int boff = (ii & 1) * a.band_bytes;
-        for (int bi = 0; bi < a.nbr; bi++) {
-            const GcBranch& br = a.br[bi];
+        float* outp = a.out[net] + (size_t)img * HW * GS(out_cs);
+        const int boff = (ii & 1) * GS(band_bytes);
+        for (int bi = 0; bi < GS(nbr); bi++) {
+            const GcBranch& br = GS(br)[bi];
             const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
             switch ((br.cout + 15) >> 4) {
-                case 1: gc_branch<1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                case 2: gc_branch<2>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                case 3: gc_branch<3>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                default: gc_branch<4>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                case 1: gc_branch<1, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                case 2: gc_branch<2, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                case 3: gc_branch<3, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                default: gc_branch<4, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
             }
             GSTAMP(gs++);
         }
@@ -478,8 +486,31 @@ int read_gc_stamps(long long* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gc_stamps), sizeof(long long) * (n > 64 ? 64 : n)) == hipSuccess ? 0 : -1;
 }
 
+template <int S>
+bool launch_gc_shape(int sid, const GcArgs& a, dim3 grid, int lds, hipStream_t st) {
+    if constexpr (S < CNF_GC_NSHAPES) {
+        if (sid == S) {
+            hipLaunchKernelGGL((k_gc<S>), grid, dim3(GC_NT), lds, st, a);
+            return true;
+        }
+        return launch_gc_shape<S + 1>(sid, a, grid, lds, st);
+    }
+    return false;
+}
+
+int gc_num_shapes() { return CNF_GC_NSHAPES; }
+
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
-    hipLaunchKernelGGL(k_gc, dim3(grid_x, 2), dim3(GC_NT), lds, st, a);
+    static const bool generic = [] {   // A/B knob: never the shape-specialised instantiations
+        const char* e = std::getenv("CNF_GC_GENERIC");
+        return e && std::atoi(e) != 0;
+    }();
+    const dim3 grid(grid_x, 2);
+    if (!generic)
+        for (int sid = 0; sid < CNF_GC_NSHAPES; sid++)
+            if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0 && launch_gc_shape<0>(sid, a, grid, lds, st))
+                return;
+    hipLaunchKernelGGL((k_gc<-1>), grid, dim3(GC_NT), lds, st, a);
 }
 
 }  // namespace cnf
