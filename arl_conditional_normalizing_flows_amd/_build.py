@@ -12,7 +12,7 @@ CSRC = PKG / 'csrc'
 LIB = PKG / 'lib' / 'libcnf_hip.so'
 SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
            'cnf_plan.cpp', 'cnf_train.cpp']
-HEADERS = ["cnf_kernels.h", "cnf_device.h", "cnf_plan.h", "cnf_netlds_shapes.inc", "cnf_gc_shapes.inc"]
+HEADERS = ["cnf_kernels.h", "cnf_device.h", "cnf_plan.h", "cnf_netlds_shapes.inc", "cnf_gc_shapes.inc", "cnf_pw_shapes.inc"]
 ARCH = os.environ.get('CNF_OFFLOAD_ARCH', 'gfx950')
 
 

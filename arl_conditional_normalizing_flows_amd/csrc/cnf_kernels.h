@@ -70,6 +70,10 @@ struct CoupArgs {
 
 // Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).
 constexpr int NETLDS_MAXBR = 8;
+#ifndef CNF_NETLDS_OTAB
+#define CNF_NETLDS_OTAB 192
+#endif
+constexpr int NETLDS_OTAB = CNF_NETLDS_OTAB;   // byte offset of the parameter-offset table (after the LN slots)
 // one conv of k_net_lds: packed format (PK_*), image floats, K extent (PK_KN: padded K; PK_Q4:
 // 16 * groups), B row stride (PK_KN)
 struct LdsConv {
@@ -166,7 +170,31 @@ int read_cycles(long long* host, int n);
 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+// k_pw launch shape: every launch-independent field a shape-specialised k_pw instantiation folds
+// in (cnf_stream.hip; table generated by gen_netlds_shapes.py from a dry run of the forward)
+struct PwShape {
+    int nr, gm, ln, res;                 // template selection
+    int H, W, tiles_per_img, nprob;
+    int in_cs, in_off, cin, out_cs, out_off, cout, lds_w_off, part_stride;
+    uint32_t st_mask_lo, st_mask_hi;
+};
+constexpr int PWSHAPE_WORDS = (int)(sizeof(PwShape) / 4);
+// the shape of a k_pw launch; false when its problems differ in a shape field
+inline bool pw_shape_of(int nr, int gm, bool ln, bool res, const ConvArgs& a, PwShape& s) {
+    const ConvProb& q = a.p[0];
+    s = PwShape{nr, gm, ln ? 1 : 0, res ? 1 : 0, a.H, a.W, a.tiles_per_img, a.nprob, q.in_cs, q.in_off, q.cin,
+                q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride, q.st_mask_lo, q.st_mask_hi};
+    for (int i = 1; i < a.nprob; i++) {
+        const ConvProb& r = a.p[i];
+        if (r.in_cs != q.in_cs || r.in_off != q.in_off || r.cin != q.cin || r.out_cs != q.out_cs ||
+            r.out_off != q.out_off || r.cout != q.cout || r.lds_w_off != q.lds_w_off || r.part_stride != q.part_stride ||
+            r.st_mask_lo != q.st_mask_lo || r.st_mask_hi != q.st_mask_hi)
+            return false;
+    }
+    return true;
+}
 void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+int pw_num_shapes();   // shape-specialised k_pw instantiations compiled in
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

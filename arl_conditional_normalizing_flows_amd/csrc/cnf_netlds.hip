@@ -30,6 +30,9 @@ namespace {
 #define CNF_NETLDS_NW 8
 #endif
 constexpr int NW = CNF_NETLDS_NW;   // waves per workgroup (one workgroup per CU: LDS-bound)
+#ifndef CNF_NETLDS_NOKS
+#define CNF_NETLDS_NOKS 0   // experiment knob: no K-split instantiations
+#endif
 #ifndef CNF_NETLDS_PAIR
 #define CNF_NETLDS_PAIR 1
 #endif
@@ -829,8 +832,8 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const float* X = a.aux;
     // this net's parameter-offset table (see NetLdsArgs) copied to LDS [192, ...): every later read
     // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
-    static_assert(NW * 4 * 4 <= 192, "LN slots overlap the offset table");
-    int* otab = reinterpret_cast<int*>(smem + 192);
+    static_assert(NW * 4 * 4 <= NETLDS_OTAB, "LN slots overlap the offset table");
+    int* otab = reinterpret_cast<int*>(smem + NETLDS_OTAB);
     for (int i = threadIdx.x; i < SA(offs_per_net); i += NT) otab[i] = a.offs[net * SA(offs_per_net) + i];
     // 16 zero bytes right below Y: the source of every 3x3 tap quad outside the image
     float* ZQ = reinterpret_cast<float*>(smem + SA(off_y) - 16);
@@ -1083,16 +1086,23 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
 template <int S>
 constexpr bool shape_narrow() { return kNetShapeWords[S][NETSHAPE_W1 + NETSHAPE_W2 - 1] <= 2; }
 template <int S>
-constexpr bool shape_ks() { return kNetShapeWords[S][NETSHAPE_W1 + NETSHAPE_W2 - 2] != 0; }
+constexpr bool shape_ks() { return !CNF_NETLDS_NOKS && kNetShapeWords[S][NETSHAPE_W1 + NETSHAPE_W2 - 2] != 0; }
 
 template <int S>
-bool launch_shape(int sid, const NetLdsArgs& a, dim3 grid, dim3 block, int lds, hipStream_t st) {
+bool launch_shape(int sid, const NetLdsArgs& a, dim3 grid, dim3 block, int lds, hipStream_t st, bool stamps) {
     if constexpr (S < CNF_NETLDS_NSHAPES) {
         if (sid == S) {
-            hipLaunchKernelGGL((k_net_lds<false, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block, lds, st, a);
+            if (stamps) {
+                NetLdsArgs b = a;
+                b.stamp_off = (lds + 15) & ~15;
+                hipLaunchKernelGGL((k_net_lds<true, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block,
+                                   b.stamp_off + 1024, st, b);
+            } else {
+                hipLaunchKernelGGL((k_net_lds<false, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block, lds, st, a);
+            }
             return true;
         }
-        return launch_shape<S + 1>(sid, a, grid, block, lds, st);
+        return launch_shape<S + 1>(sid, a, grid, block, lds, st, stamps);
     }
     return false;
 }
@@ -1115,6 +1125,15 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
     const bool narrow = a.maxnr <= 2 && !wide;
     const bool ks = a.off_ks != 0;
     const dim3 grid(B, 2), block(NT);
+    if (!generic && !wide) {
+        int w[NETSHAPE_WORDS];
+        netshape_words(a, w);
+        for (int sid = 0; sid < CNF_NETLDS_NSHAPES; sid++) {
+            bool eq = true;
+            for (int i = 0; i < NETSHAPE_WORDS && eq; i++) eq = w[i] == kNetShapeWords[sid][i];
+            if (eq && launch_shape<0>(sid, a, grid, block, lds, st, stamps)) return;
+        }
+    }
     if (stamps) {
         NetLdsArgs b = a;
         b.stamp_off = (lds + 15) & ~15;
@@ -1126,15 +1145,6 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         else
             hipLaunchKernelGGL((k_net_lds<true, 5, false, -1>), grid, block, l2, st, b);
         return;
-    }
-    if (!generic && !wide) {
-        int w[NETSHAPE_WORDS];
-        netshape_words(a, w);
-        for (int sid = 0; sid < CNF_NETLDS_NSHAPES; sid++) {
-            bool eq = true;
-            for (int i = 0; i < NETSHAPE_WORDS && eq; i++) eq = w[i] == kNetShapeWords[sid][i];
-            if (eq && launch_shape<0>(sid, a, grid, block, lds, st)) return;
-        }
     }
     if (narrow && ks) {
         hipLaunchKernelGGL((k_net_lds<false, 2, true, -1>), grid, block, lds, st, a);

@@ -123,7 +123,7 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
     // table (2 + R*(10 + 2*nbr) + 4 ints), read from LDS so no phase waits on a global load of it
     const int64_t opn = 2 + (int64_t)c.R * (10 + 2 * (int64_t)c.br.size()) + 4;
     // ... then 16 zero bytes right below Y (k_net_lds: the 3x3 taps outside the image read them)
-    int64_t off = std::max<int64_t>(512, align16(192 + 4 * opn) + 16);
+    int64_t off = std::max<int64_t>(512, align16(NETLDS_OTAB + 4 * opn) + 16);
     g.off_y = (int)off;
     off = align16(off + HW * g.sy * 4);
     g.off_t1 = (int)off;

@@ -168,6 +168,8 @@ struct Plan {
     int device = -1;
     // launch recording
     bool record = true;
+    bool dry = false;         // host-only dry run: record launches without issuing them (shape dumps)
+    std::vector<PwShape> pw_shapes;   // k_pw launch shapes seen by a dry run
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
     std::vector<Recorded> recorded;

@@ -168,6 +168,7 @@ struct Exec {
     }
 
     void record(const std::string& name, double flops, double bytes, std::function<void(void*)> fn) {
+        if (p.dry) return;
         fn(st);
         if (p.record) {
             Recorded r;
@@ -344,6 +345,14 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool lnf = probs[0].in_st.part != nullptr;
+        if (E.p.dry) {
+            PwShape sh;
+            if (pw_shape_of(nr, gm, lnf, resf, a, sh)) {
+                bool seen = false;
+                for (const PwShape& o : E.p.pw_shapes) seen = seen || std::memcmp(&o, &sh, sizeof(sh)) == 0;
+                if (!seen) E.p.pw_shapes.push_back(sh);
+            }
+        }
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
                            role_name(role) + ">";
         E.record(name, flops, bytes, [nr, gm, lnf, resf, a, grid_x, ilds](void* st) {
@@ -884,7 +893,7 @@ size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
 // workspace (cnf_flow_forward_train)
 static void flow_forward(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
                          float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs) {
-    ensure_tables(p);
+    if (!p.dry) ensure_tables(p);
     p.recorded.clear();
     Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
     TrainLayout TL;
@@ -944,7 +953,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
         const int nl = (int)p.couplings.size(), np = L.ld_parts;
         E.record("k_ld_reduce", 0, 0, [=](void* st) { launch_ld_reduce(ld, logdet_per_image, B, nl, np, 0, (hipStream_t)st); });
     }
-    check_launch();
+    if (!p.dry) check_launch();
 }
 
 extern "C" {
@@ -1254,6 +1263,35 @@ int cnf_debug_netlds_shape(const cnf_plan* plan, int coupling, int* words, int c
     return NETSHAPE_WORDS;
 }
 int cnf_debug_netlds_nshapes() { return netlds_num_shapes(); }
+
+// k_pw launch shapes of a B-image forward, from a host-only dry run (nothing is launched or
+// dereferenced: the tensors are placeholder addresses); returns the number of words written
+int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap) {
+    if (!plan || !words || B <= 0) return -1;
+    Plan& p = *plan->p;
+    CNF_TRY
+    p.dry = true;
+    p.pw_shapes.clear();
+    char* fake = reinterpret_cast<char*>(uintptr_t(1) << 40);   // never dereferenced
+    try {
+        flow_forward(p, (const float*)fake, (const float*)fake, (const float*)fake, (float*)fake, (float*)fake, fake, B,
+                     nullptr, false);
+    } catch (...) {
+        p.dry = false;
+        throw;
+    }
+    p.dry = false;
+    p.recorded.clear();
+    const int n = (int)p.pw_shapes.size() * PWSHAPE_WORDS;
+    if (n > cap) return -1;
+    for (size_t i = 0; i < p.pw_shapes.size(); i++)
+        std::memcpy(words + i * PWSHAPE_WORDS, &p.pw_shapes[i], sizeof(PwShape));
+    return n;
+    CNF_CATCH
+}
+
+int cnf_debug_pw_nshapes() { return pw_num_shapes(); }
+int cnf_debug_pw_words() { return PWSHAPE_WORDS; }
 
 // shape words of coupling `coupling`'s k_gc launches (0 if it has none)
 int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) {

@@ -19,78 +19,84 @@
 
 namespace cnf {
 
+#include "cnf_pw_shapes.inc"   // shape-specialised k_pw instantiations (gen_netlds_shapes.py)
+
 constexpr int PW_LDS_STAT = 256;    // byte offset of the per-image (mean, rstd) table
 constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 
 #ifndef CNF_PW_MINW
 #define CNF_PW_MINW 2
 #endif
-template <int NR, int GM, bool LN, bool RES>
+// shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
+#define PP(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : P.f)
+#define PA(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : a.f)
+template <int NR, int GM, bool LN, bool RES, int SID>
 __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
     const ConvProb P = a.p[blockIdx.y];
-    const int HW = a.H * a.W;
-    const int tile = blockIdx.x % a.tiles_per_img;
-    const int img0 = (blockIdx.x / a.tiles_per_img) * a.ipw;
+    const int HW = PA(H) * PA(W);
+    const int tile = blockIdx.x % PA(tiles_per_img);
+    const int img0 = (blockIdx.x / PA(tiles_per_img)) * a.ipw;
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
-    const int cin = P.cin, G = (cin + 15) >> 4, cout = P.cout;
+    const int cin = PP(cin), G = (cin + 15) >> 4, cout = PP(cout);
     constexpr int NSJ = 16 * NR;
-    float* lw = reinterpret_cast<float*>(smem + P.lds_w_off);
+    float* lw = reinterpret_cast<float*>(smem + PP(lds_w_off));
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
-    const uint32_t in_img = (uint32_t)HW * P.in_cs * 4u, out_img = (uint32_t)HW * P.out_cs * 4u;
+    const uint32_t in_img = (uint32_t)HW * PP(in_cs) * 4u, out_img = (uint32_t)HW * PP(out_cs) * 4u;
     const auto rin = buf_rsrc(P.in, (uint32_t)a.B * in_img);
     const auto rout = buf_rsrc(P.out, (uint32_t)a.B * out_img);
     const auto rres = buf_rsrc(RES ? P.res : P.out, (uint32_t)a.B * out_img);
 
-    // A operand: lane (i16, kq) feeds pixel pa, channels 16g + 4kq + s at k-step s of group g
+    // A operand: lane (i16, kq) feeds pixel pa, channels 16g + 4kq + s at k-step s of group g. Masks
+    // are evaluated per element from shape fields (folded to constants in the specialised
+    // instantiations, whose offsets then become lane base + immediate)
+    const bool full_px = HW % (16 * NW) == 0;
     const int pa = tile * (16 * NW) + wave * 16 + i16;
-    const bool pav = pa < HW;
-    const uint32_t aoff = ((uint32_t)pa * P.in_cs + P.in_off + 4 * kq) * 4u;
-    uint32_t goff[GM];   // byte offset of group g inside one image, BUF_OOB when masked
-#pragma unroll
-    for (int g = 0; g < GM; g++) goff[g] = (pav && g < G && 16 * g + 4 * kq < cin) ? aoff + 64u * g : BUF_OOB;
+    const bool pav = full_px || pa < HW;
+    const uint32_t aoff = ((uint32_t)pa * PP(in_cs) + PP(in_off) + 4 * kq) * 4u;
+    auto gok = [&](int g) { return pav && g < G && (cin % 16 == 0 || 16 * g + 4 * kq < cin); };
     // output: acc[n][r] = out[pixel po0 + r][channel 16n + i16]
     const int po0 = tile * (16 * NW) + wave * 16 + kq * 4;
-    uint32_t oo[NR][4];   // byte offset inside one image, BUF_OOB for masked pixels/channels
-    bool valid[NR * 4];
-#pragma unroll
-    for (int n = 0; n < NR; n++) {
+    const uint32_t obase = ((uint32_t)po0 * PP(out_cs) + PP(out_off) + i16) * 4u;
+    const bool all_st = PP(st_mask_lo) == ~0u && PP(st_mask_hi) == ~0u;
+    auto chv = [&](int n) { return cout % 16 == 0 || n * 16 + i16 < cout; };
+    auto pv = [&](int r) { return full_px || po0 + r < HW; };
+    auto ooff = [&](int n, int r) -> uint32_t {   // byte offset inside one image, BUF_OOB when not stored
         const int ch = n * 16 + i16;
-        const bool chv = ch < cout;
-        const bool st = chv && stored(P, ch);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const bool pv = po0 + r < HW;
-            oo[n][r] = (pv && st) ? ((uint32_t)(po0 + r) * P.out_cs + P.out_off + ch) * 4u : BUF_OOB;
-            valid[n * 4 + r] = pv && chv;
-        }
-    }
+        const bool st = all_st || ((ch < 32 ? (PP(st_mask_lo) >> ch) : (PP(st_mask_hi) >> (ch - 32))) & 1u) != 0u;
+        return (pv(r) && chv(n) && st) ? obase + (uint32_t)(r * PP(out_cs) + 16 * n) * 4u : BUF_OOB;
+    };
+    // image activations (+ residual) in registers, one image ahead (two ahead measured slower)
     f4 x[GM];
     float rv[NR][4];
-    auto load_img = [&](int ii) {
+    auto load_img = [&](int ii, f4 (&xd)[GM], float (&rd)[NR][4]) {
         const uint32_t ib = (uint32_t)(img0 + ii) * in_img;
 #pragma unroll
-        for (int g = 0; g < GM; g++) x[g] = buf_load4(rin, goff[g] == BUF_OOB ? BUF_OOB : ib + goff[g]);
+        for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
         if (RES) {
             const uint32_t ob = (uint32_t)(img0 + ii) * out_img;
 #pragma unroll
             for (int n = 0; n < NR; n++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) rv[n][r] = buf_load1(rres, oo[n][r] == BUF_OOB ? BUF_OOB : ob + oo[n][r]);
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t o = ooff(n, r);
+                    rd[n][r] = buf_load1(rres, o == BUF_OOB ? BUF_OOB : ob + o);
+                }
         }
     };
-    load_img(0);
+    load_img(0, x, rv);
     f4 gm[GM], bt[GM];
     if (LN) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
-            gm[g] = buf_load4(rg, goff[g]);   // 0 where masked: the normalised value is then exactly 0
-            bt[g] = buf_load4(rb, goff[g]);
+            const uint32_t o = gok(g) ? aoff + 64u * g : BUF_OOB;   // 0 where masked: the normalised value is then exactly 0
+            gm[g] = buf_load4(rg, o);
+            bt[g] = buf_load4(rb, o);
         }
     }
     float bias[NR];
@@ -98,7 +104,9 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     for (int n = 0; n < NR; n++) bias[n] = n * 16 + i16 < cout ? P.bias[n * 16 + i16] : 0.f;
 
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
-    copy_to_lds<64 * NW>(P.wt, lw, G * 16 * NSJ);
+    int nwf = G * 16 * NSJ;
+    asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
+    copy_to_lds<64 * NW>(P.wt, lw, nwf);
     if (LN) {
         for (int i = wave; i < nimg; i += NW) {
             float mu, rs;
@@ -112,47 +120,68 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     __syncthreads();
 
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
-    for (int ii = 0; ii < nimg; ii++) {
+    // one image: A operand from xc / rc, which then receive image pf (when it exists)
+    auto step = [&](int ii, f4 (&xc)[GM], float (&rc)[NR][4], int pf) {
         const int img = img0 + ii;
         const float rs = LN ? lstat[2 * ii + 1] : 1.f;
         const float nmr = LN ? -lstat[2 * ii] * rs : 0.f;
         float av[GM][4];
 #pragma unroll
-        for (int g = 0; g < GM; g++)
+        for (int g = 0; g < GM; g++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const float v = lrelu(x[g][j]);
+                const float v = lrelu(xc[g][j]);
                 av[g][j] = LN ? fmaf(fmaf(v, rs, nmr), gm[g][j], bt[g][j]) : v;
             }
+        }
         float res[NR][4];
         if (RES) {
 #pragma unroll
             for (int n = 0; n < NR; n++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) res[n][r] = rv[n][r];
+                for (int r = 0; r < 4; r++) res[n][r] = rc[n][r];
         }
 #ifndef CNF_ABL_PW_NOLOAD
-        if (ii + 1 < nimg) load_img(ii + 1);   // in flight during this image's MFMAs and stores
+        if (pf < nimg) load_img(pf, xc, rc);   // in flight during this image's MFMAs and stores
 #endif
         f4 acc[NR];
 #pragma unroll
         for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
+        // B quads double-buffered one group ahead; the scheduling fence per group keeps the
+        // compiler from hoisting every group's LDS reads (NR quads each) into live registers
+        // (the generic instantiations keep the plain per-group loop: their runtime group bound already
+        // limits the hoisting, and the extra buffer costs them registers)
+        f4 bq[2][NR];
+#pragma unroll
+        for (int n = 0; n < NR; n++) bq[0][n] = *reinterpret_cast<const f4*>(brow + n * 64);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
-            if (g < G) {
-                f4 bq[NR];
+            if (SID < 0 && g < G) {
+                f4 bp[NR];
 #pragma unroll
-                for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
+                for (int n = 0; n < NR; n++) bp[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
 #pragma unroll
                 for (int s = 0; s < 4; s++)
 #pragma unroll
                     for (int n = 0; n < NR; n++)
-                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bq[n][s], acc[n], 0, 0, 0);
+                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bp[n][s], acc[n], 0, 0, 0);
+            } else if (SID >= 0 && g < G) {
+                if (g + 1 < GM && g + 1 < G)
+#pragma unroll
+                    for (int n = 0; n < NR; n++)
+                        bq[(g + 1) & 1][n] = *reinterpret_cast<const f4*>(brow + (size_t)(g + 1) * 4 * NSJ * 4 + n * 64);
+#pragma unroll
+                for (int s = 0; s < 4; s++)
+#pragma unroll
+                    for (int n = 0; n < NR; n++)
+                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bq[g & 1][n][s], acc[n], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         // epilogue: bias, residual, masked store, per-wave LN partial of LeakyReLU(out)
         const uint32_t ob = (uint32_t)img * out_img;
         float vals[NR * 4];
+        bool valid[NR * 4];
 #pragma unroll
         for (int n = 0; n < NR; n++)
 #pragma unroll
@@ -160,21 +189,47 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
                 float v = acc[n][r] + bias[n];
                 if (RES) v += res[n][r];
 #ifndef CNF_ABL_PW_NOSTORE
-                buf_store1(rout, oo[n][r] == BUF_OOB ? BUF_OOB : ob + oo[n][r], v);
+                const uint32_t o = ooff(n, r);
+                buf_store1(rout, o == BUF_OOB ? BUF_OOB : ob + o, v);
 #endif
                 vals[n * 4 + r] = lrelu(v);
+                valid[n * 4 + r] = pv(r) && chv(n);
             }
         if (P.out_part != nullptr)
             ln_partial(vals, valid,
-                       P.out_part + ((size_t)img * P.part_stride + P.out_part_base + tile * NW + wave) * LNP);
-    }
+                       P.out_part + ((size_t)img * PP(part_stride) + tile * NW + wave) * LNP);
+    };
+    for (int ii = 0; ii < nimg; ii++) step(ii, x, rv, ii + 1);
 }
+
+#undef PP
+#undef PA
+
+template <int S>
+bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStream_t st) {
+    if constexpr (S < CNF_PW_NSHAPES) {
+        if (sid == S) {
+            constexpr PwShape k = kPwShapes[S];
+            hipLaunchKernelGGL((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S>), g, b, lds, st, a);
+            return true;
+        }
+        return launch_pw_shape<S + 1>(sid, a, g, b, lds, st);
+    }
+    return false;
+}
+
+int pw_num_shapes() { return CNF_PW_NSHAPES; }
 
 void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
+    static const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob
+    PwShape sh;
+    if (!generic && pw_shape_of(nr, gm, ln, res, a, sh))
+        for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
+            if (std::memcmp(&sh, &kPwShapes[sid], sizeof(sh)) == 0 && launch_pw_shape<0>(sid, a, g, b, lds, st)) return;
 #define CNF_PW_CASE(NR_, GM_, LN_, RES_)                                              \
     if (nr == NR_ && gm == GM_ && ln == LN_ && res == RES_) {                          \
-        hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, RES_>), g, b, lds, st, a);             \
+        hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
         return;                                                                        \
     }
 #define CNF_PW_NR(GM_, LN_, RES_) \

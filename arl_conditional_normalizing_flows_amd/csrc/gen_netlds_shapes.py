@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Generate cnf_netlds_shapes.inc and cnf_gc_shapes.inc. The first holds the k_net_lds "shape words" (NETSHAPE_WORDS ints: every
+"""Generate cnf_netlds_shapes.inc, cnf_gc_shapes.inc and cnf_pw_shapes.inc. The first holds the k_net_lds "shape words" (NETSHAPE_WORDS ints: every
 launch-independent field of NetLdsArgs except the mask) of the LDS-resident coupling layers of the
 presets in SPECIALISE. cnf_netlds.hip compiles one shape-specialised instantiation per entry, with
 those words as compile-time constants; launch_net_lds picks it when a launch's words match and
 otherwise runs the generic kernel, so a stale table is never wrong, only slower (and
 tests/test_capi.py fails on it). The second holds the GcShape (branch geometry, tile, strides) of the
-streamed layers' k_gc launches, used the same way by cnf_stream.hip.
+streamed layers' k_gc launches, used the same way by cnf_stream.hip; the third the PwShape of every
+k_pw launch of the forward, taken from a host-only dry run of it (cnf_debug_pw_shapes).
 
     python arl_conditional_normalizing_flows_amd/csrc/gen_netlds_shapes.py [--check]
 
@@ -26,6 +27,9 @@ from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 SPECIALISE = ('cfg2',)   # the benchmark configuration (BASELINE.json configs[1])
 OUT = HERE / 'cnf_netlds_shapes.inc'
 OUT_GC = HERE / 'cnf_gc_shapes.inc'
+OUT_PW = HERE / 'cnf_pw_shapes.inc'
+PW_BATCH = 64                 # the benchmark batch (k_pw shapes do not depend on it: ipw and B stay runtime)
+PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel masks
 GC_BRANCH_WORDS = 16          # GcBranch: 14 ints, then the two uint32 division magics
 GC_MAXBR = 8
 CNF_LAYER_COUPLING = 0
@@ -90,6 +94,40 @@ def gc_shapes(lib):
     return out
 
 
+def pw_shapes(lib):
+    lib.cnf_debug_pw_shapes.restype = C.c_int
+    lib.cnf_debug_pw_shapes.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
+    out = []
+    for name in SPECIALISE:
+        plan, _keep = _plan(lib, PRESETS[name])
+        buf = (C.c_int * (CAP * 8))()
+        n = lib.cnf_debug_pw_shapes(plan, PW_BATCH, buf, CAP * 8)
+        if n < 0:
+            raise RuntimeError('cnf_debug_pw_shapes failed: ' + lib.cnf_last_error().decode())
+        nw = lib.cnf_debug_pw_words()  # PWSHAPE_WORDS
+        for i in range(0, n, nw):
+            w = tuple(buf[i + j] for j in range(nw))
+            if w not in out:
+                out.append(w)
+        lib.cnf_plan_destroy(plan)
+    return out
+
+
+def render_pw(sh):
+    lines = ['// Generated by gen_netlds_shapes.py from dry runs of the ' + ', '.join(SPECIALISE) + ' forward: do not edit.',
+             '// One k_pw PwShape (cnf_kernels.h) per shape-specialised instantiation.',
+             f'#define CNF_PW_NSHAPES {len(sh)}',
+             f'constexpr PwShape kPwShapes[{max(1, len(sh))}] = {{']
+    for w in sh or [None]:
+        if w is None:
+            lines.append('    {},')
+            continue
+        k = len(w) - PW_MASK_WORDS
+        lines.append('    {' + ', '.join([str(x) for x in w[:k]] + [f'{x & 0xffffffff}u' for x in w[k:]]) + '},')
+    lines.append('};')
+    return '\n'.join(lines) + '\n'
+
+
 def render_gc(sh):
     lines = ['// Generated by gen_netlds_shapes.py from the plans of ' + ', '.join(SPECIALISE) + ': do not edit.',
              '// One k_gc GcShape (cnf_kernels.h) per shape-specialised instantiation.',
@@ -135,8 +173,8 @@ def render(sh):
 
 def main():
     lib = _lib.load()
-    sh, gsh = shapes(lib), gc_shapes(lib)
-    outs = [(OUT, render(sh), len(sh)), (OUT_GC, render_gc(gsh), len(gsh))]
+    sh, gsh, psh = shapes(lib), gc_shapes(lib), pw_shapes(lib)
+    outs = [(OUT, render(sh), len(sh)), (OUT_GC, render_gc(gsh), len(gsh)), (OUT_PW, render_pw(psh), len(psh))]
     if '--check' in sys.argv:
         bad = [f.name for f, text, _ in outs if (f.read_text() if f.exists() else '') != text]
         if bad:

@@ -24,6 +24,7 @@ cfg = PRESETS[os.environ.get('CNF_DIAG_CFG', 'cfg2')]
 flow = cFlow(**cfg.kwargs())
 buf = np.zeros(256, dtype=np.int64)
 cyc = np.zeros(256, dtype=np.int64)
+prev = None
 for li, layer in enumerate(flow.layers_list):
     if not hasattr(layer, 'which_mask'):
         continue
@@ -34,8 +35,9 @@ for li, layer in enumerate(flow.layers_list):
     lib.cnf_debug_read_stamps(buf.ctypes.data, 256)
     lib.cnf_debug_read_cycles(cyc.ctypes.data, 256)
     n = int(buf[255])
-    if n == 0:
-        continue   # streamed layer: no k_net_lds launch
+    if n == 0 or (prev is not None and np.array_equal(prev, buf)):
+        continue   # streamed layer: no k_net_lds launch (the stamps are the previous layer's)
+    prev = buf.copy()
     c = cyc[:n].astype(np.float64)
     rt_us = (buf[1] - buf[0]) * 10.0 / 1000.0
     ghz = (c[-1] - c[0]) / max(rt_us, 1e-9) / 1e3
