@@ -131,6 +131,7 @@ struct GcShape {
     GcBranch br[GC_MAXBR];
     int nbr, H, W, in_cs, out_cs, TH, tiles_per_img;
     int band_bytes;              // offset of the second band buffer (double-buffered staging)
+    int lnst;                    // bit 0: LN2 on load (in_part set), bit 1: LN3 partials out (out_part set)
 };
 constexpr int GCSHAPE_WORDS = (int)(sizeof(GcShape) / 4);
 struct GcArgs {

@@ -650,6 +650,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             const int64_t units = (int64_t)ga.s.tiles_per_img * 2 * B;
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
             ga.s.band_bytes = c.gc_band_bytes;
+            ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
             if (8 * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.s.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
@@ -1311,6 +1312,7 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
     s.TH = c.gc_TH;
     s.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
     s.band_bytes = c.gc_band_bytes;
+    s.lnst = p.desc.layer_norm ? 3 : 0;   // the forward's k_gc: LN2 on load and LN3 partials iff LayerNorm
     std::memcpy(words, &s, sizeof(s));
     return GCSHAPE_WORDS;
 }

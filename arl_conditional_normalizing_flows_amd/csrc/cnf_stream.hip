@@ -259,10 +259,12 @@ constexpr int GC_NT = 64 * GC_NW;   // threads
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
 #define GS(f) (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].f : a.s.f)
 
-template <int NR, int SID>
-__device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, const unsigned char* smem,
+// BI >= 0 (specialised instantiations): branch BI of table entry SID, every field a constant
+template <int NR, int SID, int BI>
+__device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, const unsigned char* smem,
                                           const float* bias, float* __restrict__ outp, int npx,
                                           int px0, LnAcc& st, bool& first, bool stats, int boff) {
+    const GcBranch& br = BI >= 0 ? kGcShapes[SID >= 0 ? SID : 0].br[BI >= 0 ? BI : 0] : brx;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     constexpr int NSJ = 16 * NR;
@@ -361,6 +363,18 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& br, c
 
 constexpr int GC_GQ = 4;   // staged band quads per thread (the plan checks the total fits)
 
+// the branches of table entry SID, unrolled at compile time
+template <int SID, int BI>
+__device__ __forceinline__ void gc_branches(const GcArgs& a, const unsigned char* smem, float* __restrict__ outp,
+                                            int npx, int px0, LnAcc& st, bool& first, bool stats, int boff) {
+    if constexpr (BI < kGcShapes[SID].nbr) {
+        constexpr GcBranch br = kGcShapes[SID].br[BI];
+        const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
+        gc_branch<(br.cout + 15) / 16, SID, BI>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff);
+        gc_branches<SID, BI + 1>(a, smem, outp, npx, px0, st, first, stats, boff);
+    }
+}
+
 // diagnostic phase stamps of workgroup (0, 0) (CNF_GC_STAMPS builds only; never in timed runs)
 __device__ long long g_gc_stamps[64];
 #ifdef CNF_GC_STAMPS
@@ -388,10 +402,10 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int H = GS(H), W = GS(W), HW = H * W;
     const int r0 = tile * GS(TH);
-    const int rows = min(GS(TH), H - r0);
+    const int rows = GS(H) % GS(TH) == 0 ? GS(TH) : min(GS(TH), H - r0);   // constant when tiles are full
     const int npx = rows * W, px0 = r0 * W;
-    const bool ln = a.in_part[net] != nullptr;
-    const bool stats = a.out_part[net] != nullptr;
+    const bool ln = SID >= 0 ? (GS(lnst) & 1) != 0 : a.in_part[net] != nullptr;
+    const bool stats = SID >= 0 ? (GS(lnst) & 2) != 0 : a.out_part[net] != nullptr;
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     float* lds_f = reinterpret_cast<float*>(smem);
     int gs = 0;
@@ -516,16 +530,20 @@ __global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
         bool first = true;
         float* outp = a.out[net] + (size_t)img * HW * GS(out_cs);
         const int boff = (ii & 1) * GS(band_bytes);
-        for (int bi = 0; bi < GS(nbr); bi++) {
-            const GcBranch& br = GS(br)[bi];
-            const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
-            switch ((br.cout + 15) >> 4) {
-                case 1: gc_branch<1, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                case 2: gc_branch<2, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                case 3: gc_branch<3, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                default: gc_branch<4, SID>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+        if constexpr (SID >= 0) {
+            gc_branches<SID, 0>(a, smem, outp, npx, px0, st, first, stats, boff);
+        } else {
+            for (int bi = 0; bi < GS(nbr); bi++) {
+                const GcBranch& br = GS(br)[bi];
+                const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
+                switch ((br.cout + 15) >> 4) {
+                    case 1: gc_branch<1, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                    case 2: gc_branch<2, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                    case 3: gc_branch<3, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                    default: gc_branch<4, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                }
+                GSTAMP(gs++);
             }
-            GSTAMP(gs++);
         }
         if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * LNP);
         if (ii + 1 < nimg) store_img(ii + 1);   // the other buffer: nobody reads it this iteration
