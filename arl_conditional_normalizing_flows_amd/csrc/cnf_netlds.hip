@@ -670,11 +670,26 @@ __device__ __forceinline__ void build_ktab(int* ktab, int cin, int ic0, int d, i
     }
 }
 
-// 3x3 dilated conv, PK_KN (any cin): scalar A reads through the tap table, K = 9*cin padded to 4
-template <int NR>
+// the tap geometry of a PK_KN conv, for decoding its tap table in registers (cin == 0: read the
+// LDS table; the shape-specialised instantiations pass constants)
+struct KTap {
+    int cin, ic0, d;
+};
+
+// 3x3 dilated conv, PK_KN (any cin): scalar A reads through the tap table, K = 9*cin padded to 4.
+// SPEC: k loop fully unrolled (constant Kpad) and entries decoded from kt instead of the table
+template <int NR, bool SPEC>
 __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* __restrict__ bias, LStat& st, bool stats, const KSplit& ks) {
+                                           const float* __restrict__ bias, LStat& st, bool stats, const KSplit& ks,
+                                           KTap kt) {
+    // table entry k: (dr + 32) << 24 | (dc + 32) << 16 | channel, or -1 beyond K
+    auto tap_of = [&](int k) -> int {
+        if (!SPEC) return ktab[k];
+        if (k >= 9 * kt.cin) return -1;
+        const int tap = k / kt.cin, c = k - tap * kt.cin;
+        return (((tap / 3 - 1) * kt.d + 32) << 24) | (((tap % 3 - 1) * kt.d + 32) << 16) | (kt.ic0 + c);
+    };
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W;
@@ -691,7 +706,7 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
         const bool pva = pa < HW;
         const int ra = pva ? pa / W : -4096, ca = pva ? pa - (pa / W) * W : -4096;
         for (int k0 = 4 * glo; k0 < 4 * ghi; k0 += 4) {
-            const int t = ktab[k0 + kq];
+            const int t = ktab[k0 + kq];   // runtime slice bounds: the table read beats a decode
             const int c = t & 0xffff;
             const int dr = ((t >> 24) & 0xff) - 32, dc = ((t >> 16) & 0xff) - 32;
             const int ya = ra + dr, xa = ca + dc;
@@ -717,9 +732,8 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
             acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
             acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
         }
-#pragma unroll 2
-        for (int k0 = 0; k0 < Kpad; k0 += 4) {
-            const int t = ktab[k0 + kq];
+        auto kstep = [&](int k0) {
+            const int t = tap_of(k0 + kq);
             const int c = t & 0xffff;
             const int dr = ((t >> 24) & 0xff) - 32, dc = ((t >> 16) & 0xff) - 32;
             const int ya = ra + dr, xa = ca + dc, yb = rb + dr, xb = cb + dc;
@@ -734,6 +748,13 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
                 acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc0[n], 0, 0, 0);
                 acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc1[n], 0, 0, 0);
             }
+        };
+        if constexpr (SPEC) {
+#pragma unroll
+            for (int k0 = 0; k0 < Kpad; k0 += 4) kstep(k0);
+        } else {
+#pragma unroll 2
+            for (int k0 = 0; k0 < Kpad; k0 += 4) kstep(k0);
         }
         if (stats) lst_setk(st, acc0[0][0] + ep.bz[0]);
         ep.store(acc0, s0, HW, out, ostride, false, stats, st);
@@ -741,22 +762,24 @@ __device__ __forceinline__ void conv3k_lds(const float* in, int istride, int H, 
     }
 }
 
-template <int MAXNR>
+template <int MAXNR, bool SPEC>
 __device__ __forceinline__ void conv3k_any(const float* in, int istride, int H, int W, const float* wl, int Kpad,
                                            int NS, const int* ktab, float* out, int ostride, int cout,
-                                           const float* bias, LStat& st, bool stats, const KSplit& ks) {
+                                           const float* bias, LStat& st, bool stats, const KSplit& ks, KTap kt) {
     const int nr = (cout + 15) / 16;
     if (MAXNR <= 2 || nr <= 2) {
         if (nr == 1)
-            conv3k_lds<1>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
+            conv3k_lds<1, SPEC>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks, kt);
         else
-            conv3k_lds<2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
+            conv3k_lds<2, SPEC>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks, kt);
         return;
     }
     if (nr == 3)
-        conv3k_lds<MAXNR >= 3 ? 3 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
+        conv3k_lds<MAXNR >= 3 ? 3 : 2, SPEC>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats,
+                                              ks, kt);
     else
-        conv3k_lds<MAXNR >= 4 ? 4 : 2>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats, ks);
+        conv3k_lds<MAXNR >= 4 ? 4 : 2, SPEC>(in, istride, H, W, wl, Kpad, NS, ktab, out, ostride, cout, bias, st, stats,
+                                              ks, kt);
 }
 
 // entries of the tap (PK_KN) / quad (PK_Q4) table of a 3x3 conv, rounded to 4
@@ -769,14 +792,15 @@ __device__ __forceinline__ void conv3_table(const LdsConv& cv, int* tab, int cin
     else
         build_ktab(tab, cin, ic0, d, cv.kpad);
 }
-template <int MAXNR>
+template <int MAXNR, bool SPEC = false>
 __device__ __forceinline__ void conv3_run(const LdsConv& cv, const float* in, int istride, int H, int W,
                                           const float* wl, const int* tab, float* out, int ostride, int cout,
-                                          const float* bias, LStat& st, bool stats, const float* zq, const KSplit& ks) {
+                                          const float* bias, LStat& st, bool stats, const float* zq, const KSplit& ks,
+                                          KTap kt = KTap{0, 0, 0}) {
     if (cv.fmt == PK_Q4)
         conv3q_any<MAXNR>(in, istride, cv.kpad >> 4, H, W, wl, tab, out, ostride, cout, bias, st, stats, zq, ks);
     else
-        conv3k_any<MAXNR>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, st, stats, ks);
+        conv3k_any<MAXNR, SPEC>(in, istride, H, W, wl, cv.kpad, cv.ns, tab, out, ostride, cout, bias, st, stats, ks, kt);
 }
 
 // position in u of element (pixel p, channel c) of the compressed u1c (mask compress, :720-759)
@@ -954,12 +978,20 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         {
             int kto = 0;
-            for (int bi = 0; bi < SA(nbr); bi++) {
+            auto run_br = [&](int bi) {
                 const LdsConv& cv = SA(gcv)[bi];
                 const float* wbr = WL + (o[10 + 2 * bi] - o[10]);
-                conv3_run<MAXNR>(cv, T1, S1, H, W, wbr, KT + kto, T2 + SA(br_out_off)[bi], S2, SA(br_cout)[bi],
-                          WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ, KSplit{ksb, bi & 1});
+                conv3_run<MAXNR, (SID >= 0)>(cv, T1, S1, H, W, wbr, KT + kto, T2 + SA(br_out_off)[bi], S2,
+                                             SA(br_cout)[bi], WL + (o[11 + 2 * bi] - o[10]), st, ln, ZQ,
+                                             KSplit{ksb, bi & 1},
+                                             KTap{SA(br_cin)[bi], SA(br_cin_off)[bi], SA(br_dil)[bi]});
                 kto += ktab_len(cv);
+            };
+            if constexpr (SID >= 0) {   // unrolled: every branch's format, extents and offsets constant
+#pragma unroll
+                for (int bi = 0; bi < kNetShapes[SID >= 0 ? SID : 0].nbr; bi++) run_br(bi);
+            } else {
+                for (int bi = 0; bi < SA(nbr); bi++) run_br(bi);
             }
         }
         if (ln) lst_flush(st, slots);
