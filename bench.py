@@ -111,13 +111,18 @@ def pmc_traffic(kernel):
                 ks = json.load(fh).get('kernels', {})
         except (OSError, ValueError):
             continue
+        # every instantiation of the symbol (shape-specialised ones included), weighted by dispatches
+        tot = n = 0.0
         for k, e in ks.items():
             sym = k.split('::')[-1]
-            if sym.startswith(kernel + '<') or sym == kernel:
-                h = e.get('hbm')
-                if h:
-                    return {'traffic': round(h['traffic_bytes'], 1), 'traffic_unit': 'bytes/launch',
-                            'traffic_source': os.path.relpath(f, ROOT)}
+            h = e.get('hbm')
+            if h and (sym.startswith(kernel + '<') or sym == kernel):
+                d = float(h.get('dispatches', 1))
+                tot += h['traffic_bytes'] * d
+                n += d
+        if n > 0:
+            return {'traffic': round(tot / n, 1), 'traffic_unit': 'bytes/launch',
+                    'traffic_source': os.path.relpath(f, ROOT)}
     return {'traffic': None}
 
 

@@ -54,7 +54,8 @@ def main(out, tag):
         if k in fetch and k in write:
             fb = fetch[k]['FETCH_SIZE'] * 1024.0
             wb = write[k]['WRITE_SIZE'] * 1024.0
-            e['hbm'] = {'fetch_size_bytes': fb, 'write_size_bytes': wb, 'traffic_bytes': 2.0 * fb + wb}
+            e['hbm'] = {'fetch_size_bytes': fb, 'write_size_bytes': wb, 'traffic_bytes': 2.0 * fb + wb,
+                        'dispatches': min(fetch[k]['dispatches'], write[k]['dispatches'])}
         if k in sq:
             s = sq[k]
             e['sq'] = s
