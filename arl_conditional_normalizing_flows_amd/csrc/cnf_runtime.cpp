@@ -308,7 +308,10 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         }
         lds = std::max(lds, off);
         flops += 2.0 * HWB * K * s.cout;
-        bytes += 4.0 * (HWB * s.cin + HWB * s.cout * (s.res ? 2 : 1) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
+        // output bytes count only the stored channels (conv_a stores just the grouped branches' inputs)
+        const uint64_t cmask = s.cout >= 64 ? ~0ull : ((1ull << s.cout) - 1);
+        const double stored = (double)__builtin_popcountll(store_mask & cmask);
+        bytes += 4.0 * (HWB * s.cin + HWB * (stored + (s.res ? s.cout : 0)) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
                         (double)K * s.cout + s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
