@@ -195,7 +195,8 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, const ConvArgs& a, Pw
     return true;
 }
 void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
-int pw_num_shapes();   // shape-specialised k_pw instantiations compiled in
+int pw_num_shapes();
+int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS): [4 workgroups][16]   // shape-specialised k_pw instantiations compiled in
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

@@ -1323,6 +1323,7 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }
 int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }
+int cnf_debug_read_pw_stamps(long long* out) { return read_pw_stamps(out); }
 
 int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)plan->p->recorded.size() : -1; }
 

@@ -30,10 +30,27 @@ constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
 #define PP(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : P.f)
 #define PA(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : a.f)
+__device__ long long g_pw_stamps[4][16];
+#ifdef CNF_PW_STAMPS
+#define PWSTAMP(i)                                                                                       \
+    do {                                                                                                 \
+        if (SID >= 0 && SID < 2 && threadIdx.x == 0 && blockIdx.y == 0 &&                                \
+            (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))                                            \
+            g_pw_stamps[2 * (SID >= 0 ? SID : 0) + (blockIdx.x == 0 ? 0 : 1)][(i)] =                     \
+                (long long)__builtin_amdgcn_s_memrealtime();                                             \
+    } while (0)
+#else
+#define PWSTAMP(i) do { } while (0)
+#endif
+int read_pw_stamps(long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pw_stamps), sizeof(g_pw_stamps)) == hipSuccess ? 0 : -1;
+}
+
 template <int NR, int GM, bool LN, bool RES, int SID>
 __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
+    PWSTAMP(0);
     const ConvProb P = a.p[blockIdx.y];
     const int HW = PA(H) * PA(W);
     const int tile = blockIdx.x % PA(tiles_per_img);
@@ -117,7 +134,9 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             }
         }
     }
+    PWSTAMP(1);
     __syncthreads();
+    PWSTAMP(2);
 
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
     // one image: A operand from xc / rc, which then receive image pf (when it exists)
@@ -199,7 +218,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             ln_partial(vals, valid,
                        P.out_part + ((size_t)img * PP(part_stride) + tile * NW + wave) * LNP);
     };
-    for (int ii = 0; ii < nimg; ii++) step(ii, x, rv, ii + 1);
+    for (int ii = 0; ii < nimg; ii++) {
+        step(ii, x, rv, ii + 1);
+        PWSTAMP(3 + ii);
+    }
 }
 
 #undef PP
