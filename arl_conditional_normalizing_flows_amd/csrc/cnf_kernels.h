@@ -120,6 +120,11 @@ inline void netshape_words(const NetLdsArgs& a, int* w) {
 // bands with their own dilation halo (LN2 + LeakyReLU applied on the way in, zero padding), so
 // the 3x3 taps need no bounds checks; weights are PK_Q4 over cin padded to a multiple of 4.
 constexpr int GC_MAXBR = 8;
+// waves per k_gc workgroup (one LN partial slot per wave): the shape-specialised instantiations
+// run 16 (one 16-pixel subtile per wave and pass, 4 waves per SIMD within their 128 VGPRs), the
+// generic one 8 (two subtiles per wave sharing every B read; it needs the registers)
+constexpr int GC_NW_GEN = 8, GC_NW_SPEC = 16, GC_NW_MAX = 16;
+constexpr int GC_STAGE_QUADS = 2048;   // staged band quads per workgroup
 struct GcBranch {
     int cin_off, cin, cinp, cout, out_off, dil;   // input window, padded channels, outputs
     int G;                                        // quad groups of the PK_Q4 image
@@ -147,6 +152,7 @@ struct GcArgs {
     int B, ipw, in_nparts, part_stride;
 };
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st);
+int gc_waves(const GcArgs& a);   // waves per workgroup of the instantiation launch_gc picks for a
 int read_gc_stamps(long long* host, int n);
 int gc_num_shapes();   // shape-specialised k_gc instantiations compiled in
 // k_toy (cnf_toy.hip): TOYcINN dense flow, one thread per 3-dimensional sample

@@ -434,7 +434,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
                     gb.push_back(g);
                 }
-                int64_t quads = 0;   // staged band quads: at most 4 per thread of the 512-thread workgroup
+                int64_t quads = 0;   // staged band quads: at most GC_STAGE_QUADS per workgroup
                 for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
                 // two band buffers: the next image is staged while the current one is computed
                 const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
@@ -443,7 +443,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     g.b_off = (int)off;
                     off = align16(off + 4LL * g.cout);
                 }
-                if (!ok || off > 160 * 1024 || quads > 4 * 512 || !allow_gc) continue;
+                if (!ok || off > 160 * 1024 || quads > GC_STAGE_QUADS || !allow_gc) continue;
                 c.gc_fused = true;
                 c.gc_TH = TH;
                 c.gc_lds = (int)off;

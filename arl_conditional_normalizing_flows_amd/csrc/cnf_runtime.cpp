@@ -115,7 +115,7 @@ WsLayout Plan::layout(int B) const {
         parts = std::max(parts, 4 * g.tiles * (int)c.br.size());   // 4 waves per workgroup
         parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
         parts = std::max(parts, 4 * ((c.hc * c.wc + 63) / 64));   // k_pw
-        if (c.gc_fused) parts = std::max(parts, 8 * ((c.hc + c.gc_TH - 1) / c.gc_TH));   // k_gc
+        if (c.gc_fused) parts = std::max(parts, GC_NW_MAX * ((c.hc + c.gc_TH - 1) / c.gc_TH));   // k_gc
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
     L.n_uv = n_uv;
@@ -655,7 +655,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.s.band_bytes = c.gc_band_bytes;
             ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
-            if (8 * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
+            const int gcw = gc_waves(ga);
+            if (gcw * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.s.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
             const int ilds = c.gc_lds;
             double fl = 0, by = 0;
@@ -664,7 +665,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (const Branch& b : c.br) win += b.cin;
             by = 4.0 * B * c.hc * c.wc * (win + c.gc) * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
-            set_parts(2, 8 * ga.s.tiles_per_img);   // 8 waves per k_gc workgroup
+            set_parts(2, gcw * ga.s.tiles_per_img);   // one slot per k_gc wave
         } else {
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {

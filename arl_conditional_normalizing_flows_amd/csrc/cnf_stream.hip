@@ -275,8 +275,9 @@ namespace cnf {
 // 583-601) for the streamed layers — LN2(LeakyReLU(t1)) on the branch windows -> every branch's
 // dense 3x3 dilated conv -> t2 slices, plus the per-wave LN3 partials of LeakyReLU(t2).
 // ---------------------------------------------------------------------------------------------
-constexpr int GC_NW = 8;            // waves per k_gc workgroup
-constexpr int GC_NT = 64 * GC_NW;   // threads
+// waves / threads of the instantiation for table entry SID (-1: generic)
+#define GC_NWS (SID >= 0 ? GC_NW_SPEC : GC_NW_GEN)
+#define GC_NTS (64 * GC_NWS)
 
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
 #define GS(f) (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].f : a.s.f)
@@ -306,13 +307,14 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     }
     const bool vq = ((GS(out_cs) | br.out_off) & 3) == 0;
     const int nsub = (npx + 15) >> 4;
-    // two subtiles per wave and pass (s0, s0 + GC_NW) share every B read: two independent MFMA
+    // two subtiles per wave and pass (s0, s0 + NW) share every B read: two independent MFMA
     // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
     constexpr int GQ = 6;
     const int G = br.G;
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
-    for (int s0 = wave; s0 < nsub; s0 += 2 * GC_NW) {
-        const int s1 = s0 + GC_NW;
+    constexpr int NW = GC_NWS;   // (16 waves cover a 256-pixel tile in one pass: the pair's second half is dead code)
+    for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
+        const int s1 = s0 + NW;
         const bool v1 = s1 < nsub;
         const float* base[2];
 #pragma unroll
@@ -383,7 +385,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     }
 }
 
-constexpr int GC_GQ = 4;   // staged band quads per thread (the plan checks the total fits)
+#define GC_GQS (GC_STAGE_QUADS / GC_NTS)   // staged band quads per thread (the plan checks the total fits)
 
 // the branches of table entry SID, unrolled at compile time
 template <int SID, int BI>
@@ -415,7 +417,8 @@ __device__ long long g_gc_stamps[64];
 // MFMAs and written (LN2 + LeakyReLU applied) into the other buffer after them, so the staging
 // latency hides behind the compute; the tile's LN2 gamma/beta stay in registers for all images.
 template <int SID>
-__global__ __launch_bounds__(GC_NT, 1) void k_gc(GcArgs a) {
+__global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
+    constexpr int GC_NW = GC_NWS, GC_NT = GC_NTS, GC_GQ = GC_GQS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
     const int tile = blockIdx.x % GS(tiles_per_img);
@@ -585,7 +588,7 @@ template <int S>
 bool launch_gc_shape(int sid, const GcArgs& a, dim3 grid, int lds, hipStream_t st) {
     if constexpr (S < CNF_GC_NSHAPES) {
         if (sid == S) {
-            hipLaunchKernelGGL((k_gc<S>), grid, dim3(GC_NT), lds, st, a);
+            hipLaunchKernelGGL((k_gc<S>), grid, dim3(64 * GC_NW_SPEC), lds, st, a);
             return true;
         }
         return launch_gc_shape<S + 1>(sid, a, grid, lds, st);
@@ -595,17 +598,25 @@ bool launch_gc_shape(int sid, const GcArgs& a, dim3 grid, int lds, hipStream_t s
 
 int gc_num_shapes() { return CNF_GC_NSHAPES; }
 
-void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
+// table entry matching a's shape, -1 for the generic instantiation
+static int gc_shape_id(const GcArgs& a) {
     static const bool generic = [] {   // A/B knob: never the shape-specialised instantiations
         const char* e = std::getenv("CNF_GC_GENERIC");
         return e && std::atoi(e) != 0;
     }();
-    const dim3 grid(grid_x, 2);
     if (!generic)
         for (int sid = 0; sid < CNF_GC_NSHAPES; sid++)
-            if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0 && launch_gc_shape<0>(sid, a, grid, lds, st))
-                return;
-    hipLaunchKernelGGL((k_gc<-1>), grid, dim3(GC_NT), lds, st, a);
+            if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0) return sid;
+    return -1;
+}
+
+int gc_waves(const GcArgs& a) { return gc_shape_id(a) >= 0 ? GC_NW_SPEC : GC_NW_GEN; }
+
+void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
+    const dim3 grid(grid_x, 2);
+    const int sid = gc_shape_id(a);
+    if (sid >= 0 && launch_gc_shape<0>(sid, a, grid, lds, st)) return;
+    hipLaunchKernelGGL((k_gc<-1>), grid, dim3(64 * GC_NW_GEN), lds, st, a);
 }
 
 }  // namespace cnf
