@@ -50,6 +50,10 @@ struct ConvArgs {
     int H, W, TH, tiles_per_img, nprob, B;
     int P;     // 1x1 kernels: pixels per tile (tiles are runs of pixels inside one image)
     int ipw;   // k_pw: images per workgroup (looped, next image prefetched)
+    // k_pw tap mode (streamed conv_in): the A operand is the im2col row of a 3x3 conv over the
+    // mask-compressed half of the raw layer input u, gathered straight from u (no u1c tensor):
+    // K index k = tap * udc + c, c < udc, pixel shifted by the tap, zero outside the image
+    int umask, uW, uD, udc, uimg;   // mask, full-res width / depth, channels per tap, floats per image
 };
 
 struct CoupArgs {
@@ -180,17 +184,20 @@ void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int
 // k_pw launch shape: every launch-independent field a shape-specialised k_pw instantiation folds
 // in (cnf_stream.hip; table generated by gen_netlds_shapes.py from a dry run of the forward)
 struct PwShape {
-    int nr, gm, ln, res;                 // template selection
+    int nr, gm, ln, res, tap;            // template selection
     int H, W, tiles_per_img, nprob;
     int in_cs, in_off, cin, out_cs, out_off, cout, lds_w_off, part_stride;
+    int umask, uW, uD, udc, uimg;        // tap mode (0 otherwise)
     uint32_t st_mask_lo, st_mask_hi;
 };
 constexpr int PWSHAPE_WORDS = (int)(sizeof(PwShape) / 4);
 // the shape of a k_pw launch; false when its problems differ in a shape field
-inline bool pw_shape_of(int nr, int gm, bool ln, bool res, const ConvArgs& a, PwShape& s) {
+inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, PwShape& s) {
     const ConvProb& q = a.p[0];
-    s = PwShape{nr, gm, ln ? 1 : 0, res ? 1 : 0, a.H, a.W, a.tiles_per_img, a.nprob, q.in_cs, q.in_off, q.cin,
-                q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride, q.st_mask_lo, q.st_mask_hi};
+    s = PwShape{nr, gm, ln ? 1 : 0, res ? 1 : 0, tap ? 1 : 0, a.H, a.W, a.tiles_per_img, a.nprob, q.in_cs, q.in_off,
+                q.cin, q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride,
+                tap ? a.umask : 0, tap ? a.uW : 0, tap ? a.uD : 0, tap ? a.udc : 0, tap ? a.uimg : 0,
+                q.st_mask_lo, q.st_mask_hi};
     for (int i = 1; i < a.nprob; i++) {
         const ConvProb& r = a.p[i];
         if (r.in_cs != q.in_cs || r.in_off != q.in_off || r.cin != q.cin || r.out_cs != q.out_cs ||
@@ -200,7 +207,7 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, const ConvArgs& a, Pw
     }
     return true;
 }
-void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
+void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 int pw_num_shapes();
 int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS): [4 workgroups][16]   // shape-specialised k_pw instantiations compiled in
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);

@@ -533,6 +533,11 @@ Plan* build_plan(const cnf_flow_desc* d) {
                      [=](int n) { return cib + n; });
                 dense_img(np.ci, ks * ks, c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
                           [=](int n) { return cib + n; });
+                // streamed layers: conv_in for k_pw's tap mode, the HWIO kernel read as its
+                // [9*dc1][nk] im2col matrix (k = tap * dc1 + c)
+                if (!c.use_lds && ks == 3 && 9 * c.dc1 <= 128 && nk <= 64)
+                    pack(np.ci_pw, PK_1X1, 9 * c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
+                         [=](int n) { return cib + n; });
                 for (auto& rb : np.rb) {
                     const int64_t ak = rb.conv_a_k, ab = rb.conv_a_b, bk = rb.conv_b_k, bb = rb.conv_b_b;
                     pack(rb.ca, PK_1X1, nk, nk, [=](int ci2, int j) { return ak + (int64_t)ci2 * nk + j; },

@@ -51,6 +51,7 @@ struct NetParams {
     std::vector<RBParams> rb;
     int64_t ln_out_g = -1, ln_out_b = -1, conv_out_k = -1, conv_out_b = -1, tanh_w = -1;
     PackedConv ci, co;                         // conv_in (PK_KN), conv_out (PK_TAP or PK_KN)
+    PackedConv ci_pw;                          // streamed conv_in as a 1x1 over its 9*dc1 im2col row (PK_1X1; size 0: none)
     std::vector<PackedConv> co_chunks;         // streamed conv_out with > 64 outputs: 64-column PK_KN chunks
 };
 

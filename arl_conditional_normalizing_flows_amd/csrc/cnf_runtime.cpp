@@ -222,9 +222,15 @@ static uint32_t magic_for(int d, int64_t xmax) {
     return (uint32_t)((((uint64_t)1 << 32) + (uint64_t)d - 1) / (uint64_t)d);
 }
 
+// tap-mode source of a k_pw launch (streamed conv_in): the probs' `in` is the raw layer input u, the
+// A operand the 3x3 im2col row over the mask-compressed half (K = 9 * dc), gathered in the kernel
+struct TapSrc {
+    int mask, W, D, dc, img;   // mask, full-res width / depth, channels per tap, floats per image of u
+};
+
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
 static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
-                       uint64_t store_mask = ~0ull) {
+                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr) {
     if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
     ConvArgs a;
@@ -302,7 +308,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
             if (off < 512) off = 512;   // k_pw keeps its per-image LN table at bytes [256, 384)
             q.lds_w_off = (int)off;
             off = align_up(off + (size_t)G * 16 * 16 * q.nr * 4, 16);
-            if (s.cin % 4 || s.in_cs % 4 || s.in_off % 4) vec = false;
+            if (!tap && (s.cin % 4 || s.in_cs % 4 || s.in_off % 4)) vec = false;   // tap mode gathers scalars
             pw_nr = std::max(pw_nr, q.nr);
             pw_gm = std::max(pw_gm, G);
         }
@@ -311,7 +317,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         // output bytes count only the stored channels (conv_a stores just the grouped branches' inputs)
         const uint64_t cmask = s.cout >= 64 ? ~0ull : ((1ull << s.cout) - 1);
         const double stored = (double)__builtin_popcountll(store_mask & cmask);
-        bytes += 4.0 * (HWB * s.cin + HWB * (stored + (s.res ? s.cout : 0)) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
+        bytes += 4.0 * (HWB * (tap ? tap->dc : s.cin) + HWB * (stored + (s.res ? s.cout : 0)) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
                         (double)K * s.cout + s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
@@ -348,9 +354,17 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool lnf = probs[0].in_st.part != nullptr;
+        const bool tapf = tap != nullptr;
+        if (tap) {
+            a.umask = tap->mask;
+            a.uW = tap->W;
+            a.uD = tap->D;
+            a.udc = tap->dc;
+            a.uimg = tap->img;
+        }
         if (E.p.dry) {
             PwShape sh;
-            if (pw_shape_of(nr, gm, lnf, resf, a, sh)) {
+            if (pw_shape_of(nr, gm, lnf, resf, tapf, a, sh)) {
                 bool seen = false;
                 for (const PwShape& o : E.p.pw_shapes) seen = seen || std::memcmp(&o, &sh, sizeof(sh)) == 0;
                 if (!seen) E.p.pw_shapes.push_back(sh);
@@ -358,8 +372,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         }
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
                            role_name(role) + ">";
-        E.record(name, flops, bytes, [nr, gm, lnf, resf, a, grid_x, ilds](void* st) {
-            launch_pw(nr, gm, lnf, resf, a, grid_x, ilds, (hipStream_t)st);
+        E.record(name, flops, bytes, [nr, gm, lnf, resf, tapf, a, grid_x, ilds](void* st) {
+            launch_pw(nr, gm, lnf, resf, tapf, a, grid_x, ilds, (hipStream_t)st);
         });
         return nw * tiles;
     } else {
@@ -572,7 +586,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         E.record("k_net_lds", fl, by, [na, B, ilds](void* st) { launch_net_lds(na, B, ilds, (hipStream_t)st); });
     } else {
     float* u1c = E.at<float>(L.u1c);
-    {
+    // conv_in straight from u (k_pw tap mode: the mask gather inside the im2col loads) when packed
+    const bool cin_tap = E.p.use_pw && c.net[0].ci_pw.size > 0;
+    if (!cin_tap) {
         const float* uu = u;
         E.record("k_gather_u1c", 0, 4.0 * B * c.hc * c.wc * c.dc1 * 2,
                  [=](void* st) { launch_gather_u1c(uu, u1c, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, (hipStream_t)st); });
@@ -596,7 +612,16 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     const float* none = nullptr;
 
     // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
-    {
+    if (cin_tap) {
+        std::vector<ProbSpec> pr;
+        for (int n = 0; n < 2; n++) {
+            const NetParams& np = c.net[n];
+            pr.push_back(ProbSpec{u, 9 * c.dc1, 0, 9 * c.dc1, Slab{}, none, none, 0, X + np.ci_pw.w, X + np.ci_pw.b,
+                                  y[n], c.nk, 0, c.nk, none, out_slab(n, 0, 4 * nt1), 0, 1});
+        }
+        const TapSrc ts{c.mask, c.W, c.D, c.dc1, c.H * c.W * c.D};
+        set_parts(0, conv_launch(E, 1, ROLE_CONV_IN, c.hc, c.wc, pr, ~0ull, &ts));
+    } else {
         std::vector<ProbSpec> pr;
         for (int n = 0; n < 2; n++) {
             const NetParams& np = c.net[n];

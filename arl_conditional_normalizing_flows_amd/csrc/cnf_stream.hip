@@ -46,7 +46,7 @@ int read_pw_stamps(long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pw_stamps), sizeof(g_pw_stamps)) == hipSuccess ? 0 : -1;
 }
 
-template <int NR, int GM, bool LN, bool RES, int SID>
+template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false>
 __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
@@ -63,7 +63,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     float* lw = reinterpret_cast<float*>(smem + PP(lds_w_off));
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
-    const uint32_t in_img = (uint32_t)HW * PP(in_cs) * 4u, out_img = (uint32_t)HW * PP(out_cs) * 4u;
+    const uint32_t in_img = TAP ? (uint32_t)PA(uimg) * 4u : (uint32_t)HW * PP(in_cs) * 4u;
+    const uint32_t out_img = (uint32_t)HW * PP(out_cs) * 4u;
     const auto rin = buf_rsrc(P.in, (uint32_t)a.B * in_img);
     const auto rout = buf_rsrc(P.out, (uint32_t)a.B * out_img);
     const auto rres = buf_rsrc(RES ? P.res : P.out, (uint32_t)a.B * out_img);
@@ -90,10 +91,29 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // image activations (+ residual) in registers, one image ahead (two ahead measured slower)
     f4 x[GM];
     float rv[NR][4];
+    // tap mode: element k = 16g + 4kq + j of the lane's im2col row -> offset inside one image of u
+    auto toff = [&](int g, int j) -> uint32_t {
+        const int k = 16 * g + 4 * kq + j;
+        if (!pav || k >= cin) return BUF_OOB;
+        const int tap = k / PA(udc), c = k - tap * PA(udc);
+        const int pr = pa / PA(W) + tap / 3 - 1, pc = pa % PA(W) + tap % 3 - 1;
+        if ((unsigned)pr >= (unsigned)PA(H) || (unsigned)pc >= (unsigned)PA(W)) return BUF_OOB;
+        return (uint32_t)mask_pos(PA(umask), pr * PA(W) + pc, c, PA(W), PA(uW), PA(uD)) * 4u;
+    };
     auto load_img = [&](int ii, f4 (&xd)[GM], float (&rd)[NR][4]) {
         const uint32_t ib = (uint32_t)(img0 + ii) * in_img;
+        if constexpr (TAP) {
 #pragma unroll
-        for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
+            for (int g = 0; g < GM; g++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
+                    xd[g][j] = buf_load1(rin, o == BUF_OOB ? BUF_OOB : ib + o);
+                }
+        } else {
+#pragma unroll
+            for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
+        }
         if (RES) {
             const uint32_t ob = (uint32_t)(img0 + ii) * out_img;
 #pragma unroll
@@ -149,7 +169,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         for (int g = 0; g < GM; g++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const float v = lrelu(xc[g][j]);
+                const float v = TAP ? xc[g][j] : lrelu(xc[g][j]);   // conv_in reads raw u (no activation)
                 av[g][j] = LN ? fmaf(fmaf(v, rs, nmr), gm[g][j], bt[g][j]) : v;
             }
         }
@@ -232,7 +252,7 @@ bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStr
     if constexpr (S < CNF_PW_NSHAPES) {
         if (sid == S) {
             constexpr PwShape k = kPwShapes[S];
-            hipLaunchKernelGGL((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S>), g, b, lds, st, a);
+            hipLaunchKernelGGL((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S, k.tap != 0>), g, b, lds, st, a);
             return true;
         }
         return launch_pw_shape<S + 1>(sid, a, g, b, lds, st);
@@ -242,13 +262,26 @@ bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStr
 
 int pw_num_shapes() { return CNF_PW_NSHAPES; }
 
-void launch_pw(int nr, int gm, bool ln, bool res, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
+void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
     static const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob
     PwShape sh;
-    if (!generic && pw_shape_of(nr, gm, ln, res, a, sh))
+    if (!generic && pw_shape_of(nr, gm, ln, res, tap, a, sh))
         for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
             if (std::memcmp(&sh, &kPwShapes[sid], sizeof(sh)) == 0 && launch_pw_shape<0>(sid, a, g, b, lds, st)) return;
+    if (tap) {   // generic tap mode (streamed conv_in): no input LN, no residual
+        if (ln || res || gm > 8) throw std::invalid_argument("k_pw tap mode: no LN / residual, K <= 128");
+#define CNF_PW_TCASE(NR_, GM_)                                                          \
+        if (nr == NR_ && gm == GM_) {                                                   \
+            hipLaunchKernelGGL((k_pw<NR_, GM_, false, false, -1, true>), g, b, lds, st, a); \
+            return;                                                                     \
+        }
+#define CNF_PW_TNR(GM_) CNF_PW_TCASE(1, GM_) CNF_PW_TCASE(2, GM_) CNF_PW_TCASE(3, GM_) CNF_PW_TCASE(4, GM_)
+        CNF_PW_TNR(1) CNF_PW_TNR(2) CNF_PW_TNR(4) CNF_PW_TNR(8)
+#undef CNF_PW_TNR
+#undef CNF_PW_TCASE
+        throw std::invalid_argument("k_pw tap mode: no instantiation for this shape");
+    }
 #define CNF_PW_CASE(NR_, GM_, LN_, RES_)                                              \
     if (nr == NR_ && gm == GM_ && ln == LN_ && res == RES_) {                          \
         hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
