@@ -54,6 +54,9 @@ struct ConvArgs {
     // mask-compressed half of the raw layer input u, gathered straight from u (no u1c tensor):
     // K index k = tap * udc + c, c < udc, pixel shifted by the tap, zero outside the image
     int umask, uW, uD, udc, uimg;   // mask, full-res width / depth, channels per tap, floats per image
+    // umask < 0: the source is a plain NHWC tensor of the conv's own H x W (uD channels per pixel,
+    // taps from channel uoff, dilation udil; LN / LeakyReLU on load as the problem says)
+    int udil, uoff;
 };
 
 struct CoupArgs {
@@ -187,7 +190,7 @@ struct PwShape {
     int nr, gm, ln, res, tap;            // template selection
     int H, W, tiles_per_img, nprob;
     int in_cs, in_off, cin, out_cs, out_off, cout, lds_w_off, part_stride;
-    int umask, uW, uD, udc, uimg;        // tap mode (0 otherwise)
+    int umask, uW, uD, udc, uimg, udil, uoff;   // tap mode (0 otherwise)
     uint32_t st_mask_lo, st_mask_hi;
 };
 constexpr int PWSHAPE_WORDS = (int)(sizeof(PwShape) / 4);
@@ -197,6 +200,7 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvA
     s = PwShape{nr, gm, ln ? 1 : 0, res ? 1 : 0, tap ? 1 : 0, a.H, a.W, a.tiles_per_img, a.nprob, q.in_cs, q.in_off,
                 q.cin, q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride,
                 tap ? a.umask : 0, tap ? a.uW : 0, tap ? a.uD : 0, tap ? a.udc : 0, tap ? a.uimg : 0,
+                tap ? a.udil : 0, tap ? a.uoff : 0,
                 q.st_mask_lo, q.st_mask_hi};
     for (int i = 1; i < a.nprob; i++) {
         const ConvProb& r = a.p[i];

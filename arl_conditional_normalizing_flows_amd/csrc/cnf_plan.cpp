@@ -567,6 +567,16 @@ Plan* build_plan(const cnf_flow_desc* d) {
                              [=](int n) { return gb[n / b.width] + (n % b.width); });
                         dense_img(pc, ks * ks, b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gc.push_back(pc);
+                        // streamed layers without k_gc: the branch as k_pw's tap mode (a 1x1 over the
+                        // 9*cin im2col row, k = tap * cin + c) when the row fits (K <= 128)
+                        // (dilations >= 4 only: below that the staged band's halo is cheap and k_conv<3>'s
+                        // coalesced band loads beat the row's strided gathers)
+                        PackedConv pw;
+                        int tap_dmin = 4;
+                        if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin = std::atoi(e);   // tuning
+                        if (!c.use_lds && !c.gc_fused && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin)
+                            pack(pw, PK_1X1, 9 * b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
+                        rb.gpw.push_back(pw);
                     }
                     pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
                          [=](int n) { return bb + n; });

@@ -44,6 +44,7 @@ struct RBParams {
     int64_t ln3g = -1, ln3b = -1, conv_b_k = -1, conv_b_b = -1;
     PackedConv ca, cb;                         // conv_a, conv_b (PK_1X1)
     std::vector<PackedConv> gc;                // grouped branches as dense 3x3 convs (PK_KN)
+    std::vector<PackedConv> gpw;               // streamed, k_gc not fused: branch as a 1x1 over its 9*cin im2col row (size 0: none)
 };
 
 struct NetParams {

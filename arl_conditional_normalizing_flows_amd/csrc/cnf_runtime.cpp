@@ -115,6 +115,7 @@ WsLayout Plan::layout(int B) const {
         parts = std::max(parts, 4 * g.tiles * (int)c.br.size());   // 4 waves per workgroup
         parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
         parts = std::max(parts, 4 * ((c.hc * c.wc + 63) / 64));   // k_pw
+        parts = std::max(parts, (int)c.br.size() * std::max(4 * g.tiles, 4 * ((c.hc * c.wc + 63) / 64)));   // mixed branches
         if (c.gc_fused) parts = std::max(parts, GC_NW_MAX * ((c.hc + c.gc_TH - 1) / c.gc_TH));   // k_gc
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
@@ -226,6 +227,7 @@ static uint32_t magic_for(int d, int64_t xmax) {
 // A operand the 3x3 im2col row over the mask-compressed half (K = 9 * dc), gathered in the kernel
 struct TapSrc {
     int mask, W, D, dc, img;   // mask, full-res width / depth, channels per tap, floats per image of u
+    int dil = 1, off = 0;      // mask < 0: plain NHWC source (D channels), taps from channel off, dilation
 };
 
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
@@ -317,7 +319,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         // output bytes count only the stored channels (conv_a stores just the grouped branches' inputs)
         const uint64_t cmask = s.cout >= 64 ? ~0ull : ((1ull << s.cout) - 1);
         const double stored = (double)__builtin_popcountll(store_mask & cmask);
-        bytes += 4.0 * (HWB * (tap ? tap->dc : s.cin) + HWB * (stored + (s.res ? s.cout : 0)) + (s.in_st.part ? 2.0 * h * w * s.cin : 0.0) +
+        bytes += 4.0 * (HWB * (tap ? tap->dc : s.cin) + HWB * (stored + (s.res ? s.cout : 0)) +
+                        (s.in_st.part ? 2.0 * h * w * (tap ? tap->dc : s.cin) : 0.0) +
                         (double)K * s.cout + s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
@@ -346,7 +349,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         const int nw = 4;
         const int tiles = (h * w + 16 * nw - 1) / (16 * nw);
         a.tiles_per_img = tiles;
-        for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = 0;
+        for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = probs[i].out_part_base;
         const int64_t units = (int64_t)tiles * a.nprob * E.B;
         a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
         if (const char* e = std::getenv(resf ? "CNF_PW_IPW_RES" : "CNF_PW_IPW"))   // tuning override
@@ -361,6 +364,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
             a.uD = tap->D;
             a.udc = tap->dc;
             a.uimg = tap->img;
+            a.udil = tap->dil;
+            a.uoff = tap->off;
         }
         if (E.p.dry) {
             PwShape sh;
@@ -692,17 +697,43 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
             set_parts(2, gcw * ga.s.tiles_per_img);   // one slot per k_gc wave
         } else {
+            // branches whose im2col row fits k_pw (9 cin <= 128): tap-mode 1x1 over the row, gathered
+            // from t1 with LN2 on load (no staged band, so large dilations cost no halo); the rest
+            // as one k_conv<3> launch. Each launch's LN3 partial slots follow the previous ones'.
+            int base = 0;
             std::vector<ProbSpec> pr;
+            for (int bi = 0; bi < nbr; bi++) {
+                const Branch& b = c.br[bi];
+                if (!(E.p.use_pw && c.net[0].rb[r].gpw[bi].size > 0)) continue;
+                std::vector<ProbSpec> pt;
+                for (int n = 0; n < 2; n++) {
+                    const RBParams& rb = c.net[n].rb[r];
+                    pt.push_back(ProbSpec{t1[n], 9 * b.cin, 0, 9 * b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
+                                          ln ? P + rb.ln2b : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.gc,
+                                          b.out_off, b.cout, none, out_slab(n, 2, 0), base, 1});
+                }
+                TapSrc ts{-1, c.wc, c.nk, b.cin, c.hc * c.wc * c.nk};
+                ts.dil = b.dil;
+                ts.off = b.cin_off;
+                base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts);
+            }
+            int nrest = 0;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
+                int k = 0;
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
+                    if (E.p.use_pw && rb.gpw[bi].size > 0) continue;
                     pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
                                           ln ? P + rb.ln2b : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
-                                          b.out_off, b.cout, none, out_slab(n, 2, 4 * nt3 * nbr), bi * nt3 * 4, b.dil});
+                                          b.out_off, b.cout, none, out_slab(n, 2, 0), base + k * nt3 * 4, b.dil});
+                    k++;
                 }
+                nrest = k;
             }
-            set_parts(2, nbr * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr));
+            if (!pr.empty()) base += nrest * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
+            if (base > L.st_parts) throw std::runtime_error("grouped branches: LN partial slab too small");
+            set_parts(2, base);
         }
         // conv_b: LN3(LReLU(t2)) -> 1x1 -> + shortcut -> y (in place)
         {

@@ -96,20 +96,31 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         const int k = 16 * g + 4 * kq + j;
         if (!pav || k >= cin) return BUF_OOB;
         const int tap = k / PA(udc), c = k - tap * PA(udc);
-        const int pr = pa / PA(W) + tap / 3 - 1, pc = pa % PA(W) + tap % 3 - 1;
+        const int d = PA(udil);
+        const int pr = pa / PA(W) + (tap / 3 - 1) * d, pc = pa % PA(W) + (tap % 3 - 1) * d;
         if ((unsigned)pr >= (unsigned)PA(H) || (unsigned)pc >= (unsigned)PA(W)) return BUF_OOB;
+        if (PA(umask) < 0) return (uint32_t)((pr * PA(W) + pc) * PA(uD) + PA(uoff) + c) * 4u;
         return (uint32_t)mask_pos(PA(umask), pr * PA(W) + pc, c, PA(W), PA(uW), PA(uD)) * 4u;
     };
+    // plain-NHWC tap sources with quad-aligned channels: one 16-byte load per (tap, quad) (the
+    // row's channel quads never straddle two taps when cin % 4 == 0)
+    const bool tquad = TAP && PA(umask) < 0 && PA(udc) % 4 == 0 && PA(uoff) % 4 == 0 && PA(uD) % 4 == 0;
     auto load_img = [&](int ii, f4 (&xd)[GM], float (&rd)[NR][4]) {
         const uint32_t ib = (uint32_t)(img0 + ii) * in_img;
         if constexpr (TAP) {
 #pragma unroll
-            for (int g = 0; g < GM; g++)
+            for (int g = 0; g < GM; g++) {
+                if (tquad) {   // the lane's 4 elements are one channel quad of one tap's pixel
+                    const uint32_t o = g < G ? toff(g, 0) : BUF_OOB;
+                    xd[g] = buf_load4(rin, o == BUF_OOB ? BUF_OOB : ib + o);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
-                    xd[g][j] = buf_load1(rin, o == BUF_OOB ? BUF_OOB : ib + o);
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
+                        xd[g][j] = buf_load1(rin, o == BUF_OOB ? BUF_OOB : ib + o);
+                    }
                 }
+            }
         } else {
 #pragma unroll
             for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
@@ -131,9 +142,24 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
-            const uint32_t o = gok(g) ? aoff + 64u * g : BUF_OOB;   // 0 where masked: the normalised value is then exactly 0
-            gm[g] = buf_load4(rg, o);
-            bt[g] = buf_load4(rb, o);
+            if constexpr (TAP) {   // the lane's im2col row: gamma / beta of every tap's pixel (0 outside: zero padding)
+                if (tquad) {
+                    const uint32_t o = g < G ? toff(g, 0) : BUF_OOB;
+                    gm[g] = buf_load4(rg, o);
+                    bt[g] = buf_load4(rb, o);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
+                        gm[g][j] = buf_load1(rg, o);
+                        bt[g][j] = buf_load1(rb, o);
+                    }
+                }
+            } else {
+                const uint32_t o = gok(g) ? aoff + 64u * g : BUF_OOB;   // 0 where masked: the normalised value is then exactly 0
+                gm[g] = buf_load4(rg, o);
+                bt[g] = buf_load4(rb, o);
+            }
         }
     }
     float bias[NR];
@@ -141,7 +167,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     for (int n = 0; n < NR; n++) bias[n] = n * 16 + i16 < cout ? P.bias[n * 16 + i16] : 0.f;
 
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
-    int nwf = G * 16 * NSJ;
+    int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
     asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
     copy_to_lds<64 * NW>(P.wt, lw, nwf);
     if (LN) {
@@ -169,7 +195,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         for (int g = 0; g < GM; g++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const float v = TAP ? xc[g][j] : lrelu(xc[g][j]);   // conv_in reads raw u (no activation)
+                const float v = !TAP || P.act ? lrelu(xc[g][j]) : xc[g][j];   // conv_in reads raw u
                 av[g][j] = LN ? fmaf(fmaf(v, rs, nmr), gm[g][j], bt[g][j]) : v;
             }
         }
@@ -236,7 +262,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             }
         if (P.out_part != nullptr)
             ln_partial(vals, valid,
-                       P.out_part + ((size_t)img * PP(part_stride) + tile * NW + wave) * LNP);
+                       P.out_part + ((size_t)img * PP(part_stride) + P.out_part_base + tile * NW + wave) * LNP);
     };
     for (int ii = 0; ii < nimg; ii++) {
         step(ii, x, rv, ii + 1);
@@ -269,15 +295,16 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
     if (!generic && pw_shape_of(nr, gm, ln, res, tap, a, sh))
         for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
             if (std::memcmp(&sh, &kPwShapes[sid], sizeof(sh)) == 0 && launch_pw_shape<0>(sid, a, g, b, lds, st)) return;
-    if (tap) {   // generic tap mode (streamed conv_in): no input LN, no residual
-        if (ln || res || gm > 8) throw std::invalid_argument("k_pw tap mode: no LN / residual, K <= 128");
-#define CNF_PW_TCASE(NR_, GM_)                                                          \
-        if (nr == NR_ && gm == GM_) {                                                   \
-            hipLaunchKernelGGL((k_pw<NR_, GM_, false, false, -1, true>), g, b, lds, st, a); \
+    if (tap) {   // generic tap mode (streamed conv_in / grouped branches): no residual, K <= 128
+        if (res || gm > 8) throw std::invalid_argument("k_pw tap mode: no residual, K <= 128");
+#define CNF_PW_TCASE(NR_, GM_, LN_)                                                     \
+        if (nr == NR_ && gm == GM_ && ln == LN_) {                                      \
+            hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, false, -1, true>), g, b, lds, st, a); \
             return;                                                                     \
         }
-#define CNF_PW_TNR(GM_) CNF_PW_TCASE(1, GM_) CNF_PW_TCASE(2, GM_) CNF_PW_TCASE(3, GM_) CNF_PW_TCASE(4, GM_)
-        CNF_PW_TNR(1) CNF_PW_TNR(2) CNF_PW_TNR(4) CNF_PW_TNR(8)
+#define CNF_PW_TNR(GM_, LN_) CNF_PW_TCASE(1, GM_, LN_) CNF_PW_TCASE(2, GM_, LN_) CNF_PW_TCASE(3, GM_, LN_) CNF_PW_TCASE(4, GM_, LN_)
+        CNF_PW_TNR(1, false) CNF_PW_TNR(2, false) CNF_PW_TNR(4, false) CNF_PW_TNR(8, false)
+        CNF_PW_TNR(1, true) CNF_PW_TNR(2, true) CNF_PW_TNR(4, true) CNF_PW_TNR(8, true)
 #undef CNF_PW_TNR
 #undef CNF_PW_TCASE
         throw std::invalid_argument("k_pw tap mode: no instantiation for this shape");

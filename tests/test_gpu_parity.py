@@ -14,14 +14,21 @@ RTOL = 1e-5
 
 
 def _setup(name, B, group_mode='reference', seed=0, netlds=True):
+    """netlds: True / False (CNF_NETLDS), or 'nogc' = streamed layers without the fused k_gc stage
+    (CNF_GC=0: the grouped branches run as k_pw tap-mode launches over their im2col rows)"""
     import os
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
-    os.environ['CNF_NETLDS'] = '1' if netlds else '0'
+    os.environ['CNF_NETLDS'] = '0' if netlds is False else '1'
+    if netlds == 'nogc':
+        os.environ['CNF_GC'] = '0'
     cfg = PRESETS[name]
     kw = cfg.kwargs()
     kw['group_mode'] = group_mode
-    flow = cFlow(**kw)
-    os.environ.pop('CNF_NETLDS', None)
+    try:
+        flow = cFlow(**kw)
+    finally:
+        os.environ.pop('CNF_NETLDS', None)
+        os.environ.pop('CNF_GC', None)
     ora = OracleCFlow(**kw)
     P = ora.init_params(seed)
     flow.set_weights(P)
@@ -51,6 +58,8 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          # (group_mode='intended' on streamed layers needs the dense grouped image in LDS: small only)
          ('small', 3, 'reference', False), ('small', 2, 'intended', False), ('cfg2', 2, 'reference', False),
          ('ref_default', 2, 'reference', False),
+         # streamed grouped branches as k_pw tap-mode launches (no fused k_gc)
+         ('cfg2', 2, 'reference', 'nogc'),
          # BASELINE configs[3] / configs[4] architectures (64x64 4-scale, 128x128 5-scale) at a small batch
          ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True)]
 
