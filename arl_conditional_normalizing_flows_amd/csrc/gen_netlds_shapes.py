@@ -24,7 +24,7 @@ sys.path.insert(0, str(ROOT))
 from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
 from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 
-SPECIALISE = ('cfg2', 'cfg3')   # the benchmark configuration (BASELINE.json configs[1]) and configs[2]
+SPECIALISE = ('cfg2', 'cfg3', 'ref_default')   # BASELINE.json configs[1] (the benchmark), configs[2], the reference's default
 OUT = HERE / 'cnf_netlds_shapes.inc'
 OUT_GC = HERE / 'cnf_gc_shapes.inc'
 OUT_PW = HERE / 'cnf_pw_shapes.inc'
