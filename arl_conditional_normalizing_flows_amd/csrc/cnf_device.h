@@ -20,6 +20,22 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
 __device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
 
+// tanh and exp of the affine coupling law (s = w * tanh(A), exp(s): conv_cINN_make_model.py:1198-1205,
+// 1215-1253) on the hardware exp (v_exp_f32): an odd Taylor polynomial below |x| = 1/4 (truncation
+// < 1e-8 relative), 1 - 2 / (e^{2|x|} + 1) above (< 1e-6 relative). k_coupling, the deferred coupling
+// in k_net_lds and the coupling backward all use these, so their results agree bit for bit.
+__device__ __forceinline__ float cpl_tanh(float x) {
+    const float ax = fabsf(x);
+    if (ax < 0.25f) {
+        const float x2 = x * x;
+        const float p = fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, 62.f / 2835.f, -17.f / 315.f), 2.f / 15.f), -1.f / 3.f), 1.f);
+        return x * p;
+    }
+    const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * ax) + 1.f);   // e^{2|x|} = inf -> 1
+    return copysignf(t, x);
+}
+__device__ __forceinline__ float cpl_exp(float s) { return __expf(s); }
+
 // Wave-wide fp32 sum by DPP lane moves (quad_perm, row_shr, row_bcast: a few cycles each instead
 // of an LDS-routed ds_bpermute per step); lane 63 ends with the total, broadcast by readlane.
 // Out-of-range source lanes read 0 (update_dpp with old = 0). Fixed order: bitwise reproducible.

@@ -87,6 +87,25 @@ struct LdsConv {
     int fmt, size, kpad, ns;
 };
 
+// A coupling law left pending by the previous layer (forward only): k_net_lds of layer k+1 applies
+// layer k's affine law itself (conv_cINN_make_model.py:1215-1233, 1258-1328) — on the fly in its u1c
+// gather, and for the whole v_k (split between its two workgroups) with layer k's log-det partials —
+// so layer k needs no k_coupling launch. Same arithmetic as k_coupling, element for element.
+struct CoupPend {
+    const float* u = nullptr;       // u_k [B][H][W][D] (layer k's input; H, W, D as layer k+1's)
+    const float* s_pre = nullptr;   // layer k's raw net-A conv_out (pre-tanh) [B][hc][wc][dc2]
+    const float* t = nullptr;       // layer k's net-b conv_out
+    const float* tanh_w = nullptr;  // layer k's tanh scale
+    float* v = nullptr;             // v_k (== layer k+1's u)
+    double* ld_part = nullptr;      // layer k's log-det partial slots [B][np]
+    int mask_c = 0, hc = 0, wc = 0, dc2 = 0, np = 0, on = 0;
+    // comp: layer k+1 conditions on exactly layer k's transformed half (mask_{k+1} == layer k's
+    // complement mask, same compressed layout): its u1c gather then yields that half of v_k as is
+    // (net A's workgroup stores it with the log-det sum), and net b's copies the other half (layer
+    // k's conditioning half, mask / dc1) from u_k — no pass over v_k at the end of the kernel
+    int comp = 0, mask = 0, dc1 = 0;
+};
+
 struct NetLdsArgs {
     const float* u;           // layer input [B][H][W][D]
     float* so[2];             // outputs: raw conv_out of net A (pre-tanh) / net b, [B][hc][wc][dc2]
@@ -105,6 +124,7 @@ struct NetLdsArgs {
     int off_ks;                                  // K-split partial buffers (0: the image has > 4 subtiles)
     int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
     int stamp_off;                               // diagnostic stamp builds: LDS byte offset of the stamp array
+    CoupPend pend;                               // previous layer's deferred coupling (pend.on)
 };
 // The launch-independent "shape" of a k_net_lds launch as int words: [offs_per_net, zero_bias) and
 // [off_y, stamp_off) of NetLdsArgs (the mask word inside is not part of it). Shape-specialised
@@ -222,6 +242,23 @@ void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st);
 void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
                         int B, hipStream_t st);
+// two independent index maps (+ optionally the per-image log-det reduction) in one launch:
+// dst[b, didx ? didx[i] : i] = src[b, sidx ? sidx[i] : i] (a gather has didx == null, a scatter sidx
+// == null or a source map). The forward's factor boundaries (keep gather + factored scatter) and its
+// tail (final scatter + log-det reduction) each take one launch instead of two.
+struct MapOp {
+    const float* src = nullptr;
+    float* dst = nullptr;
+    const int* sidx = nullptr;
+    const int* didx = nullptr;
+    int n = 0, ss = 0, ds = 0;
+};
+struct LdReduce {
+    const double* part = nullptr;   // null: no reduction
+    float* out = nullptr;
+    int nl = 0, np = 0, accumulate = 0;
+};
+void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, int B, hipStream_t st);
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st);
 void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
                    hipStream_t st);

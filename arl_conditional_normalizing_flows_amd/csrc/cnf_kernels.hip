@@ -501,14 +501,14 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
                 sp = sb[e];
                 t = tb[e];
             }
-            const float s = w * tanhf(sp);
+            const float s = w * cpl_tanh(sp);
             const float x = ub[q];
             float y;
             if (a.dir > 0) {
-                y = expf(s) * x + t;
+                y = fmaf(cpl_exp(s), x, t);   // (k_net_lds applies a deferred coupling with the same expression)
                 lsum += s;
             } else {
-                y = (1.0f / expf(s)) * (x - t);
+                y = (1.0f / cpl_exp(s)) * (x - t);
             }
             vb[q] = y;
         } else {
@@ -528,18 +528,26 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
     }
 }
 
-// out[img] (=|+=) sum over nl layers, np parts of part[((l*B)+img)*np + j]
-__global__ void k_ld_reduce(const double* __restrict__ part, float* __restrict__ out, int B, int nl, int np,
-                            int accumulate) {
-    const int img = blockIdx.x * blockDim.x + threadIdx.x;
-    if (img >= B) return;
+// out[img] (=|+=) sum over nl layers, np parts of part[((l*B)+img)*np + j]: one wave per image,
+// lane k folds entries k, k+64, ... (all its loads in flight together), then a fixed-order wave sum
+__global__ __launch_bounds__(64) void k_ld_reduce(const double* __restrict__ part, float* __restrict__ out, int B,
+                                                  int nl, int np, int accumulate) {
+    const int img = blockIdx.x, lane = threadIdx.x;
+    const int n = nl * np;
     double s = 0.0;
-    for (int l = 0; l < nl; l++)
-        for (int j = 0; j < np; j++) s += part[((size_t)l * B + img) * np + j];
-    if (accumulate)
-        out[img] = (float)((double)out[img] + s);
-    else
-        out[img] = (float)s;
+    for (int k0 = 0; k0 < n; k0 += 256) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + 64 * u + lane;
+            const int l = k / np, j = k - l * np;
+            v[u] = k < n ? part[((size_t)l * B + img) * np + j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) s += v[u];
+    }
+    s = wave_sum(s);
+    if (lane == 0) out[img] = accumulate ? (float)((double)out[img] + s) : (float)s;
 }
 
 // dst[b, i] = src[b, idx[i]]
@@ -560,6 +568,39 @@ __global__ __launch_bounds__(256) void k_map_scatter(const float* __restrict__ s
         int s = sidx ? sidx[i] : i;
         dst[(size_t)img * dst_stride + didx[i]] = src[(size_t)img * src_stride + s];
     }
+}
+
+// blocks [0, ga): map a; [ga, ga + gb): map b; block ga + gb (when r.part): the log-det reduction
+// of image blockIdx.y (as k_ld_reduce, by wave 0)
+__global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, LdReduce r, int B) {
+    const int img = blockIdx.y;
+    const int bx = blockIdx.x;
+    if (bx < ga + gb) {
+        const MapOp& m = bx < ga ? a : b;
+        const int g0 = bx < ga ? 0 : ga, gn = bx < ga ? ga : gb;
+        for (int i = (bx - g0) * 256 + threadIdx.x; i < m.n; i += gn * 256) {
+            const int s = m.sidx ? m.sidx[i] : i;
+            const int d = m.didx ? m.didx[i] : i;
+            m.dst[(size_t)img * m.ds + d] = m.src[(size_t)img * m.ss + s];
+        }
+        return;
+    }
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x, n = r.nl * r.np;
+    double acc = 0.0;
+    for (int k0 = 0; k0 < n; k0 += 256) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + 64 * u + lane;
+            const int l = k / r.np, j = k - l * r.np;
+            v[u] = k < n ? r.part[((size_t)l * B + img) * r.np + j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc += v[u];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) r.out[img] = r.accumulate ? (float)((double)r.out[img] + acc) : (float)acc;
 }
 
 // dir=+1: out[b,i,j,(di*2+dj)*C+c] = in[b,2i+di,2j+dj,c] (in: H x W x C)
@@ -614,14 +655,26 @@ __global__ __launch_bounds__(256) void k_nll(const float* __restrict__ xy, const
     const int img = blockIdx.x;
     const float* xb = xy + (size_t)img * HW * D;
     const float* zb = zy + (size_t)img * HW * D;
+    const int n = HW * D;
     double zz = 0.0, ya = 0.0;
-    for (int e = threadIdx.x; e < HW * D; e += 256) {
-        int c = e % D;
-        float z = zb[e];
-        if (c < x_d)
-            zz += (double)(z * z);
-        else
-            ya += (double)fabsf(z - xb[e]);
+    // 8 elements per thread and pass, every load issued before the first use
+    for (int e0 = threadIdx.x; e0 < n; e0 += 8 * 256) {
+        float z[8], x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = e0 + 256 * u;
+            z[u] = e < n ? zb[e] : 0.f;
+            x[u] = e < n && e % D >= x_d ? xb[e] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = e0 + 256 * u;
+            if (e >= n) continue;
+            if (e % D < x_d)
+                zz += (double)(z[u] * z[u]);
+            else
+                ya += (double)fabsf(z[u] - x[u]);
+        }
     }
     __shared__ double s1[4], s2[4];
     double a = wave_sum(zz), b = wave_sum(ya);
@@ -724,7 +777,7 @@ void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
 }
 
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(k_ld_reduce, dim3((B + 63) / 64), dim3(64), 0, st, part, out, B, nl, np, accumulate);
+    hipLaunchKernelGGL(k_ld_reduce, dim3(B), dim3(64), 0, st, part, out, B, nl, np, accumulate);
 }
 
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st) {
@@ -738,6 +791,14 @@ void launch_map_scatter(const float* src, float* dst, const int* sidx, const int
     int gx = (n + 255) / 256;
     if (gx > 64) gx = 64;
     hipLaunchKernelGGL(k_map_scatter, dim3(gx, B), dim3(256), 0, st, src, dst, sidx, didx, n, ss, ds);
+}
+
+void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, int B, hipStream_t st) {
+    auto gx = [](int n) { return n <= 0 ? 0 : (n + 255) / 256 > 64 ? 64 : (n + 255) / 256; };
+    const int ga = gx(a.n), gb = gx(b.n);
+    const int g = ga + gb + (r.part ? 1 : 0);
+    if (g == 0) return;
+    hipLaunchKernelGGL(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, B);
 }
 
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st) {

@@ -817,6 +817,20 @@ __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int
     return (pr * W + pc) * D + ch;
 }
 
+// compressed index (p * dc2 + c) in layer k's transformed half of element pos of u_k, or -1 when pos
+// lies in its conditioning half: the inverse of mask_pos_ for the complement mask q.mask_c
+__device__ __forceinline__ int pend_index(const CoupPend& q, int pos, int W, int D) {
+    const int pix = pos / D, ch = pos - pix * D;
+    const int y = pix / W, x = pix - y * W;
+    if (q.mask_c < 2) {   // checkerboard: c0 -> (even, even) / (even, odd), c1 -> (odd, odd) / (odd, even)
+        const int half = y & 1;
+        if (((x & 1) == half) != (q.mask_c == 0)) return -1;
+        return ((y >> 1) * q.wc + (x >> 1)) * q.dc2 + half * D + ch;
+    }
+    if ((ch & 1) != (q.mask_c == 3 ? 1 : 0)) return -1;   // channels 0::2 / 1::2
+    return pix * q.dc2 + (ch >> 1);
+}
+
 }  // namespace
 
 // Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs):
@@ -856,7 +870,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const float* X = a.aux;
     // this net's parameter-offset table (see NetLdsArgs) copied to LDS [192, ...): every later read
     // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
-    static_assert(NW * 4 * 4 <= NETLDS_OTAB, "LN slots overlap the offset table");
+    static_assert(NW * 4 * 4 + NW * 8 <= NETLDS_OTAB, "LN slots + log-det scratch overlap the offset table");
     int* otab = reinterpret_cast<int*>(smem + NETLDS_OTAB);
     for (int i = threadIdx.x; i < SA(offs_per_net); i += NT) otab[i] = a.offs[net * SA(offs_per_net) + i];
     // 16 zero bytes right below Y: the source of every 3x3 tap quad outside the image
@@ -895,12 +909,69 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     };
     wpf_load(pf, X + off[0], wb(SA(ci), nk));
     // gather u1c (mask compress) into T2 (stride SU)
-    {
+    if (a.pend.on == 0) {
         const float* ub = a.u + (size_t)img * SA(H) * SA(W) * SA(D);
         const int n = HW * SA(dc1);
         for (int e = threadIdx.x; e < n; e += NT) {
             const int p = e / SA(dc1), c = e - p * SA(dc1);
             T2[p * SU + c] = ub[mask_pos_(a.mask, p, c, W, SA(W), SA(D))];
+        }
+    } else if (a.pend.comp != 0) {
+        // the previous layer's coupling law is still pending and this layer conditions on exactly
+        // its transformed half: the gather computes v2c_k itself; net A's workgroup stores it into
+        // v_k and sums its s (layer k's log-det), net b's copies v_k's other half from u_k
+        const CoupPend& q = a.pend;
+        const int n_img = SA(H) * SA(W) * SA(D);
+        const float* ub = q.u + (size_t)img * n_img;
+        float* vb = q.v + (size_t)img * n_img;
+        const size_t sb = (size_t)img * HW * SA(dc1);
+        const float w = *q.tanh_w;
+        const int n = HW * SA(dc1);
+        float lsum = 0.f;
+        for (int e = threadIdx.x; e < n; e += NT) {
+            const int p = e / SA(dc1), c = e - p * SA(dc1);
+            const int pos = mask_pos_(a.mask, p, c, W, SA(W), SA(D));
+            const float s = w * cpl_tanh(q.s_pre[sb + e]);
+            const float val = fmaf(cpl_exp(s), ub[pos], q.t[sb + e]);   // k_coupling's expression, bit for bit
+            T2[p * SU + c] = val;
+            if (net == 0) {
+                vb[pos] = val;
+                lsum += s;
+            }
+        }
+        if (net == 1) {
+            const int n1 = HW * q.dc1;
+            for (int e = threadIdx.x; e < n1; e += NT) {
+                const int p = e / q.dc1, c = e - p * q.dc1;
+                const int pos = mask_pos_(q.mask, p, c, W, SA(W), SA(D));
+                vb[pos] = ub[pos];
+            }
+        } else {
+            // wave sums -> LDS scratch [NW * 16, NW * 24); thread 0 folds them after conv_in's barrier
+            const double ws = wave_sum((double)lsum);
+            if ((threadIdx.x & 63) == 0) reinterpret_cast<double*>(smem + NW * 16)[threadIdx.x >> 6] = ws;
+        }
+    } else {
+        // the previous layer's coupling law is still pending: u = v_k is computed here from u_k and
+        // layer k's s, t — on the fly for the gathered half; the whole v_k (elements split between
+        // the two workgroups) and layer k's log-det partial slots at the end of the kernel
+        const CoupPend& q = a.pend;
+        const int n_img = SA(H) * SA(W) * SA(D);
+        const float* ub = q.u + (size_t)img * n_img;
+        const size_t sb = (size_t)img * q.hc * q.wc * q.dc2;
+        const float w = *q.tanh_w;
+        auto coupled = [&](int pos, float& s) {
+            const int ci = pend_index(q, pos, SA(W), SA(D));
+            const float x = ub[pos];
+            if (ci < 0) return x;
+            s = w * cpl_tanh(q.s_pre[sb + ci]);
+            return fmaf(cpl_exp(s), x, q.t[sb + ci]);   // k_coupling's expression, bit for bit
+        };
+        const int n = HW * SA(dc1);
+        for (int e = threadIdx.x; e < n; e += NT) {
+            const int p = e / SA(dc1), c = e - p * SA(dc1);
+            float s = 0.f;
+            T2[p * SU + c] = coupled(mask_pos_(a.mask, p, c, W, SA(W), SA(D)), s);
         }
     }
     // conv_in (3x3, dc1 -> nk) -> Y, LN stats of Y
@@ -909,6 +980,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         wpf_store(pf, WL, X + off[0]);
         lst_reset(st);
         lds_barrier();
+        if (a.pend.comp != 0 && net == 0 && threadIdx.x == 0) {   // layer k's log-det partial slots
+            const double* ws = reinterpret_cast<const double*>(smem + NW * 16);
+            double t = 0.0;
+            for (int i = 0; i < NW; i++) t += ws[i];
+            double* dst = a.pend.ld_part + (size_t)img * a.pend.np;
+            dst[0] = t;
+            for (int j = 1; j < a.pend.np; j++) dst[j] = 0.0;
+        }
         if (SA(R) > 0)
             wpf_load(pf, X + rbo(0)[2], wb(SA(ca), nk));
         else
@@ -1104,6 +1183,49 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
                 dst[e] = T2[p * S2 + c];
             }
         }
+    }
+    if (a.pend.on != 0 && a.pend.comp == 0) {
+        // the deferred coupling's v_k and log-det partials (after conv_out: its loads and stores
+        // then add to the kernel's tail instead of delaying conv_in)
+        const CoupPend& q = a.pend;
+        const int n_img = SA(H) * SA(W) * SA(D);
+        const float* ub = q.u + (size_t)img * n_img;
+        const size_t sb = (size_t)img * q.hc * q.wc * q.dc2;
+        const float w = *q.tanh_w;
+        auto coupled = [&](int pos, float& s) {
+            const int ci = pend_index(q, pos, SA(W), SA(D));
+            const float x = ub[pos];
+            if (ci < 0) return x;
+            s = w * cpl_tanh(q.s_pre[sb + ci]);
+            return fmaf(cpl_exp(s), x, q.t[sb + ci]);
+        };
+        const bool split = q.np >= 2;
+        const int e0 = split && net == 1 ? n_img / 2 : 0, e1 = split && net == 0 ? n_img / 2 : n_img;
+        float lsum = 0.f;
+        if (!split && net == 1) {
+            // (one slot per image: net A's workgroup writes the whole v_k)
+        } else {
+            float* vb = q.v + (size_t)img * n_img;
+            for (int e = e0 + (int)threadIdx.x; e < e1; e += NT) {
+                float s = 0.f;
+                vb[e] = coupled(e, s);
+                lsum += s;
+            }
+        }
+        lds_barrier();   // (lst_final's reads of the LN slots are done)
+        double* lsl = reinterpret_cast<double*>(slots);   // NW doubles (LN slots: free after conv_out)
+        const double ws = wave_sum((double)lsum);
+        if ((threadIdx.x & 63) == 0) lsl[threadIdx.x >> 6] = ws;
+        lds_barrier();
+        if (threadIdx.x == 0 && (split || net == 0)) {
+            double t = 0.0;
+            for (int i = 0; i < NW; i++) t += lsl[i];
+            double* dst = q.ld_part + (size_t)img * q.np;
+            dst[net] = t;
+            if (net == 0)
+                for (int j = 2; j < q.np; j++) dst[j] = 0.0;
+        }
+        lds_barrier();
     }
     STAMP(sti++);
     if (STAMPS && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {

@@ -126,6 +126,7 @@ struct Recorded {
 struct WsLayout {
     size_t total = 0;
     size_t uv[2] = {0, 0}, u1c = 0, y[2] = {0, 0}, t1[2] = {0, 0}, t2[2] = {0, 0}, so[2] = {0, 0};
+    size_t so_alt[2] = {0, 0};   // k_net_lds layers of odd index write s/t here (a deferred coupling reads the other set)
     size_t st_part[2][3] = {};   // LN partials [net][y, t1, t2]
     size_t ld = 0;
     int64_t n_uv = 0, n_u1c = 0, n_y = 0, n_t2 = 0, n_so = 0;

@@ -98,7 +98,9 @@ static ConvGeom1 conv1_geo(int h, int w) {
     return g;
 }
 
-static int ld_parts_for(int npx) { return std::max(1, std::min(16, (npx + 255) / 256)); }
+// log-det partial slots (= k_coupling workgroups) per image: one per 64 compressed pixels, so the
+// largest layers run one element per thread (latency-bound otherwise)
+static int ld_parts_for(int npx) { return std::max(1, std::min(16, (npx + 63) / 64)); }
 
 WsLayout Plan::layout(int B) const {
     WsLayout L;
@@ -141,6 +143,7 @@ WsLayout Plan::layout(int B) const {
         L.t1[n] = take(Bz * n_y * 4);
         L.t2[n] = take(Bz * n_t2 * 4);
         L.so[n] = take(Bz * n_so * 4);
+        L.so_alt[n] = take(Bz * n_so * 4);
         for (int k = 0; k < 3; k++) {   // LN slabs y, t1, t2: per-wave partials
             L.st_part[n][k] = take(Bz * parts * LNP * 4);
         }
@@ -554,7 +557,12 @@ static double net_flops(const Coupling& c) {
 }
 
 // One coupling layer: u -> v. dir=+1 forward (ld_part may collect Σs), dir=-1 inverse.
-static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir) {
+// pend: the previous layer's deferred coupling, applied by this layer's k_net_lds (forward, LDS
+// layers only). defer: leave this layer's own coupling pending (no k_coupling launch) and describe it
+// in *out_pend for the next layer's k_net_lds (the caller allows it only when that layer is an LDS
+// layer of the same forward).
+static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir,
+                         const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr) {
     const int B = E.B;
     const WsLayout& L = E.L;
     const float* P = E.params;
@@ -563,8 +571,13 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     const int nt1 = conv1_geo(c.hc, c.wc).tiles;    // ... by a 1x1 launch
     const int nbr = (int)c.br.size();
     const bool ln = E.p.desc.layer_norm != 0;
-    float* so0 = E.at<float>(L.so[0]);
-    float* so1 = E.at<float>(L.so[1]);
+    // k_net_lds layers alternate between two s/t sets by coupling index, so a layer applying its
+    // predecessor's deferred coupling never writes the set it reads
+    const bool alt = c.use_lds && (c.index & 1) != 0;
+    float* so0 = E.at<float>(alt ? L.so_alt[0] : L.so[0]);
+    float* so1 = E.at<float>(alt ? L.so_alt[1] : L.so[1]);
+    if ((pend != nullptr || defer) && (!c.use_lds || dir <= 0))
+        throw std::logic_error("deferred couplings are only fused into forward k_net_lds layers");
     const float* tap_c[2] = {nullptr, nullptr};   // streamed tap-GEMM conv_out (finished in k_coupling)
     const float* tap_b[2] = {nullptr, nullptr};
     NetLdsArgs na;
@@ -578,6 +591,10 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.aux = X;
         na.offs = E.p.dev_table + c.dev_lds_offs;
         na.zero_bias = X + E.p.aux_zero;
+        if (pend != nullptr) {
+            na.pend = *pend;
+            na.pend.comp = pend->mask_c == c.mask && pend->hc == c.hc && pend->wc == c.wc && pend->dc2 == c.dc1 ? 1 : 0;
+        }
         const int ilds = (int)nlds;
         const double fl = 2.0 * B * net_flops(c);
         // algorithmic bytes: u1c in and s/t out per image and net, plus the per-element LN
@@ -785,6 +802,25 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     }
     }  // streamed path
     // affine coupling law + decompress + log-det partials
+    if (defer) {
+        CoupPend& q = *out_pend;
+        q = CoupPend{};
+        q.u = u;
+        q.s_pre = so0;
+        q.t = so1;
+        q.tanh_w = P + c.net[0].tanh_w;
+        q.v = v;
+        q.ld_part = ld_part;
+        q.mask_c = c.mask_c;
+        q.hc = c.hc;
+        q.wc = c.wc;
+        q.dc2 = c.dc2;
+        q.np = E.L.ld_parts;
+        q.on = 1;
+        q.mask = c.mask;
+        q.dc1 = c.dc1;
+        return;
+    }
     {
         CoupArgs ca;
         ca.u = u;
@@ -966,9 +1002,20 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     int which = 0;
     size_t bi = 0;
     const int nuv = (int)L.n_uv;
-    for (const Layer& ly : p.layers) {
+    // a k_net_lds layer followed directly by another one leaves its coupling law to that layer's
+    // kernel (CoupPend): no k_coupling launch for it. Not when saving layer inputs (training).
+    static const bool fuse = [] {   // A/B knob
+        const char* e = std::getenv("CNF_FUSE_COUPLING");
+        return !(e && std::atoi(e) == 0);
+    }();
+    CoupPend pend;
+    bool have_pend = false;
+    for (size_t li = 0; li < p.layers.size(); li++) {
+        const Layer& ly = p.layers[li];
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
+            const bool defer = fuse && !save_inputs && c.use_lds && li + 1 < p.layers.size() &&
+                               p.layers[li + 1].kind == CNF_LAYER_COUPLING && p.couplings[p.layers[li + 1].ci].use_lds;
             float* nxt = buf[which];
             if (save_inputs) {
                 float* dst = E.at<float>(TL.save_u[c.index]);
@@ -978,7 +1025,11 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
                     (void)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)st);
                 });
             }
-            run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1);
+            CoupPend next;
+            run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1, have_pend ? &pend : nullptr,
+                         defer, &next);
+            pend = next;
+            have_pend = defer;
             cur = nxt;
             which ^= 1;
         } else if (ly.kind == CNF_LAYER_FACTOR) {
@@ -992,27 +1043,24 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             const int* ks = T + b.dev_keep_src;
             const int* fs = T + b.dev_fac_src;
             const int* fo = T + b.dev_fac_orig;
-            E.record("k_map_gather", 0, 8.0 * B * nnext, [=](void* st) {
-                launch_map_gather(src, nxt, ks, nnext, ncur, nnext, B, (hipStream_t)st);
-            });
-            E.record("k_map_scatter", 0, 8.0 * B * nfac, [=](void* st) {
-                launch_map_scatter(src, zy, fs, fo, nfac, ncur, nuv, B, (hipStream_t)st);
-            });
+            // keep gather -> next buffer and factored scatter -> zy: one launch
+            MapOp mk, mf;
+            mk.src = src, mk.dst = nxt, mk.sidx = ks, mk.n = nnext, mk.ss = ncur, mk.ds = nnext;
+            mf.src = src, mf.dst = zy, mf.sidx = fs, mf.didx = fo, mf.n = nfac, mf.ss = ncur, mf.ds = nuv;
+            E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
+                     [=](void* st) { launch_map2(mk, mf, LdReduce{}, B, (hipStream_t)st); });
             cur = nxt;
             which ^= 1;
         }
     }
     {
-        const int* T = p.dev_table;
-        const int off = p.dev_final_orig, n = p.last_n;
-        const float* src = cur;
-        E.record("k_map_scatter", 0, 8.0 * B * n, [=](void* st) {
-            launch_map_scatter(src, zy, nullptr, T + off, n, n, nuv, B, (hipStream_t)st);
-        });
-    }
-    {
-        const int nl = (int)p.couplings.size(), np = L.ld_parts;
-        E.record("k_ld_reduce", 0, 0, [=](void* st) { launch_ld_reduce(ld, logdet_per_image, B, nl, np, 0, (hipStream_t)st); });
+        // final scatter (restore to xy's layout) and the per-image log-det reduction: one launch
+        MapOp mf;
+        mf.src = cur, mf.dst = zy, mf.didx = p.dev_table + p.dev_final_orig, mf.n = p.last_n, mf.ss = p.last_n;
+        mf.ds = nuv;
+        LdReduce r;
+        r.part = ld, r.out = logdet_per_image, r.nl = (int)p.couplings.size(), r.np = L.ld_parts, r.accumulate = 0;
+        E.record("k_map2", 0, 8.0 * B * p.last_n, [=](void* st) { launch_map2(mf, MapOp{}, r, B, (hipStream_t)st); });
     }
     if (!p.dry) check_launch();
 }

@@ -357,8 +357,8 @@ __global__ __launch_bounds__(256) void k_coup_bw(CoupBwArgs a) {
         for (int c = 0; c < a.dc2; c++) {
             const int e = mask_pos(a.mask_c, p, c, a.wc, a.W, a.D);
             const int q = p * a.dc2 + c;
-            const float th = tanhf(sb[q]);
-            const float ex = expf(w * th);
+            const float th = cpl_tanh(sb[q]);
+            const float ex = cpl_exp(w * th);
             const float g = dvb[e];
             dub[e] = g * ex;
             const float ds = g * ex * ub[e] + a.g_ld;
