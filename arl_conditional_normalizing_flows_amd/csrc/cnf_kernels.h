@@ -104,6 +104,7 @@ struct CoupPend {
     // (net A's workgroup stores it with the log-det sum), and net b's copies the other half (layer
     // k's conditioning half, mask / dc1) from u_k — no pass over v_k at the end of the kernel
     int comp = 0, mask = 0, dc1 = 0;
+    int W = 0, D = 0;   // u_k's width and depth (k_map2 applies a pending coupling of the last layer of a block)
 };
 
 struct NetLdsArgs {
@@ -258,7 +259,10 @@ struct LdReduce {
     float* out = nullptr;
     int nl = 0, np = 0, accumulate = 0;
 };
-void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, int B, hipStream_t st);
+// pend.on: the maps read v_k of a deferred coupling (computed from u_k, s, t on the fly; src is
+// unused), and the extra block computes layer k's log-det sum — into its partial slots, or, with
+// r.part, straight into the per-image total (r.nl then counts the layers before k)
+void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPend& pend, int B, hipStream_t st);
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st);
 void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
                    hipStream_t st);

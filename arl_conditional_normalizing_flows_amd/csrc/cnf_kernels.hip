@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <stdexcept>
 
 #include "cnf_device.h"
 
@@ -570,24 +571,55 @@ __global__ __launch_bounds__(256) void k_map_scatter(const float* __restrict__ s
     }
 }
 
-// blocks [0, ga): map a; [ga, ga + gb): map b; block ga + gb (when r.part): the log-det reduction
-// of image blockIdx.y (as k_ld_reduce, by wave 0)
-__global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, LdReduce r, int B) {
+// blocks [0, ga): map a; [ga, ga + gb): map b; block ga + gb (when r.part or pend.on): the log-det
+// work of image blockIdx.y by wave 0 — layer k's sum of s for a pending coupling, and / or the
+// reduction of the partial slots (as k_ld_reduce)
+__global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, LdReduce r, CoupPend q, int B) {
     const int img = blockIdx.y;
     const int bx = blockIdx.x;
+    const int n_img = q.on ? q.hc * q.wc * (q.dc1 + q.dc2) : 0;   // elements of u_k per image
     if (bx < ga + gb) {
         const MapOp& m = bx < ga ? a : b;
         const int g0 = bx < ga ? 0 : ga, gn = bx < ga ? ga : gb;
-        for (int i = (bx - g0) * 256 + threadIdx.x; i < m.n; i += gn * 256) {
-            const int s = m.sidx ? m.sidx[i] : i;
-            const int d = m.didx ? m.didx[i] : i;
-            m.dst[(size_t)img * m.ds + d] = m.src[(size_t)img * m.ss + s];
+        if (q.on) {
+            const float* ub = q.u + (size_t)img * n_img;
+            const size_t sb = (size_t)img * q.hc * q.wc * q.dc2;
+            const float w = *q.tanh_w;
+            for (int i = (bx - g0) * 256 + threadIdx.x; i < m.n; i += gn * 256) {
+                const int s = m.sidx ? m.sidx[i] : i;
+                const int d = m.didx ? m.didx[i] : i;
+                const int ci = pend_index(q, s, q.W, q.D);
+                float v = ub[s];
+                if (ci >= 0) v = fmaf(cpl_exp(w * cpl_tanh(q.s_pre[sb + ci])), v, q.t[sb + ci]);   // k_coupling's expression
+                m.dst[(size_t)img * m.ds + d] = v;
+            }
+        } else {
+            for (int i = (bx - g0) * 256 + threadIdx.x; i < m.n; i += gn * 256) {
+                const int s = m.sidx ? m.sidx[i] : i;
+                const int d = m.didx ? m.didx[i] : i;
+                m.dst[(size_t)img * m.ds + d] = m.src[(size_t)img * m.ss + s];
+            }
         }
         return;
     }
     if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x, n = r.nl * r.np;
+    const int lane = threadIdx.x;
     double acc = 0.0;
+    if (q.on) {
+        const int n2 = q.hc * q.wc * q.dc2;
+        const float* sp = q.s_pre + (size_t)img * n2;
+        const float w = *q.tanh_w;
+        float ls = 0.f;
+        for (int e = lane; e < n2; e += 64) ls += w * cpl_tanh(sp[e]);
+        const double t = wave_sum((double)ls);
+        if (r.part == nullptr) {
+            if (lane < q.np) q.ld_part[(size_t)img * q.np + lane] = lane == 0 ? t : 0.0;
+            return;
+        }
+        acc = t;
+    }
+    const int n = r.nl * r.np;
+    double ps = 0.0;
     for (int k0 = 0; k0 < n; k0 += 256) {
         double v[4];
 #pragma unroll
@@ -597,9 +629,9 @@ __global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, 
             v[u] = k < n ? r.part[((size_t)l * B + img) * r.np + j] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) acc += v[u];
+        for (int u = 0; u < 4; u++) ps += v[u];
     }
-    acc = wave_sum(acc);
+    acc += wave_sum(ps);
     if (lane == 0) r.out[img] = r.accumulate ? (float)((double)r.out[img] + acc) : (float)acc;
 }
 
@@ -793,12 +825,13 @@ void launch_map_scatter(const float* src, float* dst, const int* sidx, const int
     hipLaunchKernelGGL(k_map_scatter, dim3(gx, B), dim3(256), 0, st, src, dst, sidx, didx, n, ss, ds);
 }
 
-void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, int B, hipStream_t st) {
+void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPend& pend, int B, hipStream_t st) {
     auto gx = [](int n) { return n <= 0 ? 0 : (n + 255) / 256 > 64 ? 64 : (n + 255) / 256; };
     const int ga = gx(a.n), gb = gx(b.n);
-    const int g = ga + gb + (r.part ? 1 : 0);
+    const int g = ga + gb + (r.part || pend.on ? 1 : 0);
     if (g == 0) return;
-    hipLaunchKernelGGL(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, B);
+    if (pend.on && pend.np > 64) throw std::invalid_argument("k_map2: more than 64 log-det slots");
+    hipLaunchKernelGGL(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, pend, B);
 }
 
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st) {

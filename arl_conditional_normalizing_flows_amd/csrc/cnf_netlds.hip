@@ -817,20 +817,6 @@ __device__ __forceinline__ int mask_pos_(int m, int p, int c, int wc, int W, int
     return (pr * W + pc) * D + ch;
 }
 
-// compressed index (p * dc2 + c) in layer k's transformed half of element pos of u_k, or -1 when pos
-// lies in its conditioning half: the inverse of mask_pos_ for the complement mask q.mask_c
-__device__ __forceinline__ int pend_index(const CoupPend& q, int pos, int W, int D) {
-    const int pix = pos / D, ch = pos - pix * D;
-    const int y = pix / W, x = pix - y * W;
-    if (q.mask_c < 2) {   // checkerboard: c0 -> (even, even) / (even, odd), c1 -> (odd, odd) / (odd, even)
-        const int half = y & 1;
-        if (((x & 1) == half) != (q.mask_c == 0)) return -1;
-        return ((y >> 1) * q.wc + (x >> 1)) * q.dc2 + half * D + ch;
-    }
-    if ((ch & 1) != (q.mask_c == 3 ? 1 : 0)) return -1;   // channels 0::2 / 1::2
-    return pix * q.dc2 + (ch >> 1);
-}
-
 }  // namespace
 
 // Diagnostic phase stamps (CNF_STAMPS=1 selects the stamping instantiation; never in timed runs):

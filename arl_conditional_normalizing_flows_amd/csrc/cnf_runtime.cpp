@@ -819,6 +819,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         q.on = 1;
         q.mask = c.mask;
         q.dc1 = c.dc1;
+        q.W = c.W;
+        q.D = c.D;
         return;
     }
     {
@@ -1014,8 +1016,13 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
         const Layer& ly = p.layers[li];
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
-            const bool defer = fuse && !save_inputs && c.use_lds && li + 1 < p.layers.size() &&
-                               p.layers[li + 1].kind == CNF_LAYER_COUPLING && p.couplings[p.layers[li + 1].ci].use_lds;
+            // the next layer that launches anything (squeezes are folded into the factor maps)
+            size_t nx = li + 1;
+            while (nx < p.layers.size() && p.layers[nx].kind == CNF_LAYER_SQUEEZE) nx++;
+            const bool next_lds = nx < p.layers.size() && p.layers[nx].kind == CNF_LAYER_COUPLING &&
+                                  p.couplings[p.layers[nx].ci].use_lds;
+            const bool next_maps = nx >= p.layers.size() || p.layers[nx].kind == CNF_LAYER_FACTOR;
+            const bool defer = fuse && !save_inputs && c.use_lds && (next_lds || next_maps);
             float* nxt = buf[which];
             if (save_inputs) {
                 float* dst = E.at<float>(TL.save_u[c.index]);
@@ -1043,12 +1050,15 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             const int* ks = T + b.dev_keep_src;
             const int* fs = T + b.dev_fac_src;
             const int* fo = T + b.dev_fac_orig;
-            // keep gather -> next buffer and factored scatter -> zy: one launch
+            // keep gather -> next buffer and factored scatter -> zy: one launch (reading v of a
+            // pending coupling on the fly, with that layer's log-det partials)
             MapOp mk, mf;
             mk.src = src, mk.dst = nxt, mk.sidx = ks, mk.n = nnext, mk.ss = ncur, mk.ds = nnext;
             mf.src = src, mf.dst = zy, mf.sidx = fs, mf.didx = fo, mf.n = nfac, mf.ss = ncur, mf.ds = nuv;
+            const CoupPend q = have_pend ? pend : CoupPend{};
+            have_pend = false;
             E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
-                     [=](void* st) { launch_map2(mk, mf, LdReduce{}, B, (hipStream_t)st); });
+                     [=](void* st) { launch_map2(mk, mf, LdReduce{}, q, B, (hipStream_t)st); });
             cur = nxt;
             which ^= 1;
         }
@@ -1060,7 +1070,9 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
         mf.ds = nuv;
         LdReduce r;
         r.part = ld, r.out = logdet_per_image, r.nl = (int)p.couplings.size(), r.np = L.ld_parts, r.accumulate = 0;
-        E.record("k_map2", 0, 8.0 * B * p.last_n, [=](void* st) { launch_map2(mf, MapOp{}, r, B, (hipStream_t)st); });
+        const CoupPend q = have_pend ? pend : CoupPend{};
+        if (have_pend) r.nl -= 1;   // the pending layer is the last one: its log-det sum goes straight into the total
+        E.record("k_map2", 0, 8.0 * B * p.last_n, [=](void* st) { launch_map2(mf, MapOp{}, r, q, B, (hipStream_t)st); });
     }
     if (!p.dry) check_launch();
 }
