@@ -285,6 +285,9 @@ def main():
     total_imgs = B * world * args.steps
     value = total_imgs / el
 
+    # results of the timed steps, read before the roofline re-launches below overwrite the
+    # workspace (kernels re-run out of order, e.g. conv_b's in-place residual accumulates)
+    ld_mean = ld.mean().item()
     out = None
     if rank == 0:
         roof = None
@@ -302,7 +305,6 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg)
-        ld_mean = ld.mean().item()
         # global batch-mean NLL (nats/image): the all-reduced sums when sharded
         loss_mean = (red[0] / red[4]).item() if dist is not None else sums[0].item() / B
         out = {
