@@ -146,6 +146,48 @@ struct LnAcc {
 // wave on its own (no barrier); identity without LN. Each lane folds its partials (Chan merge when
 // it holds more than one), then the wave merges per-lane (n, mean, M2) in the parallel-axis form
 // (N = sum n, mean = sum n m / N, M2 = sum M2 + n (m - mean)^2) with DPP sums: fixed order, fp32.
+// one partial (K, S1, S2, n) folded into a lane's running (n, mean, M2)
+__device__ __forceinline__ void ln_fold(const f4 v, float& n, float& m, float& M2) {
+    if (v[3] > 0.f) {
+        const float r = v[1] * __builtin_amdgcn_rcpf(v[3]);
+        const float mi = v[0] + r, M2i = fmaxf(fmaf(-v[1], r, v[2]), 0.f);
+        const float nn = n + v[3], dl = mi - m, f = v[3] * __builtin_amdgcn_rcpf(nn);
+        m = fmaf(dl, f, m);
+        M2 = M2 + M2i + dl * dl * n * f;
+        n = nn;
+    }
+}
+// wave merge of the lanes' (n, mean, M2) -> (mean, rstd)
+__device__ __forceinline__ void ln_wave_final(float n, float m, float M2, float& mu, float& rstd) {
+    const float N = wave_sum_f(n);
+    const float iN = __builtin_amdgcn_rcpf(N);
+    const float mean = wave_sum_f(n * m) * iN;
+    const float d = m - mean;
+    const float M = wave_sum_f(fmaf(n * d, d, M2));
+    mu = mean;
+    rstd = __builtin_amdgcn_rsqf(fmaf(M, iN, LN_EPS));
+}
+// Split form of in_ln for prologues: in_ln_fetch issues the lane's partial-slot load early (with
+// the prologue's other global loads, so they share one memory round trip; valid when the producer
+// wrote at most 64 slots, lanes beyond read nothing), in_ln_finish folds it — the same arithmetic
+// as in_ln, bit for bit.
+__device__ __forceinline__ f4 in_ln_fetch(const ConvProb& P, int img) {
+    const int lane = threadIdx.x & 63;
+    if (P.in_part == nullptr || lane >= P.in_nparts) return f4{0.f, 0.f, 0.f, 0.f};
+    return *reinterpret_cast<const f4*>(P.in_part + ((size_t)img * P.part_stride + lane) * LNP);
+}
+__device__ __forceinline__ void in_ln_finish(const ConvProb& P, const f4 v, float& mu, float& rstd) {
+    mu = 0.f;
+    rstd = 1.f;
+    if (P.in_part == nullptr) return;
+#ifdef CNF_ABL_NOINLN
+    return;
+#endif
+    float n = 0.f, m = 0.f, M2 = 0.f;
+    ln_fold(v, n, m, M2);
+    ln_wave_final(n, m, M2, mu, rstd);
+}
+
 __device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
     mu = 0.f;
     rstd = 1.f;
@@ -158,22 +200,9 @@ __device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, flo
     float n = 0.f, m = 0.f, M2 = 0.f;
     for (int i = lane; i < P.in_nparts; i += 64) {
         const f4 v = *reinterpret_cast<const f4*>(q + (size_t)LNP * i);
-        if (v[3] > 0.f) {
-            const float r = v[1] * __builtin_amdgcn_rcpf(v[3]);
-            const float mi = v[0] + r, M2i = fmaxf(fmaf(-v[1], r, v[2]), 0.f);
-            const float nn = n + v[3], dl = mi - m, f = v[3] * __builtin_amdgcn_rcpf(nn);
-            m = fmaf(dl, f, m);
-            M2 = M2 + M2i + dl * dl * n * f;
-            n = nn;
-        }
+        ln_fold(v, n, m, M2);
     }
-    const float N = wave_sum_f(n);
-    const float iN = __builtin_amdgcn_rcpf(N);
-    const float mean = wave_sum_f(n * m) * iN;
-    const float d = m - mean;
-    const float M = wave_sum_f(fmaf(n * d, d, M2));
-    mu = mean;
-    rstd = __builtin_amdgcn_rsqf(fmaf(M, iN, LN_EPS));
+    ln_wave_final(n, m, M2, mu, rstd);
 }
 
 // Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.

@@ -1043,7 +1043,10 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             // squeeze (:179) + factor (:276-286) at a block boundary: kept half -> next buffer,
             // factored half -> its final xy-layout position in zy (:1762-1770 restoration).
             const Boundary& b = p.boundaries[bi++];
-            float* nxt = buf[which];
+            // with a pending coupling the maps read u_k (the other buffer) on the fly, and v_k's
+            // own buffer (cur, never written) takes the kept half
+            float* nxt = have_pend ? const_cast<float*>(cur) : buf[which];
+            const bool flip = !have_pend;
             const int* T = p.dev_table;
             const float* src = cur;
             const int ncur = b.n_cur, nnext = b.n_next, nfac = b.n_fac;
@@ -1060,7 +1063,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
                      [=](void* st) { launch_map2(mk, mf, LdReduce{}, q, B, (hipStream_t)st); });
             cur = nxt;
-            which ^= 1;
+            if (flip) which ^= 1;
         }
     }
     {

@@ -166,6 +166,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 #pragma unroll
     for (int n = 0; n < NR; n++) bias[n] = n * 16 + i16 < cout ? P.bias[n * 16 + i16] : 0.f;
 
+    // the first image of this wave's LN-statistics share: its partial slots fetched now, in the same
+    // memory round trip as the loads above and the weights below (folded after the weight copy)
+    const bool lnpre = LN && wave < nimg && P.in_nparts <= 64;
+    const f4 slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
     int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
     asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
@@ -173,7 +177,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     if (LN) {
         for (int i = wave; i < nimg; i += NW) {
             float mu, rs;
-            in_ln(P, img0 + i, mu, rs);
+            if (i == wave && lnpre)
+                in_ln_finish(P, slot0, mu, rs);
+            else
+                in_ln(P, img0 + i, mu, rs);
             if (lane == 0) {
                 lstat[2 * i] = mu;
                 lstat[2 * i + 1] = rs;
@@ -570,6 +577,14 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
         }
     };
     load_img(0);
+    // this wave's first LN2 image: partial slots fetched in the same memory round trip as the band
+    // and weight loads (folded below)
+    ConvProb lnP;
+    lnP.in_part = a.in_part[net];
+    lnP.in_nparts = a.in_nparts;
+    lnP.part_stride = a.part_stride;
+    const bool lnpre = ln && wave < nimg && a.in_nparts <= 64;
+    const f4 slot0 = lnpre ? in_ln_fetch(lnP, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
     // packed weights and quad-offset tables of every branch (once per workgroup)
     for (int bi = 0; bi < GS(nbr); bi++) {
         const GcBranch& br = GS(br)[bi];
@@ -589,13 +604,12 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
     }
     // per-image LN2 (mean, rstd) from the producer's partials
     if (ln) {
-        ConvProb P;
-        P.in_part = a.in_part[net];
-        P.in_nparts = a.in_nparts;
-        P.part_stride = a.part_stride;
         for (int i = wave; i < nimg; i += GC_NW) {
             float mu, rs;
-            in_ln(P, img0 + i, mu, rs);
+            if (i == wave && lnpre)
+                in_ln_finish(lnP, slot0, mu, rs);
+            else
+                in_ln(lnP, img0 + i, mu, rs);
             if (lane == 0) {
                 lstat[2 * i] = mu;
                 lstat[2 * i + 1] = rs;

@@ -90,8 +90,11 @@ def test_inverse_matches_oracle(gpu, name, B, gm, netlds):
     assert e < RTOL
 
 
-@pytest.mark.parametrize('name,B', [('small', 3), ('cfg2', 2)])
+@pytest.mark.parametrize('name,B', [('tiny', 2), ('small', 3), ('cfg2', 2), ('ref_default', 2)])
 def test_layerwise_equals_fused(gpu, name, B):
+    """The fused forward defers LDS layers' coupling laws into the next kernel (k_net_lds or the
+    factor / tail maps; complementary and general mask transitions, one or several log-det slots per
+    image: tiny has one) — zy must equal the layer-by-layer API (k_coupling every layer) bit for bit."""
     flow, ora, P, xy = _setup(name, B)
     x = torch.from_numpy(xy).to(gpu)
     zy1, ld1 = flow(x, 1, per_image_logdet=True)
