@@ -913,6 +913,21 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const size_t sb = (size_t)img * HW * SA(dc1);
         const float w = *q.tanh_w;
         const int n = HW * SA(dc1);
+        // net b: the first CPF copy elements per thread loaded before the gather (one memory round
+        // trip for both), stored after it
+        constexpr int CPF = 4;
+        const int n1 = HW * q.dc1;
+        float cv[CPF];
+        int cp[CPF];
+        if (net == 1) {
+#pragma unroll
+            for (int j = 0; j < CPF; j++) {
+                const int e = (int)threadIdx.x + j * NT;
+                const int p = e / q.dc1, c = e - p * q.dc1;
+                cp[j] = e < n1 ? mask_pos_(q.mask, p, c, W, SA(W), SA(D)) : -1;
+                cv[j] = cp[j] >= 0 ? ub[cp[j]] : 0.f;
+            }
+        }
         float lsum = 0.f;
         for (int e = threadIdx.x; e < n; e += NT) {
             const int p = e / SA(dc1), c = e - p * SA(dc1);
@@ -926,8 +941,10 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             }
         }
         if (net == 1) {
-            const int n1 = HW * q.dc1;
-            for (int e = threadIdx.x; e < n1; e += NT) {
+#pragma unroll
+            for (int j = 0; j < CPF; j++)
+                if (cp[j] >= 0) vb[cp[j]] = cv[j];
+            for (int e = (int)threadIdx.x + CPF * NT; e < n1; e += NT) {
                 const int p = e / q.dc1, c = e - p * q.dc1;
                 const int pos = mask_pos_(q.mask, p, c, W, SA(W), SA(D));
                 vb[pos] = ub[pos];
