@@ -126,6 +126,8 @@ struct NetLdsArgs {
     int maxnr;                                   // widest conv's 16-column output blocks (picks the instantiation)
     int stamp_off;                               // diagnostic stamp builds: LDS byte offset of the stamp array
     CoupPend pend;                               // previous layer's deferred coupling (pend.on)
+    int ci_off[2];                               // conv_in image offset in aux per net (offs[net][0]): its
+                                                 // prefetch starts before the offset table is staged
 };
 // The launch-independent "shape" of a k_net_lds launch as int words: [offs_per_net, zero_bias) and
 // [off_y, stamp_off) of NetLdsArgs (the mask word inside is not part of it). Shape-specialised

@@ -858,6 +858,11 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     // is an LDS broadcast, so no phase drains the in-flight prefetches (vmcnt) to read an offset
     static_assert(NW * 4 * 4 + NW * 8 <= NETLDS_OTAB, "LN slots + log-det scratch overlap the offset table");
     int* otab = reinterpret_cast<int*>(smem + NETLDS_OTAB);
+    // conv_in's packed image (weights + bias) prefetched first, from the offset passed as an argument:
+    // its loads overlap the offset table's and the u1c gather's
+    WPre pf;
+    const float* ci_src = a.aux + a.ci_off[net];
+    wpf_load(pf, ci_src, SA(ci).size + ((nk + 3) & ~3));
     for (int i = threadIdx.x; i < SA(offs_per_net); i += NT) otab[i] = a.offs[net * SA(offs_per_net) + i];
     // 16 zero bytes right below Y: the source of every 3x3 tap quad outside the image
     float* ZQ = reinterpret_cast<float*>(smem + SA(off_y) - 16);
@@ -875,7 +880,6 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     const int per_rb = 10 + 2 * SA(nbr);
     auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
     const int* oend = off + RB0 + SA(R) * per_rb;
-    WPre pf;
     LnPre lp;
     // full-width LNs (Y: nk channels, T2: gc channels) take the prefetched path when quad-shaped
     const bool yq = ln && (nk & 3) == 0, tq = ln && (gc & 3) == 0;
@@ -893,7 +897,6 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const int l = SA(nbr) - 1;
         return o[11 + 2 * l] + ((SA(br_cout)[l] + 3) & ~3) - o[10];
     };
-    wpf_load(pf, X + off[0], wb(SA(ci), nk));
     // gather u1c (mask compress) into T2 (stride SU)
     if (a.pend.on == 0) {
         const float* ub = a.u + (size_t)img * SA(H) * SA(W) * SA(D);
@@ -980,7 +983,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     // conv_in (3x3, dc1 -> nk) -> Y, LN stats of Y
     {
         conv3_table(SA(ci), KT, SA(dc1), 0, 1);
-        wpf_store(pf, WL, X + off[0]);
+        wpf_store(pf, WL, ci_src);
         lst_reset(st);
         lds_barrier();
         if (a.pend.comp != 0 && net == 0 && threadIdx.x == 0) {   // layer k's log-det partial slots

@@ -590,6 +590,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.params = P;
         na.aux = X;
         na.offs = E.p.dev_table + c.dev_lds_offs;
+        for (int n = 0; n < 2; n++) na.ci_off[n] = E.p.host_table[(size_t)c.dev_lds_offs + (size_t)n * na.offs_per_net];
         na.zero_bias = X + E.p.aux_zero;
         if (pend != nullptr) {
             if (pend->v == pend->u || pend->u == u) throw std::logic_error("deferred coupling: v_k aliases u_k");
