@@ -602,6 +602,7 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
             qo[qd] = o;
         }
     }
+    GSTAMP(gs++);   // (diagnostic builds: band / gamma / beta / weight loads landed)
     // per-image LN2 (mean, rstd) from the producer's partials
     if (ln) {
         for (int i = wave; i < nimg; i += GC_NW) {
