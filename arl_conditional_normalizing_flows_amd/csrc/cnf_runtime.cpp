@@ -593,7 +593,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         for (int n = 0; n < 2; n++) na.ci_off[n] = E.p.host_table[(size_t)c.dev_lds_offs + (size_t)n * na.offs_per_net];
         na.zero_bias = X + E.p.aux_zero;
         if (pend != nullptr) {
-            if (pend->v == pend->u || pend->u == u) throw std::logic_error("deferred coupling: v_k aliases u_k");
+            if (!E.p.dry && (pend->v == pend->u || pend->u == u))   // (dry runs carry no real pointers)
+                throw std::logic_error("deferred coupling: v_k aliases u_k");
             na.pend = *pend;
             na.pend.comp = pend->mask_c == c.mask && pend->hc == c.hc && pend->wc == c.wc && pend->dc2 == c.dc1 ? 1 : 0;
         }
@@ -1061,7 +1062,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             mk.src = src, mk.dst = nxt, mk.sidx = ks, mk.n = nnext, mk.ss = ncur, mk.ds = nnext;
             mf.src = src, mf.dst = zy, mf.sidx = fs, mf.didx = fo, mf.n = nfac, mf.ss = ncur, mf.ds = nuv;
             const CoupPend q = have_pend ? pend : CoupPend{};
-            if (q.on && (nxt == q.u || zy == q.u)) throw std::logic_error("k_map2 would overwrite the u_k it reads");
+            if (!p.dry && q.on && (nxt == q.u || zy == q.u)) throw std::logic_error("k_map2 would overwrite the u_k it reads");
             have_pend = false;
             E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
                      [=](void* st) { launch_map2(mk, mf, LdReduce{}, q, B, (hipStream_t)st); });
