@@ -11,7 +11,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / 'csrc'
 LIB = PKG / 'lib' / 'libcnf_hip.so'
 SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
-           'cnf_plan.cpp', 'cnf_train.cpp']
+           'cnf_plan.cpp', 'cnf_train.cpp', 'cnf_comm.cpp']
 HEADERS = ["cnf_kernels.h", "cnf_device.h", "cnf_plan.h", "cnf_netlds_shapes.inc", "cnf_gc_shapes.inc", "cnf_pw_shapes.inc"]
 ARCH = os.environ.get('CNF_OFFLOAD_ARCH', 'gfx950')
 
@@ -85,7 +85,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         for f in [ex.submit(_compile, src, obj, verbose) for src, obj in jobs]:
             f.result()
     tmp = LIB.with_suffix('.so.tmp')
-    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(tmp)] + [str(o) for o in objs]
+    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(tmp)] + [str(o) for o in objs] + ['-ldl']
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')

@@ -82,6 +82,14 @@ _SIGS = [
     ('cnf_plan_recorded_launch_info', C.c_int, [_P, C.c_int, C.c_char_p, C.c_int,
                                                 C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     ('cnf_plan_relaunch', C.c_int, [_P, C.c_int, _P]),
+    ('cnf_plan_set_launch_timing', C.c_int, [_P, C.c_int]),
+    ('cnf_plan_launch_time_ms', C.c_int, [_P, C.c_int, C.POINTER(C.c_float)]),
+    ('cnf_plan_weight_map', C.c_int64, [_P, C.c_int, C.POINTER(C.c_int64), C.c_int64]),
+    ('cnf_comm_unique_id', C.c_int, [C.c_char_p]),
+    ('cnf_comm_init', C.c_int, [C.c_int, C.c_int, C.c_char_p, C.POINTER(_P)]),
+    ('cnf_comm_destroy', None, [_P]),
+    ('cnf_allreduce_sum_f32', C.c_int, [_P, _F, C.c_size_t, _P]),
+    ('cnf_nll_allreduce', C.c_int, [_P, _F, C.c_int, _F, _P]),
     ('cnf_last_error', C.c_char_p, []),
     ('cnf_version', C.c_char_p, []),
 ]

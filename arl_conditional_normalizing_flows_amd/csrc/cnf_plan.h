@@ -3,6 +3,8 @@
 // and the workspace layout. No GPU code here.
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <functional>
 #include <string>
@@ -176,6 +178,9 @@ struct Plan {
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
     std::vector<Recorded> recorded;
+    // in-stream launch timing (bench.py): a HIP event pair around every recorded launch
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // 2 per recorded launch, grown on demand, owned by the plan
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;
 };

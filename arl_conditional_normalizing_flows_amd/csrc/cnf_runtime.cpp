@@ -173,7 +173,17 @@ struct Exec {
 
     void record(const std::string& name, double flops, double bytes, std::function<void(void*)> fn) {
         if (p.dry) return;
+        const size_t k = p.recorded.size();
+        if (p.timing && p.record) {
+            while (p.ev.size() < 2 * (k + 1)) {
+                hipEvent_t e;
+                if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
+                p.ev.push_back(e);
+            }
+            (void)hipEventRecord(p.ev[2 * k], st);
+        }
         fn(st);
+        if (p.timing && p.record) (void)hipEventRecord(p.ev[2 * k + 1], st);
         if (p.record) {
             Recorded r;
             r.name = name;
@@ -593,8 +603,13 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         for (int n = 0; n < 2; n++) na.ci_off[n] = E.p.host_table[(size_t)c.dev_lds_offs + (size_t)n * na.offs_per_net];
         na.zero_bias = X + E.p.aux_zero;
         if (pend != nullptr) {
-            if (!E.p.dry && (pend->v == pend->u || pend->u == u))   // (dry runs carry no real pointers)
-                throw std::logic_error("deferred coupling: v_k aliases u_k");
+            // buffer discipline of the deferred law (dry runs carry no real pointers): this layer's
+            // input is the pending layer's output v_k, which must not be the u_k it is computed
+            // from, and this layer's s/t outputs must not overwrite the pending s_pre / t it reads
+            // (LDS layers alternate s/t sets by coupling index)
+            if (!E.p.dry && (pend->v != u || pend->u == u || so0 == pend->s_pre || so0 == pend->t ||
+                             so1 == pend->s_pre || so1 == pend->t))
+                throw std::logic_error("deferred coupling: buffer aliasing (v_k / u_k / s,t sets)");
             na.pend = *pend;
             na.pend.comp = pend->mask_c == c.mask && pend->hc == c.hc && pend->wc == c.wc && pend->dc2 == c.dc1 ? 1 : 0;
         }
@@ -915,6 +930,7 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->dev_table) (void)hipFree(plan->p->dev_table);
         if (plan->p->dev_aux_map) (void)hipFree(plan->p->dev_aux_map);
         if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
+        for (hipEvent_t e : plan->p->ev) (void)hipEventDestroy(e);
         delete plan->p;
     }
     delete plan;
@@ -1090,6 +1106,7 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
                      float* logdet_per_image, void* workspace, int B, void* stream) {
     if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
+    if (xy == zy) return fail(CNF_E_INVALID, "xy and zy must not alias (out-of-place only)");
     CNF_TRY
     flow_forward(*plan->p, params, aux, xy, zy, logdet_per_image, workspace, B, (hipStream_t)stream, false);
     return CNF_OK;
@@ -1109,6 +1126,7 @@ int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux
                            float* logdet_per_image, void* train_workspace, int B, void* stream) {
     if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !train_workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
+    if (xy == zy) return fail(CNF_E_INVALID, "xy and zy must not alias (out-of-place only)");
     CNF_TRY
     flow_forward(*plan->p, params, aux, xy, zy, logdet_per_image, train_workspace, B, (hipStream_t)stream, true);
     return CNF_OK;
@@ -1159,6 +1177,7 @@ int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, cons
                      void* workspace, int B, void* stream) {
     if (!plan || !params || !aux || !xy || !zy || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
+    if (xy == zy) return fail(CNF_E_INVALID, "zy and xy must not alias (out-of-place only)");
     CNF_TRY
     Plan& p = *plan->p;
     ensure_tables(p);
@@ -1460,6 +1479,32 @@ int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int n
     if (flops) *flops = p.recorded[i].flops;
     if (bytes) *bytes = p.recorded[i].bytes;
     return CNF_OK;
+}
+
+int cnf_plan_set_launch_timing(cnf_plan* plan, int on) {
+    if (!plan) return fail(CNF_E_INVALID, "null plan");
+    plan->p->timing = on != 0;
+    return CNF_OK;
+}
+
+int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms) {
+    if (!plan || !ms) return fail(CNF_E_INVALID, "null argument");
+    const Plan& p = *plan->p;
+    if (i < 0 || i >= (int)p.recorded.size() || 2 * (size_t)i + 1 >= p.ev.size())
+        return fail(CNF_E_INVALID, "launch index out of range (or the last call ran without launch timing)");
+    CNF_TRY
+    hip_check(hipEventSynchronize(p.ev[2 * i + 1]), "hipEventSynchronize");
+    hip_check(hipEventElapsedTime(ms, p.ev[2 * i], p.ev[2 * i + 1]), "hipEventElapsedTime");
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int64_t cnf_plan_weight_map(const cnf_plan* plan, int which, int64_t* out, int64_t cap) {
+    if (!plan || (which != 0 && which != 1)) return fail(CNF_E_INVALID, "null plan or which not in {0, 1}");
+    const std::vector<int64_t>& m = which == 0 ? plan->p->aux_map : plan->p->bw_map;
+    if (out)
+        for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)m.size()); i++) out[i] = m[i];
+    return (int64_t)m.size();
 }
 
 int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream) {

@@ -197,6 +197,32 @@ def _agree_stop(model, process_group):
     model.stop_training = bool(int(flag.item()))
 
 
+def _agreed_batches(model, data, process_group, what):
+    """The epoch's batches; data-parallel, every rank must run the same number of them (each
+    train_step / test_step is a collective: a rank with more batches would block forever in its
+    extra all-reduce), so the counts are compared once per epoch (one all-reduce of two ints) and
+    a mismatch raises on every rank instead of hanging."""
+    batches = _batches(data)
+    if process_group is None:
+        return batches
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return batches
+    batches = list(batches)
+    grp = None if process_group is True else process_group
+    dev = getattr(model, 'device', None)
+    if dist.get_backend(grp) == 'gloo' or dev is None:
+        dev = torch.device('cpu')
+    n = torch.tensor([len(batches), -len(batches)], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=grp)
+    hi, lo = int(n[0]), -int(n[1])
+    if hi != lo:
+        raise ValueError(f'data-parallel fit: ranks hold {lo}..{hi} {what} batches this epoch; every shard '
+                         f'must have the same number of batches')
+    return batches
+
+
 def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Optional[List[Callback]] = None,
         verbose=0, process_group=None):
     """keras Model.fit over train_step / test_step. Logs per epoch: loss, z_loss, y_loss, detJ_loss
@@ -206,7 +232,8 @@ def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Op
     shard of the batches; train_step and test_step all-reduce over the global batch, so the
     logged losses (and EarlyStopping's val_loss) are the same on every rank; rank 0's
     stop_training decision is broadcast after each epoch, and callbacks that write files
-    (CSVLogger, ModelCheckpoint) run on rank 0 only."""
+    (CSVLogger, ModelCheckpoint) run on rank 0 only. Every rank's shard must yield the same number
+    of training (and validation) batches per epoch; a mismatch raises ValueError on every rank."""
     hist = History()
     rank = _rank(process_group)
     cbs = [cb for cb in list(callbacks or []) if rank == 0 or not cb.writes_files] + [hist]
@@ -220,7 +247,7 @@ def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Op
         for t in model.metrics:
             t.reset_state()
         logs = {}
-        for i, xy in enumerate(_batches(x)):
+        for i, xy in enumerate(_agreed_batches(model, x, process_group, 'training')):
             logs = model.train_step(xy, process_group=process_group)
             for cb in cbs:
                 cb.on_train_batch_end(i, logs)
@@ -229,7 +256,7 @@ def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Op
             for t in model.metrics:
                 t.reset_state()
             vlogs = {}
-            for xy in _batches(validation_data):
+            for xy in _agreed_batches(model, validation_data, process_group, 'validation'):
                 vlogs = model.test_step(xy, process_group=process_group)
             logs.update({'val_' + k: v for k, v in vlogs.items()})
         if verbose and rank == 0:
@@ -255,7 +282,7 @@ def anneal_and_fit(model, xy_train: Iterable, xy_val: Optional[Iterable], num_an
     rank = _rank(process_group)
     for i in range(int(num_annealing_epochs)):
         alpha = i / num_annealing_epochs
-        if verbose:
+        if verbose and rank == 0:
             print(f'Annealing instance noise, alpha={alpha}, annealing epoch {i} of {num_annealing_epochs}.')
 
         def noisy(data, tag):

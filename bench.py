@@ -1,20 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark: images/sec of fwd + log-det (+ NLL sums) of the conditional RealNVP hot path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2] [--global-batch G]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one cFlow.call(xy, +1) (zy + per-image log-det) + the NLL 4-sum over one batch of
 synthetic inputs already resident in HBM; with N>1 every rank processes its own batch
-(weak scaling, BASELINE configs[1] batch 64 per GPU) and the 4 NLL sums are all-reduced
-(the path's only exchange step, one RCCL all-reduce of 5 fp32: the 4 sums + the image count). value = images processed by
-all ranks / max-over-ranks wall time of the K timed steps.
+(weak scaling, BASELINE configs[1] batch 64 per GPU; --global-batch G instead shards a fixed
+global batch of G images: strong scaling, BASELINE configs[3]/[4]) and the 4 NLL sums are
+all-reduced (the path's only exchange step, one RCCL all-reduce of 5 fp32: the 4 sums + the image
+count). value = images processed by all ranks / max-over-ranks wall time of the K timed steps.
+
+Extra fields of the JSON line (rank 0):
+  roofline        the dominant kernel (largest GPU time per step, by kernel symbol): algorithmic
+                  FLOPs or bytes per launch / its average duration measured IN THE STREAM (an eager
+                  forward with a HIP event pair around every launch, the queue pre-filled so the
+                  kernels run back to back as in the graph); `per_kernel` gives every symbol.
+                  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary.
+  step_roofline   the whole step against the path's roofline: SURVEY.md §8(d) algorithmic FLOPs
+                  and bytes per image x images, the bound the slower of the two roofs sets.
+  bits_per_dim    of the GPU's NLL on the bench batch; cpu_baseline.bits_per_dim_ref is the float64
+                  oracle's on the same batch and weights (computed in the CPU leg).
+  step_ms_median  median of per-step HIP-event times over >= 100 extra graph replays (BASELINE.md's
+                  protocol); `value` / `ms_per_step` are the K-step wall-clock means.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -41,62 +56,81 @@ def synth(cfg, B, seed):
     return sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=seed)
 
 
-def measure_dominant_kernel(flow, stream, reps=50):
-    """Re-launch every recorded launch of the last forward with HIP events on the launch
-    stream; aggregate per kernel symbol; return the symbol with the largest total time."""
+def kernel_symbol(name):
+    """recorded launch name -> kernel symbol (k_pw<4,8,conv_b> -> k_pw), the granularity of the
+    rocprofv3 summary once its template instantiations are summed."""
+    return name.split('<', 1)[0]
+
+
+def measure_in_stream(flow, forward, reps=20):
+    """Per-launch GPU durations of the forward in its place in the stream: cnf_plan_set_launch_timing
+    brackets every launch with a HIP event pair; a GPU-side sleep before each rep lets the host
+    enqueue the whole forward ahead of the GPU, so the kernels run back to back as in the graph.
+    Returns [(name, flops, bytes, mean ms)] in launch order."""
+    import ctypes as C
     lib = _lib.load()
     plan = flow._plan
-    n = lib.cnf_plan_num_recorded_launches(plan)
-    import ctypes as C
-    name = C.create_string_buffer(256)
-    fl = C.c_double()
-    by = C.c_double()
-    per = {}
-    s = torch.cuda.current_stream()
-    for i in range(n):
-        _lib.check(lib.cnf_plan_recorded_launch_info(plan, i, name, 256, C.byref(fl), C.byref(by)), 'info')
-        nm = name.value.decode()
-        if not nm.startswith('k_'):
-            continue
-        # warm
-        for _ in range(3):
-            _lib.check(lib.cnf_plan_relaunch(plan, i, stream), 'relaunch')
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(s)
+    _lib.check(lib.cnf_plan_set_launch_timing(plan, 1), 'timing on')
+    acc = None
+    try:
         for _ in range(reps):
-            _lib.check(lib.cnf_plan_relaunch(plan, i, stream), 'relaunch')
-        e1.record(s)
-        e1.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        d = per.setdefault(nm, {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'launches': 0})
-        d['ms'] += ms
-        d['flops'] += fl.value
-        d['bytes'] += by.value
-        d['launches'] += 1
-    return per
+            torch.cuda._sleep(50_000_000)
+            forward()
+            torch.cuda.synchronize()
+            n = lib.cnf_plan_num_recorded_launches(plan)
+            ms = C.c_float()
+            t = []
+            for i in range(n):
+                _lib.check(lib.cnf_plan_launch_time_ms(plan, i, C.byref(ms)), 'launch time')
+                t.append(ms.value)
+            acc = t if acc is None else [a + b for a, b in zip(acc, t)]
+    finally:
+        _lib.check(lib.cnf_plan_set_launch_timing(plan, 0), 'timing off')
+    name = C.create_string_buffer(256)
+    fl, by = C.c_double(), C.c_double()
+    out = []
+    for i, tot in enumerate(acc):
+        _lib.check(lib.cnf_plan_recorded_launch_info(plan, i, name, 256, C.byref(fl), C.byref(by)), 'info')
+        out.append((name.value.decode(), fl.value, by.value, tot / reps))
+    return out
 
 
-def roofline_for(per):
-    name, d = max(per.items(), key=lambda kv: kv[1]['ms'])
-    t = d['ms'] / 1e3
-    tflops = d['flops'] / t / 1e12
-    gbs = d['bytes'] / t / 1e9
-    # bound = the roof the kernel's algorithmic intensity runs into first
-    ai = d['flops'] / max(d['bytes'], 1.0)
+def roofline_of(flops, nbytes, ms):
+    t = ms / 1e3
+    ai = flops / max(nbytes, 1.0)
     ridge = FP32_MFMA_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
     if ai >= ridge:
-        rf = {'bound': 'mfma', 'achieved': round(tflops, 3), 'peak': FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
-              'frac': round(tflops / FP32_MFMA_TFLOPS, 4)}
-    else:
-        rf = {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-              'frac': round(gbs / HBM_PEAK_GBS, 4)}
+        a = flops / t / 1e12
+        return {'bound': 'mfma', 'achieved': round(a, 3), 'peak': FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
+                'frac': round(a / FP32_MFMA_TFLOPS, 4)}
+    a = nbytes / t / 1e9
+    return {'bound': 'hbm', 'achieved': round(a, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(a / HBM_PEAK_GBS, 4)}
+
+
+def roofline_for(launches):
+    per = {}
+    for nm, fl, by, ms in launches:
+        if not nm.startswith('k_'):
+            continue
+        d = per.setdefault(kernel_symbol(nm), {'ms': 0.0, 'flops': 0.0, 'bytes': 0.0, 'launches': 0})
+        d['ms'] += ms
+        d['flops'] += fl
+        d['bytes'] += by
+        d['launches'] += 1
+    name, d = max(per.items(), key=lambda kv: kv[1]['ms'])
+    rf = roofline_of(d['flops'], d['bytes'], d['ms'])
     rf.update({'kernel': name, 'launches_per_step': d['launches'],
                'avg_launch_us': round(d['ms'] * 1e3 / d['launches'], 3),
                'alg_flops_per_launch': d['flops'] / d['launches'],
-               'alg_bytes_per_launch': d['bytes'] / d['launches']})
+               'alg_bytes_per_launch': d['bytes'] / d['launches'],
+               'timing': 'in-stream HIP events (eager forward, queue pre-filled)'})
     rf.update(pmc_traffic(name))
-    return rf
+    rf['per_kernel'] = {
+        k: dict(roofline_of(v['flops'], v['bytes'], v['ms']), ms_per_step=round(v['ms'], 4), launches=v['launches'],
+                avg_launch_us=round(v['ms'] * 1e3 / v['launches'], 3))
+        for k, v in sorted(per.items(), key=lambda kv: -kv[1]['ms'])}
+    return rf, per
 
 
 def pmc_traffic(kernel):
@@ -116,7 +150,7 @@ def pmc_traffic(kernel):
         for k, e in ks.items():
             sym = k.split('::')[-1]
             h = e.get('hbm')
-            if h and (sym.startswith(kernel + '<') or sym == kernel):
+            if h and (sym.startswith(kernel + '<') or sym.split('(')[0] == kernel):
                 d = float(h.get('dispatches', 1))
                 tot += h['traffic_bytes'] * d
                 n += d
@@ -126,33 +160,88 @@ def pmc_traffic(kernel):
     return {'traffic': None}
 
 
-def cpu_baseline(cfg, budget_s=12.0):
+def algorithmic_per_image(flow, B):
+    """SURVEY.md §8(d): FLOPs = 2 x conv MACs (grouped convs at the reference's group widths);
+    bytes = 4*2*H*W*D (xy in, zy out) + 8*N_LN (every LN input written once and read once) +
+    4*P_LN/B (LN gamma/beta read once per batch). From the plan's parameter table."""
+    import ctypes as C
+    lib = _lib.load()
+    hw = {}
+    info = _lib.cnf_layer_info()
+    for li in range(lib.cnf_plan_num_layers(flow._plan)):
+        _lib.check(lib.cnf_plan_layer_info(flow._plan, li, C.byref(info)), 'layer info')
+        if info.kind == 0:
+            hw[info.coupling_index] = info.hc * info.wc
+    flops = 0.0
+    n_ln = 0
+    for n, _o, s in flow.param_specs:
+        if n.endswith('.kernel'):
+            ci = int(n.split('.', 1)[0][1:])
+            flops += 2.0 * hw[ci] * float(np.prod(s))
+        elif n.endswith('.gamma'):
+            n_ln += int(np.prod(s))
+    H, W, D = flow.io_shape
+    nbytes = 4.0 * 2 * H * W * D + 8.0 * n_ln + 4.0 * 2 * n_ln / B
+    return flops, nbytes, n_ln
+
+
+def cpu_threads():
+    """The host cores this process may use: its affinity set, capped by a cgroup CPU quota when
+    one is set (on the GPU box os.cpu_count() reports every core of the machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, per = f.read().split()
+            if q != 'max':
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as f:
+                q = int(f.read())
+            with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(math.ceil(quota))))
+    return n
+
+
+def cpu_baseline(cfg, flow, xy_np, B, budget_s=20.0):
     """The oracle's torch-CPU fp32 op-for-op restatement of the reference graph, timed on this
-    host on a bounded sample of the same workload (rank 0, N=1 only)."""
+    host on a bounded sample of the same workload (rank 0, N=1 only): whole batches of the config's
+    B images, median per-batch time. Also the float64 oracle's bits/dim on the bench batch and
+    weights (the `bits/dim vs ref` half of the metric)."""
     try:
         from oracle.cflow_torch_cpu import TorchCPUFlow
     except Exception as e:  # pragma: no cover
         return {'value': None, 'unit': 'images/s', 'cores': 0, 'kind': 'port', 'sample': f'unavailable: {e}'}
-    # the host's CPU share, not the machine's: os.cpu_count() on the GPU box reports every core
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        threads = os.cpu_count() or 1
-    threads = max(1, min(threads, int(os.environ.get('OMP_NUM_THREADS', '16') or 16), 16))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
-    flow = TorchCPUFlow(**cfg.kwargs())
-    P = flow.init_params(0)
-    B = 8
-    xy = torch.from_numpy(synth(cfg, B, 123))
+    tf = TorchCPUFlow(**cfg.kwargs())
+    W = flow.get_weights()
+    P32 = {k: torch.from_numpy(np.ascontiguousarray(v, np.float32)) for k, v in W.items()}
+    xy = torch.from_numpy(np.ascontiguousarray(xy_np, np.float32))
+    times = []
     with torch.no_grad():
-        flow.log_loss(xy, P)          # warm-up
-        n_img, t0 = 0, time.perf_counter()
+        tf.log_loss(xy, P32)          # warm-up
+        t_all = time.perf_counter()
         while True:
-            flow.log_loss(xy, P)
-            n_img += B
-            el = time.perf_counter() - t0
-            if el > budget_s:
+            t0 = time.perf_counter()
+            tf.log_loss(xy, P32)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_all > budget_s and len(times) >= 3:
                 break
+        # bits/dim of the float64 oracle on the same batch and weights
+        P64 = {k: v.double() for k, v in P32.items()}
+        loss64 = float(tf.log_loss(xy.double(), P64)[0])
+    med = float(np.median(times))
     model = platform.processor() or platform.machine()
     try:
         with open('/proc/cpuinfo') as f:
@@ -162,9 +251,13 @@ def cpu_baseline(cfg, budget_s=12.0):
                     break
     except OSError:
         pass
-    return {'value': round(n_img / el, 3), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
-            'sample': f'{n_img} images ({n_img // B} batches of {B}) of {cfg.name} fwd+logdet+NLL, '
-                      f'{el:.1f}s, torch-CPU fp32 restatement (oracle/cflow_torch_cpu.py), {model}'}
+    H, Wd, _ = cfg.io_shape
+    return {'value': round(B / med, 3), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{len(times)} batches of {B} images of {cfg.name} fwd+logdet+NLL (the bench batch and weights), '
+                      f'median {med * 1e3:.1f} ms/batch over {sum(times):.1f}s, torch-CPU fp32 restatement '
+                      f'(oracle/cflow_torch_cpu.py), {threads} threads, {model}',
+            'loss_ref_f64': loss64,
+            'bits_per_dim_ref': loss64 / (math.log(2) * H * Wd * cfg.x_d)}
 
 
 def main():
@@ -174,6 +267,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--config', default='cfg2')
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (default: the config batch)')
+    ap.add_argument('--global-batch', type=int, default=0,
+                    help='strong scaling: shard this many images over the ranks (default: weak scaling, '
+                         'the per-GPU batch on every rank)')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -198,13 +294,24 @@ def main():
             dist.init_process_group(backend)
 
     cfg = PRESETS[args.config]
-    B = args.batch or cfg.batch
+    from arl_conditional_normalizing_flows_amd.distributed import shard_range, pack_nll_sums
+    if args.global_batch:
+        G = args.global_batch
+        lo, hi = shard_range(G, rank, world)
+        scaling = 'strong'
+    else:
+        Bp = args.batch or cfg.batch
+        G = Bp * world
+        lo, hi = shard_range(G, rank, world)
+        scaling = 'weak'
+    B = hi - lo
+    if B <= 0:
+        raise SystemExit(f'rank {rank}: empty shard of a global batch of {G}')
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
     flow = cFlow(**cfg.kwargs(), device=dev, seed=0)
-    # one seeded global batch, sliced per rank (weak scaling: B images per rank)
-    from arl_conditional_normalizing_flows_amd.distributed import shard_range, pack_nll_sums
-    lo, hi = shard_range(B * world, rank, world)
-    xy = torch.from_numpy(synth(cfg, B * world, 1000)[lo:hi].copy()).to(dev)
+    # one seeded global batch, sliced per rank
+    xy_np = synth(cfg, G, 1000)[lo:hi].copy()
+    xy = torch.from_numpy(xy_np).to(dev)
     red = torch.empty(5, device=dev)
     zy = torch.empty_like(xy)
     ld = torch.empty(B, device=dev)
@@ -282,48 +389,75 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
     ms = el / args.steps * 1e3
-    total_imgs = B * world * args.steps
+    total_imgs = G * args.steps
     value = total_imgs / el
 
-    # results of the timed steps, read before the roofline re-launches below overwrite the
-    # workspace (kernels re-run out of order, e.g. conv_b's in-place residual accumulates)
+    # results of the timed steps
     ld_mean = ld.mean().item()
+    loss_mean = (red[0] / red[4]).item() if dist is not None else sums[0].item() / B
     out = None
     if rank == 0:
-        roof = None
-        if not args.no_roofline:
-            local_step()   # eager forward records its launches (no collective: rank 0 only)
+        # per-step times for the median (BASELINE.md protocol): local work only, rank 0
+        st_ms = []
+        if graph is not None:
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(100)]
+            for a, b in evs:
+                a.record()
+                graph.replay()
+                b.record()
             torch.cuda.synchronize()
-            per_k = measure_dominant_kernel(flow, torch.cuda.current_stream().cuda_stream)
-            roof = roofline_for(per_k)
+            st_ms = [a.elapsed_time(b) for a, b in evs]
+        roof = None
+        step_roof = None
+        fl_img, by_img, n_ln = algorithmic_per_image(flow, B)
+        if not args.no_roofline:
+            launches = measure_in_stream(flow, local_step)
+            roof, per_k = roofline_for(launches)
             tot = sum(d['ms'] for d in per_k.values())
-            print(f'# per-kernel (re-launched in isolation): total {tot:.3f} ms/step', file=sys.stderr)
-            for nm, d in sorted(per_k.items(), key=lambda kv: -kv[1]['ms']):
-                t = d['ms'] / 1e3
-                print(f'#  {nm:34s} {d["ms"]:8.3f} ms  x{d["launches"]:3d}  {d["flops"] / t / 1e12:7.2f} TF/s '
-                      f'{d["bytes"] / t / 1e9:8.1f} GB/s', file=sys.stderr)
+            print(f'# per-kernel (in-stream HIP events): total {tot:.3f} ms/step', file=sys.stderr)
+            for nm, fl, by, t_ms in launches:
+                print(f'#  {nm:34s} {t_ms * 1e3:8.2f} us  {fl / max(t_ms, 1e-9) / 1e9:7.2f} TF/s '
+                      f'{by / max(t_ms, 1e-9) / 1e6:8.1f} GB/s', file=sys.stderr)
+        t_mfma = fl_img * B / (FP32_MFMA_TFLOPS * 1e12) * 1e3
+        t_hbm = by_img * B / (HBM_PEAK_GBS * 1e9) * 1e3
+        step_ms = float(np.median(st_ms)) if st_ms else ms
+        step_roof = {'bound': 'mfma' if t_mfma >= t_hbm else 'hbm', 'alg_gflop_per_image': round(fl_img / 1e9, 4),
+                     'alg_mb_per_image': round(by_img / 1e6, 3), 'ln_elems_per_image': n_ln,
+                     'roof_ms': round(max(t_mfma, t_hbm), 4), 'mfma_ms': round(t_mfma, 4), 'hbm_ms': round(t_hbm, 4),
+                     'step_ms': round(step_ms, 4), 'frac': round(max(t_mfma, t_hbm) / step_ms, 4),
+                     'achieved_tflops': round(fl_img * B / (step_ms / 1e3) / 1e12, 3),
+                     'achieved_gbs': round(by_img * B / (step_ms / 1e3) / 1e9, 1)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg)
-        # global batch-mean NLL (nats/image): the all-reduced sums when sharded
-        loss_mean = (red[0] / red[4]).item() if dist is not None else sums[0].item() / B
+            cpu = cpu_baseline(cfg, flow, xy_np, B)
+        H, W, _ = cfg.io_shape
+        bpd = float(loss_mean / (np.log(2) * H * W * cfg.x_d))
         out = {
             'metric': 'images/sec fwd+logdet, 32x32x3 3-scale flow @1/2/4/8 GPU; bits/dim vs ref'
             if args.config == 'cfg2' else f'images/sec fwd+logdet ({args.config})',
             'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(ms, 4), 'higher_is_better': True, 'scaling': 'weak',
+            'warmup': args.warmup, 'ms_per_step': round(ms, 4), 'higher_is_better': True, 'scaling': scaling,
             'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded class-conditional batch, 2% noise), '
-                                                        'seeded orthogonal-init weights',
+                                                        'seeded orthogonal-init weights'
+            if cfg.data == 'class' else 'synthetic (seeded SR batch: residual x, down/up y, 2% noise), '
+                                        'seeded orthogonal-init weights',
             'config': {'workload': f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, '
-                                   f'{B} images per GPU', 'model': f'cFlow {cfg.name}', 'global_batch': B * world,
+                                   + (f'{G} images global over {world} GPUs' if scaling == 'strong'
+                                      else f'{B} images per GPU'),
+                       'model': f'cFlow {cfg.name}', 'global_batch': G,
                        'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world} (batch shards, '
                                                                           f'1 all-reduce of 5 fp32)',
                        'graph': graph is not None},
-            'bits_per_dim': round(float(loss_mean / (np.log(2) * cfg.io_shape[0] * cfg.io_shape[1] * cfg.x_d)), 6),
+            'step_ms_median': round(float(np.median(st_ms)), 4) if st_ms else None,
+            'bits_per_dim': round(bpd, 6),
             'logdet_mean': ld_mean,
             'roofline': roof,
+            'step_roofline': step_roof,
             'cpu_baseline': cpu,
         }
+        if cpu and cpu.get('bits_per_dim_ref') is not None and world == 1:
+            out['bits_per_dim_ref'] = round(cpu['bits_per_dim_ref'], 6)
+            out['bits_per_dim_abs_err'] = abs(bpd - cpu['bits_per_dim_ref'])
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -108,12 +108,14 @@ size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B);
 
 /* cFlow.call(xy, direction=+1) (:1743-1772): xy[B,H,W,D] -> zy[B,H,W,D] in xy
  * layout, logdet_per_image[B] = sum over coupling layers of sum_{h,w,c} A(u1)
- * (the reference returns its batch mean, :1323-1326). */
+ * (the reference returns its batch mean, :1323-1326). xy and zy must not alias
+ * (CNF_E_INVALID): the reference returns new tensors, and the fused schedule
+ * reads xy after zy's first writes. */
 int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux,
                      const float* xy, float* zy, float* logdet_per_image,
                      void* workspace, int B, void* stream);
 
-/* cFlow.call(zy, direction=-1) (:1774-1798): zy -> xy. */
+/* cFlow.call(zy, direction=-1) (:1774-1798): zy -> xy (must not alias). */
 int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux,
                      const float* zy, float* xy, void* workspace, int B, void* stream);
 
@@ -235,6 +237,37 @@ int cnf_up(const float* in, float* out, int B, int H, int W, int C, void* stream
 int cnf_instance_noise(const float* x, float* out, int64_t n, float alpha, uint64_t seed, uint64_t offset,
                        void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Data-parallel exchange: one process per GPU, the batch
+ * sharded over ranks, ONE all-reduce of the NLL sums. Replaces the batch means
+ * of the log-det (:1323-1326) and of log_loss (:1840-1848) over a sharded batch.
+ * RCCL over xGMI, loaded at run time (CNF_E_STATE when librccl is absent).
+ * ------------------------------------------------------------------------- */
+#define CNF_COMM_ID_BYTES 128
+typedef struct cnf_comm cnf_comm;
+
+/* Rank 0 creates the communicator id and hands it to every rank by any
+ * out-of-band means (a file, a key-value store, MPI). */
+int cnf_comm_unique_id(char uid[CNF_COMM_ID_BYTES]);
+/* Collective over `world` processes; binds the communicator to the calling
+ * thread's current HIP device. */
+int cnf_comm_init(int rank, int world, const char uid[CNF_COMM_ID_BYTES], cnf_comm** out);
+void cnf_comm_destroy(cnf_comm* comm);
+/* In-place sum all-reduce of n fp32 device values, asynchronous on stream. */
+int cnf_allreduce_sum_f32(cnf_comm* comm, float* buf, size_t n, void* stream);
+/* The path's exchange step: red5 (device, 5 floats) = sum over ranks of
+ * (sums[0..3] of this rank's cnf_nll, B); red5[k] / red5[4] for k < 4 is the
+ * reference's (loss, z_loss, y_loss, detJ_loss) over the global batch. comm may
+ * be NULL (one process: no collective, red5 = local sums and B). */
+int cnf_nll_allreduce(cnf_comm* comm, const float* sums, int B, float* red5, void* stream);
+
+/* Plan introspection (tests): the canonical parameter index behind every float
+ * of the kernel image (which = 0; -1 = zero padding; cnf_pack_params computes
+ * aux[i] = params[map[i]]) or of the dense training image (which = 1: every
+ * conv as [taps][cin][cout] + bias padded to 4, in layer order). Returns the
+ * map length; copies min(length, cap) entries when out != NULL. */
+int64_t cnf_plan_weight_map(const cnf_plan* plan, int which, int64_t* out, int64_t cap);
+
 /* Measurement hooks (bench.py): number of kernel launches recorded by the last
  * forward/inverse call on this plan, their kernel symbol names, and a re-launch
  * of one recorded launch with identical arguments (same buffers). */
@@ -242,6 +275,12 @@ int cnf_plan_num_recorded_launches(const cnf_plan* plan);
 int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int name_cap,
                                   double* flops, double* bytes);
 int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream);
+/* In-stream launch timing: while on, every launch of a forward/inverse call is
+ * bracketed by a HIP event pair on the call's stream (eager calls only, not
+ * inside graph capture); cnf_plan_launch_time_ms then gives launch i's GPU
+ * duration in its place in the sequence (waits for it). */
+int cnf_plan_set_launch_timing(cnf_plan* plan, int on);
+int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms);
 
 const char* cnf_last_error(void);
 const char* cnf_version(void);

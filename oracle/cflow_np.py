@@ -451,8 +451,9 @@ def st_net(u1c, c: CouplingSpec, P, net: str, ksize=3, ln=True):
 # layers
 # ----------------------------------------------------------------------------
 
-def coupling_forward(u, c: CouplingSpec, P, ksize=3, ln=True):
-    """forward_and_Jacobian :1258-1328. Returns v and the per-image sum of A(u1)."""
+def coupling_forward(u, c: CouplingSpec, P, ksize=3, ln=True, with_abs=False):
+    """forward_and_Jacobian :1258-1328. Returns v and the per-image sum of A(u1) (with_abs: also
+    the per-image sum of |A(u1)|, the conditioning scale of that sum)."""
     u1 = mask_uncompressed(u, c.mask)
     u1c = mask_compress(u, c.mask)
     u2c = mask_compress(u, c.mask_c)
@@ -460,6 +461,8 @@ def coupling_forward(u, c: CouplingSpec, P, ksize=3, ln=True):
     t = st_net(u1c, c, P, 'b', ksize, ln)
     v2c = np.exp(s) * u2c + t
     v = u1 + decompress(v2c, c.mask_c, u.shape)
+    if with_abs:
+        return v, s.reshape(s.shape[0], -1).sum(axis=1), np.abs(s).reshape(s.shape[0], -1).sum(axis=1)
     return v, s.reshape(s.shape[0], -1).sum(axis=1)
 
 
@@ -543,18 +546,22 @@ class OracleCFlow:
     def _cast(self, P, dtype):
         return {k: np.asarray(v, dtype=dtype) for k, v in P.items()}
 
-    def forward(self, xy, P, dtype=np.float64, per_layer=False):
+    def forward(self, xy, P, dtype=np.float64, per_layer=False, abs_s=False):
         """cFlow.call(xy, 1) :1743-1772. Returns (zy, logdet_per_image[B]);
-        the reference's scalar log_detJ is logdet_per_image.mean()."""
+        the reference's scalar log_detJ is logdet_per_image.mean(). abs_s: also the per-image
+        sum over layers of sum|s| (the log-det's conditioning scale), appended
+        to the returned tuple."""
         P = self._cast(P, dtype)
         uv = np.asarray(xy, dtype=dtype)
         zy = None
         ld = np.zeros(uv.shape[0], dtype=dtype)
+        sabs = np.zeros(uv.shape[0], dtype=dtype)
         trace = []
         for e in self.layers:
             if e.kind == 'coupling':
-                uv, d = coupling_forward(uv, e.coupling, P, self.ksize, self.ln)
+                uv, d, a = coupling_forward(uv, e.coupling, P, self.ksize, self.ln, with_abs=True)
                 ld = ld + d
+                sabs = sabs + a
                 if per_layer:
                     trace.append((uv.copy(), d.copy()))
             elif e.kind == 'squeeze':
@@ -572,9 +579,8 @@ class OracleCFlow:
                 else:
                     vu, zy = squeeze_backward(vu, zy)
             out = vu
-        if per_layer:
-            return out, ld, trace
-        return out, ld
+        res = (out, ld) + ((trace,) if per_layer else ()) + ((sabs,) if abs_s else ())
+        return res
 
     def inverse(self, zy_in, P, dtype=np.float64):
         """cFlow.call(zy, -1) :1774-1798."""

@@ -133,7 +133,7 @@ class TorchCPUFlow:
             y = torch.tanh(y) * P[f'{p}.tanh_scale.w']
         return y
 
-    def _coupling(self, u, c, P, direction):
+    def _coupling(self, u, c, P, direction, per_image=False):
         u1 = _masked(u, c.mask)
         u1c = _compress(u, c.mask)
         u2c = _compress(u, c.mask_c)
@@ -141,17 +141,22 @@ class TorchCPUFlow:
         t = self._net(u1c, c, P, 'b')
         if direction > 0:
             v2c = torch.exp(s) * u2c + t
-            ld = s.reshape(s.shape[0], -1).sum(1).mean()
+            ld = s.reshape(s.shape[0], -1).sum(1)
+            ld = torch.stack([ld, s.abs().reshape(s.shape[0], -1).sum(1)]) if per_image else ld.mean()
         else:
             v2c = torch.reciprocal(torch.exp(s)) * (u2c - t)
             ld = None
         return u1 + _decompress(v2c, c.mask_c, u.shape), ld
 
-    def forward(self, xy, P):
+    def forward(self, xy, P, per_image=False):
+        """cFlow.call(xy, 1). per_image: the log-det is returned as the [2][B] stack of the
+        per-image sum of s and sum of |s| over every coupling layer (run in float64 with float64
+        params and inputs this is the full-size parity oracle of tests/test_gpu_parity.py)."""
         uv, zy, ld = xy, None, 0.0
         for e in self.layers:
             if e.kind == 'coupling':
-                uv, d = self._coupling(uv, e.coupling, P, +1)
+                uv, d = (self._coupling(uv, e.coupling, P, +1, True) if per_image else
+                         self._coupling(uv, e.coupling, P, +1))
                 ld = ld + d
             elif e.kind == 'squeeze':
                 uv = _s2d(uv)

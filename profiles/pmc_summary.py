@@ -64,6 +64,23 @@ def main(out, tag):
             if s.get('SQ_WAVE_CYCLES'):
                 e['sq']['active_frac'] = s.get('SQ_ACTIVE_INST_ANY', 0.0) / s['SQ_WAVE_CYCLES']
                 e['sq']['wait_frac'] = s.get('SQ_WAIT_ANY', 0.0) / s['SQ_WAVE_CYCLES']
+    # per kernel symbol (template instantiations summed): the granularity of bench.py's roofline
+    sym = {}
+    for k, e in res['kernels'].items():
+        name = re.sub(r'<.*$', '', k.split('::')[-1])
+        d = sym.setdefault(name, {'calls': 0, 'total_ns': 0.0, 'hbm_bytes': 0.0, 'hbm_dispatches': 0})
+        t = e.get('trace')
+        if t:
+            d['calls'] += t['calls']
+            d['total_ns'] += t['total_ns']
+        h = e.get('hbm')
+        if h:
+            d['hbm_bytes'] += h['traffic_bytes'] * h['dispatches']
+            d['hbm_dispatches'] += h['dispatches']
+    for d in sym.values():
+        d['avg_ns'] = d['total_ns'] / d['calls'] if d['calls'] else None
+        d['traffic_bytes_per_launch'] = d['hbm_bytes'] / d['hbm_dispatches'] if d['hbm_dispatches'] else None
+    res['symbols'] = sym
     dst = os.path.join(ROOT, 'profiles', f'{tag}_summary.json')
     with open(dst, 'w') as fh:
         json.dump(res, fh, indent=1, sort_keys=True)

@@ -90,15 +90,95 @@ def test_plan_rejects_like_reference_asserts(lib, bad, msg):
     assert msg in lib.cnf_last_error().decode()
 
 
-def test_aux_pack_map_is_grouped_kernel_gather(lib):
-    """The aux image (dense grouped-conv weights) is exactly the per-group Conv2D kernels placed
-    block-wise (reference mode: all groups share the input slice)."""
-    kw = PRESETS['small'].kwargs()
+def _weight_map(lib, p, which):
+    n = lib.cnf_plan_weight_map(p, which, None, 0)
+    assert n > 0
+    buf = (C.c_int64 * n)()
+    assert lib.cnf_plan_weight_map(p, which, buf, n) == n
+    return np.frombuffer(buf, dtype=np.int64).copy()
+
+
+@pytest.mark.parametrize('name', ['small', 'cfg2', 'ref_default'])
+@pytest.mark.parametrize('gm', ['reference', 'intended'])
+def test_grouped_conv_images_are_the_per_group_kernels(lib, name, gm):
+    """The dense image of every grouped dilated stage (the one the kernels' packed images and the
+    training path are built from) is exactly the card per-group Conv2D kernels
+    (conv_cINN_base_functions.py:389-411) placed block-wise: output channel n = j*_d + o of branch d
+    comes from group j's kernel [tap][c - in_offset_j][o] — in reference mode every group reads the
+    LAST _d-channel slice (the Lambda closure quirk), in intended mode slice j — and is
+    zero elsewhere. Checked entry by entry against the oracle's parameter table. The packed kernel
+    image then holds every conv element (each grouped kernel element equally often) and no LN or
+    tanh parameter."""
+    kw = PRESETS[name].kwargs()
     kw.pop('group_mode')
-    rc, p, keep = _plan(lib, kw)
+    rc, p, keep = _plan(lib, kw, 0 if gm == 'reference' else 1)
     assert rc == 0
-    assert lib.cnf_plan_aux_floats(p) > 0
-    lib.cnf_plan_destroy(p)
+    try:
+        o = OracleCFlow(**kw, group_mode=gm)
+        offs, at = {}, 0
+        for n_, s_ in o.specs:
+            offs[n_] = (at, s_)
+            at += int(np.prod(s_)) if s_ else 1
+        bw = _weight_map(lib, p, 1)
+        pad4 = lambda v: (v + 3) // 4 * 4
+        pos = 0
+
+        def take(taps, cin, cout, kernel_idx, bias_idx):
+            nonlocal pos
+            w = bw[pos:pos + taps * cin * cout].reshape(taps, cin, cout)
+            pos += taps * cin * cout
+            b = bw[pos:pos + pad4(cout)]
+            pos += pad4(cout)
+            assert np.array_equal(w, kernel_idx)
+            assert np.array_equal(b[:cout], bias_idx) and np.all(b[cout:] == -1)
+
+        def plain(nm, taps, cin, cout):
+            k0, _ = offs[nm + '.kernel']
+            b0, _ = offs[nm + '.bias']
+            take(taps, cin, cout, k0 + np.arange(taps * cin * cout).reshape(taps, cin, cout), b0 + np.arange(cout))
+
+        n_grouped = 0
+        for c in o.coupling_specs:
+            for net in ('A', 'b'):
+                q = f'c{c.index}.{net}'
+                plain(f'{q}.conv_in', 9, c.dc1, c.nk)
+                for r in range(c.R):
+                    plain(f'{q}.rb{r}.conv_a', 1, c.nk, c.nk)
+                    for bi, br in enumerate(c.branches):
+                        lo = min(br.in_offsets)
+                        cin = max(br.in_offsets) + br.width - lo
+                        cout = len(br.in_offsets) * br.width
+                        exp = -np.ones((9, cin, cout), np.int64)
+                        bias = np.zeros(cout, np.int64)
+                        for j, off in enumerate(br.in_offsets):
+                            k0, shp = offs[f'{q}.rb{r}.gc.d{bi}.g{j}.kernel']
+                            assert tuple(shp) == (3, 3, br.width, br.width)
+                            kk = k0 + np.arange(9 * br.width * br.width).reshape(9, br.width, br.width)
+                            exp[:, off - lo:off - lo + br.width, j * br.width:(j + 1) * br.width] = kk
+                            bias[j * br.width:(j + 1) * br.width] = offs[f'{q}.rb{r}.gc.d{bi}.g{j}.bias'][0] + \
+                                np.arange(br.width)
+                        if gm == 'reference' and len(br.in_offsets) > 1:
+                            assert len(set(br.in_offsets)) == 1 and cin == br.width   # all groups: last slice
+                        take(9, cin, cout, exp, bias)
+                        n_grouped += 1
+                    plain(f"{q}.rb{r}.conv_b", 1, c.gc_channels, c.nk)
+                plain(f'{q}.conv_out', 9, c.nk, c.dc2)
+        assert pos == bw.size and n_grouped > 0
+        # the packed kernel image: conv elements only, each grouped kernel element equally often
+        aux = _weight_map(lib, p, 0)
+        assert aux.size == lib.cnf_plan_aux_floats(p)
+        cnt = np.bincount(aux[aux >= 0], minlength=o.num_params())
+        for n_, (k0, s_) in offs.items():
+            size = int(np.prod(s_)) if s_ else 1
+            seg = cnt[k0:k0 + size]
+            if n_.endswith('.kernel') or n_.endswith('.bias'):
+                assert seg.min() >= 1, n_
+                if '.gc.' in n_:
+                    assert seg.min() == seg.max(), n_
+            else:
+                assert seg.max() == 0, n_
+    finally:
+        lib.cnf_plan_destroy(p)
 
 
 def test_version(lib):
@@ -144,3 +224,20 @@ def test_netlds_shape_table_is_current(lib):
     gen = root / 'arl_conditional_normalizing_flows_amd' / 'csrc' / 'gen_netlds_shapes.py'
     r = subprocess.run([sys.executable, str(gen), '--check'], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_forward_rejects_aliased_xy_zy(lib):
+    """cnf_flow_forward / _inverse / _forward_train are out-of-place (cnf.h): an aliased call is
+    refused before anything is launched (so this runs without a GPU)."""
+    kw = PRESETS['tiny'].kwargs()
+    kw.pop('group_mode')
+    rc, p, keep = _plan(lib, kw)
+    assert rc == 0
+    try:
+        a, b = 1 << 40, 2 << 40   # never dereferenced
+        assert lib.cnf_flow_forward(p, a, a, b, b, a, a, 2, None) == -1
+        assert b'alias' in lib.cnf_last_error()
+        assert lib.cnf_flow_inverse(p, a, a, b, b, a, 2, None) == -1
+        assert lib.cnf_flow_forward_train(p, a, a, b, b, a, a, 2, None) == -1
+    finally:
+        lib.cnf_plan_destroy(p)

@@ -1,0 +1,118 @@
+"""The path's exchange step with the HIP-produced NLL sums.
+
+* gloo, world size 2 (both ranks on cuda:0): every rank runs the HIP forward + cnf_nll on its
+  shard of the global batch, and the single 5-float all-reduce of its sums (distributed.py) must
+  reproduce the float64 oracle's log_loss over the global batch
+  (conv_cINN_make_model.py:1800-1848), ragged shards included.
+* The C-ABI communicator (cnf_comm_* / cnf_nll_allreduce, RCCL) for a non-torch caller: one rank
+  (RCCL refuses two ranks on one device, and the box has one GPU); the 8-GPU path is the
+  driver's scaling run.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from arl_conditional_normalizing_flows_amd import _lib
+from arl_conditional_normalizing_flows_amd.config import PRESETS
+from arl_conditional_normalizing_flows_amd.distributed import shard_range
+from oracle.cflow_np import OracleCFlow, synthetic_class_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _hip_worker(rank, world, port, G, out_dir):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from arl_conditional_normalizing_flows_amd.make_model import cFlow
+        from arl_conditional_normalizing_flows_amd.distributed import reduce_nll_sums
+        dev = torch.device('cuda', 0)
+        cfg = PRESETS['small']
+        kw = cfg.kwargs()
+        flow = cFlow(**kw, device=dev)
+        flow.set_weights(OracleCFlow(**kw).init_params(0))
+        H, W, _ = cfg.io_shape
+        xy = synthetic_class_batch(G, H, W, cfg.x_d, seed=7)
+        lo, hi = shard_range(G, rank, world)
+        x = torch.from_numpy(xy[lo:hi]).to(dev)
+        lib = _lib.load()
+        zy, ld = flow(x, 1, per_image_logdet=True)
+        per = torch.empty((hi - lo, 3), device=dev)
+        sums = torch.empty(4, device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        _lib.check(lib.cnf_nll(flow._plan, x.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
+                               sums.data_ptr(), hi - lo, st), 'nll')
+        torch.cuda.synchronize()
+        got = torch.stack(reduce_nll_sums(sums.cpu(), hi - lo)).numpy()   # the gloo all-reduce
+        np.save(os.path.join(out_dir, f'r{rank}.npy'), got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('G', [6, 7])
+def test_gloo_world2_hip_nll_sums_match_global_batch(gpu, tmp_path, G):
+    world = 2
+    mp.spawn(_hip_worker, args=(world, _free_port(), G, str(tmp_path)), nprocs=world, join=True)
+    cfg = PRESETS['small']
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(0)
+    H, W, _ = cfg.io_shape
+    xy = synthetic_class_batch(G, H, W, cfg.x_d, seed=7).astype(np.float64)
+    ref = np.array(ora.log_loss(xy, P))
+    _, _, abs_s = ora.forward(xy, P, abs_s=True)
+    r0 = np.load(tmp_path / 'r0.npy')
+    r1 = np.load(tmp_path / 'r1.npy')
+    print('global means', r0, 'oracle', ref)
+    assert np.array_equal(r0, r1)          # every rank sees the same global means
+    assert np.all(np.abs(r0 - ref) <= 1e-5 * np.maximum(np.abs(ref), abs_s.mean()))
+
+
+def test_capi_comm_one_rank(gpu):
+    """cnf_comm_unique_id -> cnf_comm_init -> cnf_nll_allreduce / cnf_allreduce_sum_f32 on one rank:
+    the packed payload is (the 4 cnf_nll sums, B) and a sum over one rank is the identity."""
+    lib = _lib.load()
+    uid = C.create_string_buffer(128)
+    _lib.check(lib.cnf_comm_unique_id(uid), 'unique id')
+    comm = C.c_void_p()
+    _lib.check(lib.cnf_comm_init(0, 1, uid, C.byref(comm)), 'comm init')
+    try:
+        dev = torch.device('cuda', 0)
+        st = torch.cuda.current_stream().cuda_stream
+        sums = torch.tensor([1.5, -2.0, 3.25, 4.0], device=dev)
+        red = torch.full((5,), 7.0, device=dev)
+        _lib.check(lib.cnf_nll_allreduce(comm, sums.data_ptr(), 13, red.data_ptr(), st), 'nll allreduce')
+        x = torch.arange(1000, dtype=torch.float32, device=dev)
+        _lib.check(lib.cnf_allreduce_sum_f32(comm, x.data_ptr(), 1000, st), 'allreduce')
+        torch.cuda.synchronize()
+        assert red.cpu().tolist() == [1.5, -2.0, 3.25, 4.0, 13.0]
+        assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
+        # the no-communicator form packs only
+        _lib.check(lib.cnf_nll_allreduce(None, sums.data_ptr(), 2, red.data_ptr(), st), 'pack')
+        torch.cuda.synchronize()
+        assert red.cpu().tolist() == [1.5, -2.0, 3.25, 4.0, 2.0]
+    finally:
+        lib.cnf_comm_destroy(comm)
+    assert lib.cnf_comm_init(1, 1, uid, C.byref(comm)) == -1      # rank out of range
+
+
+def test_capi_comm_rejects_bad_arguments(gpu):
+    lib = _lib.load()
+    comm = C.c_void_p()
+    assert lib.cnf_comm_init(0, 0, b'\0' * 128, C.byref(comm)) == -1
+    assert lib.cnf_allreduce_sum_f32(None, None, 4, None) == -1

@@ -1,6 +1,13 @@
-"""GPU parity: the HIP path (through the C ABI) against the numpy oracle on identical
-weights and inputs. Tolerance (north star): fp32 result vs the float64 restatement within
-1e-5 relative; log-det within 1e-5 * max(|ref|, sum|s|)."""
+"""GPU parity: the HIP path (through the C ABI) against the oracle on identical weights and
+inputs. Tolerance (north star): fp32 result vs the float64 restatement within
+1e-5 relative; per-image log-det within 1e-5 * max(|ref|, sum|s|), where sum|s| is the per-image
+sum over every coupling layer of |s| (the conditioning scale of the log-det sum: a sum of
+thousands of terms of both signs cannot be asked for better than its terms' rounding).
+
+Small batches compare against the numpy oracle (oracle/cflow_np.py); the bench sizes (cfg2 B=64,
+cfg3 B=128) and the larger architectures against the float64 torch-CPU restatement
+(oracle/cflow_torch_cpu.py, pinned to the numpy oracle in tests/test_oracle.py), which finishes
+them in seconds."""
 import numpy as np
 import pytest
 import torch
@@ -40,10 +47,30 @@ def _setup(name, B, group_mode='reference', seed=0, netlds=True):
     return flow, ora, P, xy
 
 
-def _abs_sum_s(ora, xy, P):
-    """sum over layers of sum|s| per image (the log-det conditioning scale)."""
-    _, _, trace = ora.forward(xy, P, per_layer=True)
-    return None
+def ld_tol(ld_ref, abs_s):
+    """per-image log-det bound of the north star: 1e-5 * max(|ref|, sum|s|)."""
+    return RTOL * np.maximum(np.abs(np.asarray(ld_ref, np.float64)), np.asarray(abs_s, np.float64))
+
+
+def check_logdet(ld_gpu, ld_ref, abs_s, what=''):
+    e = np.abs(np.asarray(ld_gpu, np.float64) - np.asarray(ld_ref, np.float64))
+    tol = ld_tol(ld_ref, abs_s)
+    print(f'{what} logdet: max abs err {e.max():.3e}, worst err/tol {np.max(e / tol):.3f} '
+          f'(|ref| <= {np.abs(ld_ref).max():.3e}, sum|s| >= {np.min(abs_s):.3e})')
+    assert np.all(e <= tol), (e, tol)
+
+
+def torch64_forward(name, xy, P, group_mode='reference'):
+    """float64 torch-CPU oracle: (zy, per-image log-det, per-image sum|s|)."""
+    from oracle.cflow_torch_cpu import TorchCPUFlow
+    kw = PRESETS[name].kwargs()
+    kw['group_mode'] = group_mode
+    t = TorchCPUFlow(**kw)
+    torch.set_num_threads(max(1, min(16, len(__import__('os').sched_getaffinity(0)))))
+    with torch.no_grad():
+        zy, st = t.forward(torch.from_numpy(np.asarray(xy, np.float64)),
+                           {k: torch.from_numpy(np.asarray(v, np.float64)) for k, v in P.items()}, per_image=True)
+    return zy.numpy(), st[0].numpy(), st[1].numpy()
 
 
 def _err(a, b):
@@ -67,15 +94,50 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
 def test_forward_logdet_matches_oracle(gpu, name, B, gm, netlds):
     flow, ora, P, xy = _setup(name, B, gm, netlds=netlds)
-    zy_ref, ld_ref = ora.forward(xy, P)
+    zy_ref, ld_ref, abs_s = ora.forward(xy, P, abs_s=True)
     zy, ld = flow(torch.from_numpy(xy).to(gpu), 1, per_image_logdet=True)
     torch.cuda.synchronize()
     e_zy = _err(zy.cpu().numpy(), zy_ref)
-    ld_g = ld.cpu().numpy().astype(np.float64)
-    e_ld = np.max(np.abs(ld_g - ld_ref))
-    print(f'{name} {gm} lds={netlds}: zy rel err {e_zy:.3e}, logdet abs err {e_ld:.3e} (|ref| {np.abs(ld_ref).max():.3e})')
+    print(f'{name} {gm} lds={netlds}: zy rel err {e_zy:.3e}')
     assert e_zy < RTOL
-    assert e_ld <= RTOL * max(np.abs(ld_ref).max(), 1.0) * 10
+    check_logdet(ld.cpu().numpy(), ld_ref, abs_s, f'{name} {gm} lds={netlds}')
+
+
+# the bench sizes of BASELINE configs[1] / configs[2] (and the multi-scale configs at a batch whose
+# image-looping kernels give workgroups several images) against the float64 torch-CPU oracle
+FULL = [('cfg2', 64, True), ('cfg3', 128, True), ('cfg2', 64, False), ('cfg4', 6, True), ('cfg5', 2, True)]
+
+
+@pytest.mark.parametrize('name,B,netlds', FULL)
+def test_full_size_forward_inverse_match_oracle(gpu, name, B, netlds):
+    flow, ora, P, xy = _setup(name, B, netlds=netlds)
+    zy_ref, ld_ref, abs_s = torch64_forward(name, xy, P)
+    zy, ld = flow(torch.from_numpy(xy).to(gpu), 1, per_image_logdet=True)
+    # inverse of the oracle's zy: the float64 flow is invertible to 1e-12, so its preimage is xy
+    x = flow(torch.from_numpy(zy_ref.astype(np.float32)).to(gpu), -1)
+    torch.cuda.synchronize()
+    e_zy = _err(zy.cpu().numpy(), zy_ref)
+    e_x = _err(x.cpu().numpy(), xy)
+    print(f'{name} B={B} lds={netlds}: zy rel err {e_zy:.3e}, inverse rel err {e_x:.3e}')
+    assert e_zy < RTOL and e_x < RTOL
+    check_logdet(ld.cpu().numpy(), ld_ref, abs_s, f'{name} B={B}')
+
+
+def test_full_size_nll_matches_oracle(gpu):
+    """log_loss (:1800-1848) at the bench batch (cfg2, B=64): the 4 batch means against float64,
+    each within 1e-5 of its conditioning scale (mean over images of the sum of |terms|)."""
+    flow, ora, P, xy = _setup('cfg2', 64)
+    zy_ref, ld_ref, abs_s = torch64_forward('cfg2', xy, P)
+    llz, lly, _ = ora.nll_terms(xy.astype(np.float64), zy_ref, ld_ref)
+    x_d = PRESETS['cfg2'].x_d
+    lp_abs = (0.5 * zy_ref[..., :x_d] ** 2).reshape(64, -1).sum(1) + 0.5 * x_d * np.log(2 * np.pi) * 32 * 32
+    cz, cy, cd = lp_abs.mean(), np.abs(lly).mean(), abs_s.mean()
+    ref = [-((llz + lly).mean() + ld_ref.mean()), -llz.mean(), -lly.mean(), -ld_ref.mean()]
+    scale = [cz + cy + cd, cz, cy, cd]
+    got = [t.item() for t in flow.log_loss(torch.from_numpy(xy).to(gpu))]
+    print('nll ref', ref, 'got', got, 'scale', scale)
+    for r, g, c in zip(ref, got, scale):
+        assert abs(r - g) <= RTOL * max(abs(r), c)
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
@@ -90,7 +152,8 @@ def test_inverse_matches_oracle(gpu, name, B, gm, netlds):
     assert e < RTOL
 
 
-@pytest.mark.parametrize('name,B', [('tiny', 2), ('small', 3), ('cfg2', 2), ('ref_default', 2)])
+@pytest.mark.parametrize('name,B', [('tiny', 2), ('small', 3), ('cfg2', 2), ('ref_default', 2), ('cfg3', 5),
+                                    ('cfg4', 3), ('cfg5', 1)])
 def test_layerwise_equals_fused(gpu, name, B):
     """The fused forward defers LDS layers' coupling laws into the next kernel (k_net_lds or the
     factor / tail maps; complementary and general mask transitions, one or several log-det slots per
@@ -120,15 +183,17 @@ def test_roundtrip_cfg2_full_batch(gpu):
     assert torch.isfinite(ld).all()
 
 
-@pytest.mark.parametrize('netlds', [True, False])
-def test_ragged_large_batch_matches_small_batches(gpu, netlds):
+@pytest.mark.parametrize('name,netlds', [('cfg2', True), ('cfg2', False), ('cfg3', True)])
+def test_ragged_large_batch_matches_small_batches(gpu, name, netlds):
     """Every op is per image, so an image's result must not depend on the batch it rides in: a
     ragged batch of 67 (the image-looping kernels' last workgroups get partial image sets) against
     the same images in batches of 5, on the LDS and the streamed paths (tolerance: fp32 ordering
     of the LN partial merges, 1e-6 relative)."""
-    from oracle.cflow_np import synthetic_class_batch
-    flow, ora, P, _ = _setup('cfg2', 2, netlds=netlds)
-    xy = synthetic_class_batch(67, 32, 32, 3, seed=5)
+    flow, ora, P, _ = _setup(name, 2, netlds=netlds)
+    cfg = PRESETS[name]
+    H, W, _D = cfg.io_shape
+    xy = (synthetic_class_batch(67, H, W, cfg.x_d, seed=5) if cfg.data == 'class'
+          else synthetic_sr_batch(67, H, W, cfg.x_d, cfg.sr_pow, seed=5))
     x = torch.from_numpy(xy).to(gpu)
     zy, ld = flow(x, 1, per_image_logdet=True)
     for s in range(0, 67, 5):
@@ -142,10 +207,12 @@ def test_ragged_large_batch_matches_small_batches(gpu, netlds):
 def test_nll_matches_oracle(gpu):
     flow, ora, P, xy = _setup('cfg2', 2)
     ref = ora.log_loss(xy, P)
+    _, _, abs_s = ora.forward(xy, P, abs_s=True)
     got = [t.item() for t in flow.log_loss(torch.from_numpy(xy).to(gpu))]
     print('nll', ref, got)
+    # conditioning: the log-det terms' sum|s| (the NLL terms themselves are sums of one sign)
     for r, g in zip(ref, got):
-        assert abs(r - g) <= RTOL * max(abs(r), 1.0) * 10
+        assert abs(r - g) <= RTOL * max(abs(r), abs_s.mean())
 
 
 def test_deterministic(gpu):
@@ -164,12 +231,12 @@ def test_coupling_layer_api_matches_oracle(gpu):
     Pd = {k: np.asarray(v, np.float64) for k, v in P.items()}
     u = xy.astype(np.float64)
     for layer, entry in zip(flow.layers_list[:4], ora.layers[:4]):
-        v_ref, ld_ref = coupling_forward(u, entry.coupling, Pd)
+        v_ref, ld_ref, abs_s = coupling_forward(u, entry.coupling, Pd, with_abs=True)
         ut = torch.from_numpy(u.astype(np.float32)).to(gpu)
         v, s, z = layer.forward_and_Jacobian(ut, torch.zeros(2, device=gpu), None)
         assert z is None
         assert _err(v.cpu().numpy(), v_ref) < RTOL
-        assert np.max(np.abs(s.cpu().numpy() - ld_ref)) <= 1e-4 * max(1.0, np.abs(ld_ref).max())
+        check_logdet(s.cpu().numpy(), ld_ref, abs_s, f'layer {entry.coupling.index}')
         u_back, _ = layer.backward(v, None)
         assert _err(u_back.cpu().numpy(), coupling_backward(v.cpu().numpy().astype(np.float64), entry.coupling, Pd)) < RTOL
         u = v_ref

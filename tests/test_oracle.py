@@ -164,3 +164,26 @@ def test_torch_cpu_baseline_matches_oracle():
     got = t.log_loss(torch.from_numpy(xy), {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in P.items()})
     for r, g in zip(ref, got):
         assert abs(r - float(g)) <= 1e-4 * max(1.0, abs(r))
+
+
+def test_torch_cpu_float64_is_the_numpy_oracle():
+    """The float64 torch-CPU restatement (the full-size parity oracle of the GPU tests) equals the
+    numpy oracle: zy, per-image log-det and per-image sum|s| to float64 rounding."""
+    import torch
+    from oracle.cflow_torch_cpu import TorchCPUFlow
+    from arl_conditional_normalizing_flows_amd.config import PRESETS
+    for name in ('small', 'tiny'):
+        kw = PRESETS[name].kwargs()
+        o = _flow(**kw)
+        P = o.init_params(2)
+        H, W, D = PRESETS[name].io_shape
+        xy = O.synthetic_class_batch(3, H, W, PRESETS[name].x_d, seed=4)
+        zr, lr, ar = o.forward(xy, P, abs_s=True)
+        t = TorchCPUFlow(**kw)
+        with torch.no_grad():
+            zt, st = t.forward(torch.from_numpy(xy).double(), {k: torch.from_numpy(np.asarray(v, np.float64))
+                                                               for k, v in P.items()}, per_image=True)
+        assert np.allclose(zt.numpy(), zr, rtol=0, atol=1e-11)
+        assert np.allclose(st[0].numpy(), lr, rtol=0, atol=1e-10)
+        assert np.allclose(st[1].numpy(), ar, rtol=0, atol=1e-10)
+        assert np.all(ar >= np.abs(lr))

@@ -182,6 +182,39 @@ def test_gloo_world2_fit_agrees_on_early_stop(tmp_path):
     assert os.path.exists(tmp_path / 'w0.e04.npz') and not any(p.name.startswith('w1') for p in tmp_path.iterdir())
 
 
+def _mismatch_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        stub = _DPStub([1.0] * 3)
+        msg = ''
+        try:
+            T.fit(stub, [0, 0, 0] if rank == 0 else [0, 0], epochs=1, process_group=True)
+        except ValueError as e:
+            msg = str(e)
+        with open(os.path.join(out_dir, f'm{rank}.txt'), 'w') as f:
+            f.write(f'{stub.steps}|{msg}')
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_fit_rejects_unequal_shards(tmp_path):
+    """Shards with different batch counts would leave one rank blocked in an all-reduce the other
+    never joins: fit compares the counts first and raises on every rank, before any step."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_mismatch_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in (0, 1):
+        steps, msg = (tmp_path / f'm{r}.txt').read_text().split('|', 1)
+        assert steps == '0' and 'same number of batches' in msg
+
+
 @pytest.mark.gpu
 def test_anneal_and_fit_end_to_end(gpu, tmp_path):
     from arl_conditional_normalizing_flows_amd.config import PRESETS
