@@ -4,6 +4,7 @@
 #include <cstddef>
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 
@@ -17,6 +18,23 @@ constexpr double LOG_2PI_D = 1.8378770664093453;
 constexpr int LNP = 4;
 
 constexpr int MAXPROB = 12;
+
+// Launch timing (bench.py via cnf_plan_set_launch_timing): while a pair is armed, the launch
+// helpers dispatch through hipExtLaunchKernelGGL, which stores the kernel's own begin / end
+// timestamps (the dispatch packet's profiling timestamps, as rocprofv3 reads them) into the
+// events: no extra packets between the kernels, so the stream runs as it does untimed.
+struct LaunchTiming {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchTiming& launch_timing();   // per host thread (cnf_runtime.cpp)
+#define CNF_LAUNCH(K, G, B, L, S, ...)                                                              \
+    do {                                                                                            \
+        const ::cnf::LaunchTiming& lt_ = ::cnf::launch_timing();                                    \
+        if (lt_.start != nullptr)                                                                   \
+            hipExtLaunchKernelGGL(K, G, B, L, S, lt_.start, lt_.stop, 0, __VA_ARGS__);              \
+        else                                                                                        \
+            hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                         \
+    } while (0)
 
 // packed weight-image formats (see cnf_plan.h PackedConv)
 enum { PK_1X1 = 0, PK_KN = 1, PK_TAP = 2, PK_Q4 = 3 };

@@ -762,7 +762,7 @@ __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ params, 
 void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(256);
 #define CNF_CONV_CASE(MR_, R_) \
-    if (ks == 3 && mr == MR_ && role == R_) { hipLaunchKernelGGL((k_conv<3, MR_, R_>), g, b, lds, st, a); return; }
+    if (ks == 3 && mr == MR_ && role == R_) { CNF_LAUNCH((k_conv<3, MR_, R_>), g, b, lds, st, a); return; }
     CNF_CONV_CASE(1, ROLE_CONV_IN)
     CNF_CONV_CASE(1, ROLE_GC)
     CNF_CONV_CASE(1, ROLE_CONV_OUT)
@@ -775,7 +775,7 @@ void launch_conv(int ks, int mr, int role, const ConvArgs& a, int grid_x, int ld
 void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(256);
 #define CNF_CONV1_CASE(MR_, V_, R_) \
-    if (mr == MR_ && vec == V_ && role == R_) { hipLaunchKernelGGL((k_conv1<MR_, V_, R_>), g, b, lds, st, a); return; }
+    if (mr == MR_ && vec == V_ && role == R_) { CNF_LAUNCH((k_conv1<MR_, V_, R_>), g, b, lds, st, a); return; }
     CNF_CONV1_CASE(1, true, ROLE_CONV_A)
     CNF_CONV1_CASE(1, true, ROLE_CONV_B)
     CNF_CONV1_CASE(1, false, ROLE_CONV_A)
@@ -790,7 +790,7 @@ void launch_conv1(int mr, bool vec, int role, const ConvArgs& a, int grid_x, int
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(256);
 #define CNF_TAP_CASE(MT_, V_) \
-    if (mt == MT_ && vec == V_) { hipLaunchKernelGGL((k_convtap<MT_, V_>), g, b, lds, st, a); return; }
+    if (mt == MT_ && vec == V_) { CNF_LAUNCH((k_convtap<MT_, V_>), g, b, lds, st, a); return; }
     CNF_TAP_CASE(1, true) CNF_TAP_CASE(2, true) CNF_TAP_CASE(3, true) CNF_TAP_CASE(4, true) CNF_TAP_CASE(6, true)
     CNF_TAP_CASE(1, false) CNF_TAP_CASE(2, false) CNF_TAP_CASE(3, false) CNF_TAP_CASE(4, false) CNF_TAP_CASE(6, false)
 #undef CNF_TAP_CASE
@@ -801,28 +801,28 @@ void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, i
     int n = hc * wc * dc1;
     int gx = (n + 255) / 256;
     if (gx > 64) gx = 64;
-    hipLaunchKernelGGL(k_gather_u1c, dim3(gx, B), dim3(256), 0, st, u, u1c, H, W, D, mask, hc, wc, dc1);
+    CNF_LAUNCH(k_gather_u1c, dim3(gx, B), dim3(256), 0, st, u, u1c, H, W, D, mask, hc, wc, dc1);
 }
 
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
-    hipLaunchKernelGGL(k_coupling, dim3(nparts, B), dim3(256), 0, st, a);
+    CNF_LAUNCH(k_coupling, dim3(nparts, B), dim3(256), 0, st, a);
 }
 
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st) {
-    hipLaunchKernelGGL(k_ld_reduce, dim3(B), dim3(64), 0, st, part, out, B, nl, np, accumulate);
+    CNF_LAUNCH(k_ld_reduce, dim3(B), dim3(64), 0, st, part, out, B, nl, np, accumulate);
 }
 
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st) {
     int gx = (n + 255) / 256;
     if (gx > 64) gx = 64;
-    hipLaunchKernelGGL(k_map_gather, dim3(gx, B), dim3(256), 0, st, src, dst, idx, n, ss, ds);
+    CNF_LAUNCH(k_map_gather, dim3(gx, B), dim3(256), 0, st, src, dst, idx, n, ss, ds);
 }
 
 void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
                         int B, hipStream_t st) {
     int gx = (n + 255) / 256;
     if (gx > 64) gx = 64;
-    hipLaunchKernelGGL(k_map_scatter, dim3(gx, B), dim3(256), 0, st, src, dst, sidx, didx, n, ss, ds);
+    CNF_LAUNCH(k_map_scatter, dim3(gx, B), dim3(256), 0, st, src, dst, sidx, didx, n, ss, ds);
 }
 
 void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPend& pend, int B, hipStream_t st) {
@@ -831,7 +831,7 @@ void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPe
     const int g = ga + gb + (r.part || pend.on ? 1 : 0);
     if (g == 0) return;
     if (pend.on && pend.np > 64) throw std::invalid_argument("k_map2: more than 64 log-det slots");
-    hipLaunchKernelGGL(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, pend, B);
+    CNF_LAUNCH(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, pend, B);
 }
 
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st) {
@@ -839,7 +839,7 @@ void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int
     long long gx = (total + 255) / 256;
     if (gx > 8192) gx = 8192;
     if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(k_squeeze, dim3((unsigned)gx), dim3(256), 0, st, in, out, H, W, C, dir, total);
+    CNF_LAUNCH(k_squeeze, dim3((unsigned)gx), dim3(256), 0, st, in, out, H, W, C, dir, total);
 }
 
 void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
@@ -848,25 +848,25 @@ void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_c
     long long gx = (total + 255) / 256;
     if (gx > 8192) gx = 8192;
     if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(k_chcopy, dim3((unsigned)gx), dim3(256), 0, st, in, in_cs, in_off, out, out_cs, out_off, C,
+    CNF_LAUNCH(k_chcopy, dim3((unsigned)gx), dim3(256), 0, st, in, in_cs, in_off, out, out_cs, out_off, C,
                        npix);
 }
 
 void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, int B, int HW,
                 int D, int x_d, float lambda_y, hipStream_t st) {
-    hipLaunchKernelGGL(k_nll, dim3(B), dim3(256), 0, st, xy, zy, ld, per_image, HW, D, x_d, lambda_y);
-    hipLaunchKernelGGL(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
+    CNF_LAUNCH(k_nll, dim3(B), dim3(256), 0, st, xy, zy, ld, per_image, HW, D, x_d, lambda_y);
+    CNF_LAUNCH(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
 }
 
 void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st) {
-    hipLaunchKernelGGL(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
+    CNF_LAUNCH(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
 }
 
 void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st) {
     long long gx = (n + 255) / 256;
     if (gx > 4096) gx = 4096;
     if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)gx), dim3(256), 0, st, params, map, aux, n);
+    CNF_LAUNCH(k_pack, dim3((unsigned)gx), dim3(256), 0, st, params, map, aux, n);
 }
 
 }  // namespace cnf

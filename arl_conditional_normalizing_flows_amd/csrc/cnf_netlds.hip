@@ -1255,10 +1255,10 @@ bool launch_shape(int sid, const NetLdsArgs& a, dim3 grid, dim3 block, int lds, 
             if (stamps) {
                 NetLdsArgs b = a;
                 b.stamp_off = (lds + 15) & ~15;
-                hipLaunchKernelGGL((k_net_lds<true, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block,
+                CNF_LAUNCH((k_net_lds<true, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block,
                                    b.stamp_off + 1024, st, b);
             } else {
-                hipLaunchKernelGGL((k_net_lds<false, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block, lds, st, a);
+                CNF_LAUNCH((k_net_lds<false, shape_narrow<S>() ? 2 : 5, shape_ks<S>(), S>), grid, block, lds, st, a);
             }
             return true;
         }
@@ -1299,19 +1299,19 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
         b.stamp_off = (lds + 15) & ~15;
         const int l2 = b.stamp_off + 1024;
         if (narrow && ks)
-            hipLaunchKernelGGL((k_net_lds<true, 2, true, -1>), grid, block, l2, st, b);
+            CNF_LAUNCH((k_net_lds<true, 2, true, -1>), grid, block, l2, st, b);
         else if (narrow)
-            hipLaunchKernelGGL((k_net_lds<true, 2, false, -1>), grid, block, l2, st, b);
+            CNF_LAUNCH((k_net_lds<true, 2, false, -1>), grid, block, l2, st, b);
         else
-            hipLaunchKernelGGL((k_net_lds<true, 5, false, -1>), grid, block, l2, st, b);
+            CNF_LAUNCH((k_net_lds<true, 5, false, -1>), grid, block, l2, st, b);
         return;
     }
     if (narrow && ks) {
-        hipLaunchKernelGGL((k_net_lds<false, 2, true, -1>), grid, block, lds, st, a);
+        CNF_LAUNCH((k_net_lds<false, 2, true, -1>), grid, block, lds, st, a);
     } else if (narrow) {
-        hipLaunchKernelGGL((k_net_lds<false, 2, false, -1>), grid, block, lds, st, a);
+        CNF_LAUNCH((k_net_lds<false, 2, false, -1>), grid, block, lds, st, a);
     } else {
-        hipLaunchKernelGGL((k_net_lds<false, 5, false, -1>), grid, block, lds, st, a);
+        CNF_LAUNCH((k_net_lds<false, 5, false, -1>), grid, block, lds, st, a);
     }
 }
 

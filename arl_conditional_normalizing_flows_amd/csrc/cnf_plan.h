@@ -123,6 +123,7 @@ struct Recorded {
     std::string name;
     double flops = 0, bytes = 0;
     std::function<void(void*)> relaunch;
+    bool timed = false;   // its kernel wrote begin / end timestamps into the plan's event pair
 };
 
 struct WsLayout {

@@ -63,6 +63,11 @@ namespace cnf {
 // error reporting for the entry points defined outside this file (cnf_transforms.hip)
 int set_error(int code, const char* msg) { return fail(code, msg); }
 
+LaunchTiming& launch_timing() {
+    thread_local LaunchTiming t;
+    return t;
+}
+
 // ----------------------------------------------------------------------------------------------
 // geometry
 // ----------------------------------------------------------------------------------------------
@@ -174,22 +179,29 @@ struct Exec {
     void record(const std::string& name, double flops, double bytes, std::function<void(void*)> fn) {
         if (p.dry) return;
         const size_t k = p.recorded.size();
-        if (p.timing && p.record) {
+        const bool timed = p.timing && p.record && name.rfind("k_", 0) == 0;   // kernels only (not copies)
+        if (timed) {
             while (p.ev.size() < 2 * (k + 1)) {
                 hipEvent_t e;
                 if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
                 p.ev.push_back(e);
             }
-            (void)hipEventRecord(p.ev[2 * k], st);
+            launch_timing() = LaunchTiming{p.ev[2 * k], p.ev[2 * k + 1]};
         }
-        fn(st);
-        if (p.timing && p.record) (void)hipEventRecord(p.ev[2 * k + 1], st);
+        try {
+            fn(st);
+        } catch (...) {
+            launch_timing() = LaunchTiming{};
+            throw;
+        }
+        launch_timing() = LaunchTiming{};
         if (p.record) {
             Recorded r;
             r.name = name;
             r.flops = flops;
             r.bytes = bytes;
             r.relaunch = std::move(fn);
+            r.timed = timed;
             p.recorded.push_back(std::move(r));
         }
     }
@@ -1490,8 +1502,11 @@ int cnf_plan_set_launch_timing(cnf_plan* plan, int on) {
 int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms) {
     if (!plan || !ms) return fail(CNF_E_INVALID, "null argument");
     const Plan& p = *plan->p;
-    if (i < 0 || i >= (int)p.recorded.size() || 2 * (size_t)i + 1 >= p.ev.size())
-        return fail(CNF_E_INVALID, "launch index out of range (or the last call ran without launch timing)");
+    if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");
+    if (!p.recorded[i].timed) {   // not a kernel (a copy), or the call ran without launch timing
+        *ms = 0.f;
+        return CNF_OK;
+    }
     CNF_TRY
     hip_check(hipEventSynchronize(p.ev[2 * i + 1]), "hipEventSynchronize");
     hip_check(hipEventElapsedTime(ms, p.ev[2 * i], p.ev[2 * i + 1]), "hipEventElapsedTime");

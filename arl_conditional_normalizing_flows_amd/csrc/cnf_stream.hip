@@ -285,7 +285,7 @@ bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStr
     if constexpr (S < CNF_PW_NSHAPES) {
         if (sid == S) {
             constexpr PwShape k = kPwShapes[S];
-            hipLaunchKernelGGL((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S, k.tap != 0>), g, b, lds, st, a);
+            CNF_LAUNCH((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S, k.tap != 0>), g, b, lds, st, a);
             return true;
         }
         return launch_pw_shape<S + 1>(sid, a, g, b, lds, st);
@@ -306,7 +306,7 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
         if (res || gm > 8) throw std::invalid_argument("k_pw tap mode: no residual, K <= 128");
 #define CNF_PW_TCASE(NR_, GM_, LN_)                                                     \
         if (nr == NR_ && gm == GM_ && ln == LN_) {                                      \
-            hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, false, -1, true>), g, b, lds, st, a); \
+            CNF_LAUNCH((k_pw<NR_, GM_, LN_, false, -1, true>), g, b, lds, st, a); \
             return;                                                                     \
         }
 #define CNF_PW_TNR(GM_, LN_) CNF_PW_TCASE(1, GM_, LN_) CNF_PW_TCASE(2, GM_, LN_) CNF_PW_TCASE(3, GM_, LN_) CNF_PW_TCASE(4, GM_, LN_)
@@ -318,7 +318,7 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
     }
 #define CNF_PW_CASE(NR_, GM_, LN_, RES_)                                              \
     if (nr == NR_ && gm == GM_ && ln == LN_ && res == RES_) {                          \
-        hipLaunchKernelGGL((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
+        CNF_LAUNCH((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
         return;                                                                        \
     }
 #define CNF_PW_NR(GM_, LN_, RES_) \
@@ -663,7 +663,7 @@ template <int S>
 bool launch_gc_shape(int sid, const GcArgs& a, dim3 grid, int lds, hipStream_t st) {
     if constexpr (S < CNF_GC_NSHAPES) {
         if (sid == S) {
-            hipLaunchKernelGGL((k_gc<S>), grid, dim3(64 * GC_NW_SPEC), lds, st, a);
+            CNF_LAUNCH((k_gc<S>), grid, dim3(64 * GC_NW_SPEC), lds, st, a);
             return true;
         }
         return launch_gc_shape<S + 1>(sid, a, grid, lds, st);
@@ -691,7 +691,7 @@ void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
     const dim3 grid(grid_x, 2);
     const int sid = gc_shape_id(a);
     if (sid >= 0 && launch_gc_shape<0>(sid, a, grid, lds, st)) return;
-    hipLaunchKernelGGL((k_gc<-1>), grid, dim3(64 * GC_NW_GEN), lds, st, a);
+    CNF_LAUNCH((k_gc<-1>), grid, dim3(64 * GC_NW_GEN), lds, st, a);
 }
 
 }  // namespace cnf

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "cnf_device.h"
 #include "cnf_kernels.h"
@@ -122,8 +123,126 @@ __global__ __launch_bounds__(256) void k_tconv(TConvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_tconv_mfma: the same convolution as an implicit GEMM on v_mfma_f32_16x16x4_f32. A workgroup of
+// 4 waves owns 64 pixels (16 per wave) x 16*NR output channels of one image. Per tap, the weights
+// W(tap, k, n) are staged into LDS as [g][kq][j][s] (k = 16g + 4kq + s, j = n - n0), so lane (i16, kq)
+// reads one float4 per 16-column block; its A operand is the float4 of channels 16g + 4kq .. +3 of
+// its (shifted) pixel, loaded straight from global with LN + LeakyReLU applied in registers. The
+// K order inside a group is permuted identically on both operands, so the sum is the conv's.
+// ------------------------------------------------------------------------------------------------
+template <int NR, bool VEC>
+__global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float wsm[];
+    constexpr int NS = 16 * NR;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int npx = a.H * a.W, b = blockIdx.y;
+    const int p0 = blockIdx.x * 64, n0 = blockIdx.z * NS;
+    const int G = (a.K + 15) >> 4;
+    const int pa = p0 + wave * 16 + i16;
+    const bool pav = pa < npx;
+    const int pr = pa / a.W, pc = pa - pr * a.W;
+    const float* inb = a.in + (size_t)b * npx * a.in_cs + a.in_off;
+    const bool ln = a.stats != nullptr;
+    const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+    f4 acc[NR];
+#pragma unroll
+    for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+    const int nw = G * 16 * NS;
+    for (int tap = 0; tap < a.taps; tap++) {
+        const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
+        const int r = pr + a.sgn * a.dil * dr, c = pc + a.sgn * a.dil * dc;
+        const bool sv = pav && r >= 0 && r < a.H && c >= 0 && c < a.W;
+        const size_t q = sv ? (size_t)r * a.W + c : 0;
+        __syncthreads();   // the previous tap's B reads are done
+        for (int e = threadIdx.x; e < nw; e += 256) {
+            const int s4 = e & 3, j = (e >> 2) % NS, gq = (e >> 2) / NS;   // gq = 4g + kq'
+            const int k = 4 * gq + s4, n = n0 + j;
+            wsm[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+        }
+        __syncthreads();
+        for (int g = 0; g < G; g++) {
+            const int k0 = 16 * g + 4 * kq;
+            f4 x = f4{0.f, 0.f, 0.f, 0.f};
+            if (sv) {
+                const size_t gi = q * a.in_cs + k0;
+                if (VEC) {
+                    if (k0 < a.K) {
+                        x = *reinterpret_cast<const f4*>(inb + gi);
+                        if (ln) {
+                            const f4 gm = *reinterpret_cast<const f4*>(a.gamma + a.in_off + gi);
+                            const f4 bt = *reinterpret_cast<const f4*>(a.beta + a.in_off + gi);
+#pragma unroll
+                            for (int j = 0; j < 4; j++) x[j] = (lrelu(x[j]) - mu) * rs * gm[j] + bt[j];
+                        } else if (a.act) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) x[j] = lrelu(x[j]);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (k0 + j < a.K) x[j] = act_load(inb[gi + j], a.act, a.stats, a.gamma, a.beta, b, a.in_off + gi + j);
+                }
+            }
+            const f4* bw = reinterpret_cast<const f4*>(wsm) + (size_t)(4 * g + kq) * NS + i16;
+#pragma unroll
+            for (int m = 0; m < NR; m++) {
+                const f4 bv = bw[16 * m];
+#pragma unroll
+                for (int s = 0; s < 4; s++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], bv[s], acc[m], 0, 0, 0);
+            }
+        }
+    }
+    // acc[m][rr] = out[pixel p0 + 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+        const int p = p0 + wave * 16 + 4 * kq + rr;
+        if (p >= npx) continue;
+        const size_t ob = ((size_t)b * npx + p) * a.out_cs + a.out_off;
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const int n = n0 + 16 * m + i16;
+            if (n >= a.N) continue;
+            float v = acc[m][rr];
+            if (a.bias) v += a.bias[n];
+            if (a.res) v += a.res[ob + n];
+            if (a.accumulate) v += a.out[ob + n];
+            a.out[ob + n] = v;
+        }
+    }
+}
+
+static bool train_valu() {
+    static const bool v = [] {   // A/B knob: the register-blocked VALU kernels
+        const char* e = std::getenv("CNF_TRAIN_VALU");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 void launch_tconv(const TConvArgs& a, hipStream_t st) {
     const int npx = a.H * a.W;
+    if (!train_valu()) {
+        const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
+        const int NS = 16 * nr;
+        const int G = (a.K + 15) / 16;
+        const size_t lds = (size_t)G * 16 * NS * 4;
+        if (lds <= 64 * 1024) {
+            const bool vec = a.K % 4 == 0 && a.in_cs % 4 == 0 && a.in_off % 4 == 0;
+            const dim3 g((npx + 63) / 64, a.B, (a.N + NS - 1) / NS), blk(256);
+#define CNF_TM(NR_)                                                                                   \
+    if (nr == NR_) {                                                                                  \
+        if (vec)                                                                                      \
+            hipLaunchKernelGGL((k_tconv_mfma<NR_, true>), g, blk, lds, st, a);                      \
+        else                                                                                          \
+            hipLaunchKernelGGL((k_tconv_mfma<NR_, false>), g, blk, lds, st, a);                     \
+        return;                                                                                       \
+    }
+            CNF_TM(1) CNF_TM(2) CNF_TM(3) CNF_TM(4)
+#undef CNF_TM
+        }
+    }
     const int TN = a.N <= 4 ? 4 : a.N <= 16 ? 16 : 64;
     const int TP = 4096 / TN;
     const dim3 g((npx + TP - 1) / TP, a.B, (a.N + TN - 1) / TN), blk(256);
@@ -215,9 +334,99 @@ __global__ __launch_bounds__(256) void k_wgrad(WGradArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_wgrad_mfma: the same weight gradient on v_mfma_f32_16x16x4_f32, a (ci, co) = 64 x 64 tile per
+// workgroup, K = the chunk's pixels. Each 32-pixel step stages X (LN-on-load, shifted by the tap)
+// and dY into LDS (the next step's values are loaded into registers behind this step's MFMAs);
+// wave w owns ci rows 16w.. of the tile: lane (i16, kq) feeds X[px 4s+kq][ci 16w+i16] and
+// dY[px 4s+kq][co 16m+i16], so acc[m][r] = dW[ci 16w+4kq+r][co 16m+i16].
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wgrad_mfma(WGradArgs a) {
+    constexpr int SP = 32, XS = 80, NE = SP * 64 / 256;   // row stride 80: conflict-free half-wave reads
+    __shared__ __attribute__((aligned(16))) float Xs[SP * XS];
+    __shared__ __attribute__((aligned(16))) float Ds[SP * XS];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int npx = a.H * a.W;
+    const long long total = (long long)a.B * npx;
+    const int tap = blockIdx.y;
+    const int nco = (a.CO + 63) / 64;
+    const int ci0 = (blockIdx.z / nco) * 64, co0 = (blockIdx.z % nco) * 64;
+    const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
+    const long long g0 = (long long)blockIdx.x * a.chunk_px;
+    const long long g1 = g0 + a.chunk_px < total ? g0 + a.chunk_px : total;
+    const bool do_bias = a.bpart != nullptr && tap == 0 && ci0 == 0;
+    f4 acc[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+    float bacc = 0.f;
+    float xv[NE], dv[NE];
+    auto load = [&](long long gs) {
+#pragma unroll
+        for (int u = 0; u < NE; u++) {
+            const int e = t + 256 * u;
+            const int c = e & 63, px = e >> 6;
+            const long long g = gs + px;
+            float x = 0.f, d = 0.f;
+            if (g < g1) {
+                const int b = (int)(g / npx), p = (int)(g - (long long)b * npx);
+                if (co0 + c < a.CO) d = a.dy[((size_t)b * npx + p) * a.dy_cs + a.dy_off + co0 + c];
+                if (ci0 + c < a.CI) {
+                    const int r = p / a.W + a.dil * dr, cc = p % a.W + a.dil * dc;
+                    if (r >= 0 && r < a.H && cc >= 0 && cc < a.W) {
+                        const size_t q = (size_t)r * a.W + cc;
+                        const size_t gi = q * a.x_cs + a.x_off + ci0 + c;
+                        x = act_load(a.x[(size_t)b * npx * a.x_cs + gi], a.act, a.stats, a.gamma, a.beta, b, gi);
+                    }
+                }
+            }
+            xv[u] = x;
+            dv[u] = d;
+        }
+    };
+    load(g0);
+    for (long long gs = g0; gs < g1; gs += SP) {
+        __syncthreads();   // the previous step's LDS reads are done
+#pragma unroll
+        for (int u = 0; u < NE; u++) {
+            const int e = t + 256 * u;
+            Xs[(e >> 6) * XS + (e & 63)] = xv[u];
+            Ds[(e >> 6) * XS + (e & 63)] = dv[u];
+        }
+        __syncthreads();
+        if (gs + SP < g1) load(gs + SP);   // in flight during this step's MFMAs
+#pragma unroll
+        for (int s = 0; s < SP / 4; s++) {
+            const int px = 4 * s + kq;
+            const float av = Xs[px * XS + 16 * wave + i16];
+#pragma unroll
+            for (int m = 0; m < 4; m++)
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Ds[px * XS + 16 * m + i16], acc[m], 0, 0, 0);
+        }
+        if (do_bias && t < 64) {
+#pragma unroll
+            for (int px = 0; px < SP; px++) bacc += Ds[px * XS + t];
+        }
+    }
+    float* part = a.part + (size_t)blockIdx.x * a.taps * a.CI * a.CO;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int ci = ci0 + 16 * wave + 4 * kq + r;
+        if (ci >= a.CI) continue;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const int co = co0 + 16 * m + i16;
+            if (co < a.CO) part[((size_t)tap * a.CI + ci) * a.CO + co] = acc[m][r];
+        }
+    }
+    if (do_bias && t < 64 && co0 + t < a.CO) a.bpart[(size_t)blockIdx.x * a.CO + co0 + t] = bacc;
+}
+
 void launch_wgrad(const WGradArgs& a, hipStream_t st) {
     const dim3 g(a.chunks, a.taps, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
-    hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);
+    if (train_valu())
+        hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);
+    else
+        hipLaunchKernelGGL(k_wgrad_mfma, g, blk, 0, st, a);
 }
 
 __global__ __launch_bounds__(256) void k_grad_scatter(const float* __restrict__ part, int chunks, long long n,

@@ -63,9 +63,11 @@ def kernel_symbol(name):
 
 
 def measure_in_stream(flow, forward, reps=20):
-    """Per-launch GPU durations of the forward in its place in the stream: cnf_plan_set_launch_timing
-    brackets every launch with a HIP event pair; a GPU-side sleep before each rep lets the host
-    enqueue the whole forward ahead of the GPU, so the kernels run back to back as in the graph.
+    """Per-launch GPU durations of the forward in its place in the stream: with
+    cnf_plan_set_launch_timing on, every kernel is dispatched with hipExtLaunchKernelGGL start/stop
+    events that receive its own begin / end timestamps (no packets in between, the numbers
+    rocprofv3's kernel trace reads); a GPU-side sleep before each rep lets the host enqueue the
+    whole forward ahead of the GPU, so the kernels run back to back as in the graph.
     Returns [(name, flops, bytes, mean ms)] in launch order."""
     import ctypes as C
     lib = _lib.load()
@@ -74,7 +76,7 @@ def measure_in_stream(flow, forward, reps=20):
     acc = None
     try:
         for _ in range(reps):
-            torch.cuda._sleep(50_000_000)
+            torch.cuda._sleep(20_000_000)
             forward()
             torch.cuda.synchronize()
             n = lib.cnf_plan_num_recorded_launches(plan)
@@ -124,7 +126,7 @@ def roofline_for(launches):
                'avg_launch_us': round(d['ms'] * 1e3 / d['launches'], 3),
                'alg_flops_per_launch': d['flops'] / d['launches'],
                'alg_bytes_per_launch': d['bytes'] / d['launches'],
-               'timing': 'in-stream HIP events (eager forward, queue pre-filled)'})
+               'timing': 'in-stream kernel timestamps (hipExtLaunchKernelGGL start/stop events, eager forward, queue pre-filled)'})
     rf.update(pmc_traffic(name))
     rf['per_kernel'] = {
         k: dict(roofline_of(v['flops'], v['bytes'], v['ms']), ms_per_step=round(v['ms'], 4), launches=v['launches'],
@@ -260,6 +262,50 @@ def cpu_baseline(cfg, flow, xy_np, B, budget_s=20.0):
             'bits_per_dim_ref': loss64 / (math.log(2) * H * Wd * cfg.x_d)}
 
 
+def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
+    """images/s of cFlow.train_step (conv_cINN_make_model.py:1850-1880) on the bench batch: every
+    step = cnf_flow_forward_train + cnf_nll + the 5-float loss all-reduce + cnf_flow_backward + the
+    gradient all-reduce (N>1) + Keras Adam + cnf_pack_params, eager (one host sync per step for the
+    Mean trackers, as Keras)."""
+    from arl_conditional_normalizing_flows_amd.optimizers import Adam
+    flow.compile(Adam(3e-4))                       # conv_cINN.py:567
+    pg = True if dist is not None else None
+    for _ in range(args.warmup):
+        logs = flow.train_step(xy, process_group=pg)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        logs = flow.train_step(xy, process_group=pg)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    if rank == 0:
+        fl_img, _by, _n = algorithmic_per_image(flow, B)
+        ms = el / args.steps * 1e3
+        # backward = recompute (1x the forward convs) + data and weight gradients (2x): 4x forward FLOPs
+        tf = 4.0 * fl_img * G / (ms / 1e3) / 1e12 / world
+        out = {'metric': f'images/sec NLL train step (fwd + bwd + Adam), {cfg.name}',
+               'value': round(G * args.steps / el, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
+               'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': scaling,
+               'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic', 'config': {
+                   'workload': f'{cfg.name}: cFlow.train_step(xy), xy {list(cfg.io_shape)}, {B} images per GPU',
+                   'model': f'cFlow {cfg.name}', 'global_batch': G, 'per_gpu_batch': B, 'seq_len': None,
+                   'parallelism': f'dp{world} (batch shards, gradient all-reduce)'},
+               'alg_tflops_per_gpu': round(tf, 3), 'mfma_frac': round(tf / FP32_MFMA_TFLOPS, 4),
+               'loss': logs['loss']}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -270,6 +316,10 @@ def main():
     ap.add_argument('--global-batch', type=int, default=0,
                     help='strong scaling: shard this many images over the ranks (default: weak scaling, '
                          'the per-GPU batch on every rank)')
+    ap.add_argument('--mode', choices=['forward', 'train'], default='forward',
+                    help='train: the NLL training step (cFlow.train_step: forward with saved layer inputs, '
+                         'backward, gradient all-reduce when N>1, Keras Adam, weight repack) instead of the '
+                         'fwd+logdet metric step; prints its own JSON line')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -312,6 +362,8 @@ def main():
     # one seeded global batch, sliced per rank
     xy_np = synth(cfg, G, 1000)[lo:hi].copy()
     xy = torch.from_numpy(xy_np).to(dev)
+    if args.mode == 'train':
+        return train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling)
     red = torch.empty(5, device=dev)
     zy = torch.empty_like(xy)
     ld = torch.empty(B, device=dev)
@@ -414,7 +466,7 @@ def main():
             launches = measure_in_stream(flow, local_step)
             roof, per_k = roofline_for(launches)
             tot = sum(d['ms'] for d in per_k.values())
-            print(f'# per-kernel (in-stream HIP events): total {tot:.3f} ms/step', file=sys.stderr)
+            print(f'# per-kernel (in-stream kernel timestamps): total {tot:.3f} ms/step', file=sys.stderr)
             for nm, fl, by, t_ms in launches:
                 print(f'#  {nm:34s} {t_ms * 1e3:8.2f} us  {fl / max(t_ms, 1e-9) / 1e9:7.2f} TF/s '
                       f'{by / max(t_ms, 1e-9) / 1e6:8.1f} GB/s', file=sys.stderr)

@@ -275,10 +275,11 @@ int cnf_plan_num_recorded_launches(const cnf_plan* plan);
 int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int name_cap,
                                   double* flops, double* bytes);
 int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream);
-/* In-stream launch timing: while on, every launch of a forward/inverse call is
- * bracketed by a HIP event pair on the call's stream (eager calls only, not
- * inside graph capture); cnf_plan_launch_time_ms then gives launch i's GPU
- * duration in its place in the sequence (waits for it). */
+/* In-stream launch timing: while on, every kernel of a forward/inverse call is
+ * dispatched with hipExtLaunchKernelGGL start/stop events, which receive the
+ * kernel's own begin/end timestamps (eager calls only, not inside graph
+ * capture); cnf_plan_launch_time_ms then gives launch i's GPU duration in its
+ * place in the sequence (waits for it; 0 for a launch that is not a kernel). */
 int cnf_plan_set_launch_timing(cnf_plan* plan, int on);
 int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms);
 

@@ -11,3 +11,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -2 $out/tests.log
 timeout -k 10 400 python bench.py > $out/bench.json 2> $out/bench.err || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
+if [ -n "$CNF_ROUND_TRAIN" ]; then
+  timeout -k 10 300 python bench.py --mode train --steps 5 --warmup 2 > $out/train.json 2> $out/train.err || { echo "train bench failed"; tail -20 $out/train.err; exit 1; }
+  cat $out/train.json
+fi

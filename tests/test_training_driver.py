@@ -257,3 +257,66 @@ def test_pretrain_on_noise(gpu):
     losses = hist.history['loss']
     assert len(losses) == 3 and all(math.isfinite(v) for v in losses)
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.gpu
+def test_fit_trajectory_matches_float64_oracle(gpu):
+    """(f3) end to end: training.fit over the HIP train_step for 2 epochs of one batch (2 Keras Adam
+    steps, conv_cINN.py:567 / :617) against the same loop in float64 — torch autograd over the
+    oracle's op-for-op graph (oracle/cflow_torch_cpu.py) and the Keras Adam restatement.
+
+    Adam normalises each gradient element by its own magnitude, so an element whose gradient is
+    near 0 (below the fp32 gradient's error) may legitimately move by up to +-lr per step in either
+    direction; every other element must land on the float64 trajectory to 1e-3 lr (the update's
+    sensitivity to the gradient's relative error) plus fp32 rounding of the parameter. The stable
+    elements must be the large majority."""
+    import math
+    from arl_conditional_normalizing_flows_amd.config import PRESETS
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    from arl_conditional_normalizing_flows_amd.optimizers import Adam
+    from oracle.cflow_np import OracleCFlow, synthetic_class_batch
+    from oracle.cflow_torch_cpu import TorchCPUFlow
+    cfg = PRESETS['small']
+    kw = cfg.kwargs()
+    ora = OracleCFlow(**kw)
+    P0 = ora.init_params(12)
+    H, W, _ = cfg.io_shape
+    xy = synthetic_class_batch(3, H, W, cfg.x_d, seed=13)
+    lr = 1e-3
+    flow = cFlow(**kw, device=gpu)
+    flow.set_weights(P0)
+    flow.compile(Adam(learning_rate=lr))
+    T.fit(flow, [torch.from_numpy(xy).to(gpu)], epochs=2)
+    got = flow.params.detach().cpu().numpy().astype(np.float64)
+    # float64 reference loop
+    tf = TorchCPUFlow(**kw)
+    names = [n for n, _o, _s in flow.param_specs]
+    p = {n: np.asarray(P0[n], np.float64) for n in names}
+    m = {n: np.zeros_like(p[n]) for n in names}
+    v = {n: np.zeros_like(p[n]) for n in names}
+    gabs = {n: [] for n in names}
+    for t in (1, 2):
+        Tp = {n: torch.tensor(p[n], requires_grad=True) for n in names}
+        tf.log_loss(torch.from_numpy(np.asarray(xy, np.float64)), Tp)[0].backward()
+        alpha = lr * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        for n in names:
+            g = Tp[n].grad.numpy()
+            gabs[n].append(np.abs(g))
+            m[n] = m[n] + (g - m[n]) * 0.1
+            v[n] = v[n] + (g * g - v[n]) * 0.001
+            p[n] = p[n] - alpha * m[n] / (np.sqrt(v[n]) + 1e-7)
+    n_stable = n_all = 0
+    worst = 0.0
+    for n, o, s in flow.param_specs:
+        size = int(np.prod(s)) if s else 1
+        ref = p[n].reshape(-1)
+        d = np.abs(got[o:o + size] - ref)
+        gmx = max(float(np.max(gabs[n][0])), 1e-30)
+        stable = np.minimum(gabs[n][0], gabs[n][1]).reshape(-1) > 1e-3 * gmx
+        tol = np.where(stable, 1e-3 * lr + 1e-6 * np.abs(ref), 2 * 2 * lr + 1e-6 * np.abs(ref))
+        assert np.all(d <= tol), (n, float(np.max(d / tol)))
+        worst = max(worst, float(np.max(d / tol)))
+        n_stable += int(stable.sum())
+        n_all += size
+    print(f'fit trajectory: {n_stable}/{n_all} stable elements, worst deviation / tolerance {worst:.3f}')
+    assert n_stable >= 0.8 * n_all   # measured 84 % (LN gamma/beta of pixels the batch barely reaches)
