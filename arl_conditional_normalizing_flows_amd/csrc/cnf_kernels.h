@@ -332,14 +332,22 @@ struct WGradArgs {
     int H, W, taps, dil, B, chunks, chunk_px;
 };
 void launch_wgrad(const WGradArgs& a, hipStream_t st);
+// k_wgrad_band (the MFMA weight gradient): partial rows per launch (<= WGRAD_MAX_CHUNKS), each
+// [taps][CI][CO] weights then [CO] bias, and its LDS bytes
+constexpr int WGRAD_MAX_CHUNKS = 256;
+int wgrad_band_chunks(int B, int H, int W, int taps, int CI, int CO);
+size_t wgrad_band_lds(int H, int W, int taps, int dil, int CI, int CO);
+bool train_valu_kernels();   // CNF_TRAIN_VALU=1: the register-blocked VALU convolutions (A/B)
 // dparams[map[i]] += sum_c part[c][i] for i < n (map[i] >= 0)
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st);
 void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st);
 // LN + LeakyReLU backward: dx (=|+=) d/dx of LN(LeakyReLU(x)) given dxo = dL/d(LN output);
 // dgamma/dbeta (+=) per element; stats == null: LeakyReLU backward only
+// (the batch runs in LNB_SLICES slices: scratch holds their [2][LNB_SLICES][n] gamma / beta partials)
+constexpr int LNB_SLICES = 8;
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        hipStream_t st);
+                        float* scratch, hipStream_t st);
 struct CoupBwArgs {
     const float* u;           // layer input [B][H][W][D]
     const float* dv;          // dL/dv

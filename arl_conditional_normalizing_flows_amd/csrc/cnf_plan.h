@@ -145,7 +145,7 @@ struct TrainLayout {
     size_t bw = 0;
     size_t ys[2] = {}, t1s[2] = {}, t2s[2] = {}, so[2] = {}, dso[2] = {}, stats[2] = {};
     size_t dy = 0, dln = 0, dbuf = 0, dt1 = 0, dc = 0, dt2 = 0, u1c = 0, du1c = 0, duv[2] = {}, dzy = 0;
-    size_t lnsum = 0, wpart = 0, bpart = 0, dwpart = 0;
+    size_t lnsum = 0, wpart = 0, bpart = 0, dwpart = 0, lnpart = 0;
 };
 
 struct Plan {

@@ -98,9 +98,12 @@ TrainLayout Plan::train_layout(int B) const {
     for (int k = 0; k < 2; k++) T.duv[k] = take(Bz * L.n_uv * 4);
     T.dzy = take(Bz * L.n_uv * 4);
     T.lnsum = take(Bz * 2 * 8);
+    // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
+    T.lnpart = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
     int chunks = 1;
     for (const Coupling& c : couplings) chunks = std::max(chunks, wgrad_chunks(B, c.hc * c.wc));
-    T.wpart = take((size_t)chunks * m_dense * 4);
+    // the MFMA weight gradient writes up to WGRAD_MAX_CHUNKS rows of [weights | bias]
+    T.wpart = take((size_t)std::max(chunks, WGRAD_MAX_CHUNKS) * (m_dense + m_co) * 4);
     T.bpart = take((size_t)chunks * m_co * 4);
     T.dwpart = take(Bz * std::max(1, L.ld_parts) * 8);
     T.total = off;
@@ -207,19 +210,30 @@ void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int
     a.taps = pc.taps;
     a.dil = dil;
     a.B = E.B;
-    a.chunks = wgrad_chunks(E.B, h * w);
-    const long long total = (long long)E.B * h * w;
-    a.chunk_px = (int)(((total + a.chunks - 1) / a.chunks + 15) / 16 * 16);
-    launch_wgrad(a, E.st);
     const int64_t* map = E.p.dev_bw_map;
-    launch_grad_scatter(a.part, a.chunks, (long long)pc.taps * cin * cout, map + pc.dw, E.dparams, E.st);
-    launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
+    const long long nw = (long long)pc.taps * cin * cout;
+    if (train_valu_kernels()) {
+        a.chunks = wgrad_chunks(E.B, h * w);
+        const long long total = (long long)E.B * h * w;
+        a.chunk_px = (int)(((total + a.chunks - 1) / a.chunks + 15) / 16 * 16);
+        launch_wgrad(a, E.st);
+        launch_grad_scatter(a.part, a.chunks, nw, map + pc.dw, E.dparams, E.st);
+        launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
+        return;
+    }
+    // k_wgrad_band: rows of [weights | bias]; the dense image keeps the bias right after the
+    // weights (pc.db == pc.dw + taps * cin * cout), so one scatter reduces both
+    a.chunks = wgrad_band_chunks(E.B, h, w, pc.taps, cin, cout);
+    launch_wgrad(a, E.st);
+    if (pc.db != pc.dw + nw) throw std::logic_error("dense image: bias not after the weights");
+    launch_grad_scatter(a.part, a.chunks, nw + cout, map + pc.dw, E.dparams, E.st);
 }
 
 void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
             int64_t g_off, int64_t b_off) {
     launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum), n, E.B, 1, dx, accumulate,
-                       ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr, E.st);
+                       ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr,
+                       E.at<float>(E.T.lnpart), E.st);
 }
 
 void coupling_backward(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {

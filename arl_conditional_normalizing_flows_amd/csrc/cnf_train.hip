@@ -17,7 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "cnf_device.h"
 #include "cnf_kernels.h"
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void k_tconv(TConvArgs a) {
 // K order inside a group is permuted identically on both operands, so the sum is the conv's.
 // ------------------------------------------------------------------------------------------------
 template <int NR, bool VEC>
-__global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a) {
+__global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     extern __shared__ __attribute__((aligned(16))) float wsm[];
     constexpr int NS = 16 * NR;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
@@ -148,50 +150,75 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a) {
     f4 acc[NR];
 #pragma unroll
     for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
-    const int nw = G * 16 * NS;
-    for (int tap = 0; tap < a.taps; tap++) {
-        const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
-        const int r = pr + a.sgn * a.dil * dr, c = pc + a.sgn * a.dil * dc;
-        const bool sv = pav && r >= 0 && r < a.H && c >= 0 && c < a.W;
-        const size_t q = sv ? (size_t)r * a.W + c : 0;
-        __syncthreads();   // the previous tap's B reads are done
+    const int nw = G * 16 * NS;   // weight floats of one tap
+    auto stage_w = [&](int tap, float* dst) {
         for (int e = threadIdx.x; e < nw; e += 256) {
             const int s4 = e & 3, j = (e >> 2) % NS, gq = (e >> 2) / NS;   // gq = 4g + kq'
             const int k = 4 * gq + s4, n = n0 + j;
-            wsm[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+            dst[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
         }
-        __syncthreads();
-        for (int g = 0; g < G; g++) {
-            const int k0 = 16 * g + 4 * kq;
-            f4 x = f4{0.f, 0.f, 0.f, 0.f};
-            if (sv) {
-                const size_t gi = q * a.in_cs + k0;
-                if (VEC) {
-                    if (k0 < a.K) {
-                        x = *reinterpret_cast<const f4*>(inb + gi);
-                        if (ln) {
-                            const f4 gm = *reinterpret_cast<const f4*>(a.gamma + a.in_off + gi);
-                            const f4 bt = *reinterpret_cast<const f4*>(a.beta + a.in_off + gi);
+    };
+    // A operand of flat step it = tap * G + g: raw channels 16g + 4kq .. +3 of the lane's shifted pixel
+    // (+ its LN gamma / beta), loaded one step ahead so the loads overlap the previous step's MFMAs
+    auto load = [&](int it, f4& x, f4& gm, f4& bt) -> bool {
+        const int tap = it / G, g = it - tap * G;
+        const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
+        const int r = pr + a.sgn * a.dil * dr, c = pc + a.sgn * a.dil * dc;
+        const int k0 = 16 * g + 4 * kq;
+        const bool sv = pav && r >= 0 && r < a.H && c >= 0 && c < a.W && k0 < a.K;
+        x = gm = bt = f4{0.f, 0.f, 0.f, 0.f};
+        if (!sv) return false;
+        const size_t gi = ((size_t)r * a.W + c) * a.in_cs + k0;
+        if (VEC) {
+            x = *reinterpret_cast<const f4*>(inb + gi);
+            if (ln) {
+                gm = *reinterpret_cast<const f4*>(a.gamma + a.in_off + gi);
+                bt = *reinterpret_cast<const f4*>(a.beta + a.in_off + gi);
+            }
+        } else {
 #pragma unroll
-                            for (int j = 0; j < 4; j++) x[j] = (lrelu(x[j]) - mu) * rs * gm[j] + bt[j];
-                        } else if (a.act) {
-#pragma unroll
-                            for (int j = 0; j < 4; j++) x[j] = lrelu(x[j]);
-                        }
+            for (int j = 0; j < 4; j++)
+                if (k0 + j < a.K) {
+                    x[j] = inb[gi + j];
+                    if (ln) {
+                        gm[j] = a.gamma[a.in_off + gi + j];
+                        bt[j] = a.beta[a.in_off + gi + j];
                     }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        if (k0 + j < a.K) x[j] = act_load(inb[gi + j], a.act, a.stats, a.gamma, a.beta, b, a.in_off + gi + j);
                 }
-            }
-            const f4* bw = reinterpret_cast<const f4*>(wsm) + (size_t)(4 * g + kq) * NS + i16;
+        }
+        return true;
+    };
+    if (all_taps) {   // every tap's weights staged once
+        for (int tap = 0; tap < a.taps; tap++) stage_w(tap, wsm + (size_t)tap * nw);
+    }
+    const int total = a.taps * G;
+    f4 xn, gn, bn;
+    bool vn = load(0, xn, gn, bn);
+    for (int it = 0; it < total; it++) {
+        const int tap = it / G, g = it - tap * G;
+        f4 x = xn, gm = gn, bt = bn;
+        const bool v = vn;
+        if (g == 0 && !all_taps) {
+            __syncthreads();   // the previous tap's B reads are done
+            stage_w(tap, wsm);
+        }
+        if (it + 1 < total) vn = load(it + 1, xn, gn, bn);
+        if (g == 0 && (!all_taps ? true : tap == 0)) __syncthreads();
+        if (v) {
+            if (ln) {
 #pragma unroll
-            for (int m = 0; m < NR; m++) {
-                const f4 bv = bw[16 * m];
+                for (int j = 0; j < 4; j++) x[j] = (lrelu(x[j]) - mu) * rs * gm[j] + bt[j];
+            } else if (a.act) {
 #pragma unroll
-                for (int s = 0; s < 4; s++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], bv[s], acc[m], 0, 0, 0);
+                for (int j = 0; j < 4; j++) x[j] = lrelu(x[j]);
             }
+        }
+        const f4* bw = reinterpret_cast<const f4*>(wsm + (all_taps ? (size_t)tap * nw : 0)) + (size_t)(4 * g + kq) * NS + i16;
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const f4 bv = bw[16 * m];
+#pragma unroll
+            for (int s = 0; s < 4; s++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], bv[s], acc[m], 0, 0, 0);
         }
     }
     // acc[m][rr] = out[pixel p0 + 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
@@ -213,6 +240,145 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_tconv_band: 3x3 (dilation <= 2) convolution, forward or transposed, for images of width <= 64.
+// A workgroup owns TH full rows (TH * W <= 64 pixels, 16 per wave) x 16*NR output channels of one
+// image. Per 64-channel chunk of K the input band (rows r0 - d .. r0 + TH + d, columns -d .. W + d)
+// is staged into LDS once, LN + LeakyReLU applied once per element and zero padding written, so
+// the nine taps read their A operands from LDS (one float4 per lane and group) instead of
+// re-reading global memory per tap; the chunk's weights for every tap sit in LDS as in
+// k_tconv_mfma ([tap][g][kq][j][s]).
+// ------------------------------------------------------------------------------------------------
+constexpr int TB_KS = 68;   // band pixel stride (floats)
+
+template <int NR>
+__global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all_taps) {
+    extern __shared__ __attribute__((aligned(16))) float tsm[];
+    constexpr int NS = 16 * NR;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int H = a.H, W = a.W, npx = H * W, b = blockIdx.y;
+    const int r0 = blockIdx.x * TH, n0 = blockIdx.z * NS;
+    const int d = a.dil, BW = W + 2 * d, BH = TH + 2 * d;
+    float* band = tsm;                                   // [BH * BW][TB_KS]
+    float* wl = tsm + (size_t)BH * BW * TB_KS;           // [tap][16 gq][NS][4] of the chunk (all_taps) or one tap
+    const int p = wave * 16 + i16;                       // the lane's A pixel inside the tile
+    const int tr = p / W, tc = p - tr * W;
+    const bool pav = p < TH * W && r0 + tr < H;
+    const float* inb = a.in + (size_t)b * npx * a.in_cs + a.in_off;
+    const bool ln = a.stats != nullptr;
+    const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+    f4 acc[NR];
+#pragma unroll
+    for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+    const bool vq = (a.in_cs & 3) == 0 && (a.in_off & 3) == 0;
+    for (int kc = 0; kc < a.K; kc += 64) {
+        // quads up to the 16-channel group boundary (the MFMA reads whole groups: zeros past K)
+        const int KC = min(64, a.K - kc), cq = ((KC + 15) >> 4) * 4;
+        __syncthreads();   // the previous chunk's reads are done
+        // band: quads of KC channels (zero beyond KC / outside the image), LN on load
+        const int nq = BH * BW * cq;
+        for (int e0 = threadIdx.x; e0 < nq; e0 += 256 * 4) {
+            f4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + 256 * u;
+                v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                if (e < nq) {
+                    const int q = e % cq, pb = e / cq;
+                    const int br = pb / BW, bc = pb - br * BW;
+                    const int r = r0 - d + br, c = bc - d;
+                    if (r >= 0 && r < H && c >= 0 && c < W) {
+                        const int k = kc + 4 * q;
+                        const size_t gi = ((size_t)r * W + c) * a.in_cs + k;
+                        f4 x = f4{0.f, 0.f, 0.f, 0.f}, gm = f4{1.f, 1.f, 1.f, 1.f}, bt = f4{0.f, 0.f, 0.f, 0.f};
+                        if (vq && k + 4 <= a.K) {
+                            x = *reinterpret_cast<const f4*>(inb + gi);
+                            if (ln) {
+                                gm = *reinterpret_cast<const f4*>(a.gamma + a.in_off + gi);
+                                bt = *reinterpret_cast<const f4*>(a.beta + a.in_off + gi);
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                if (k + j < a.K) {
+                                    x[j] = inb[gi + j];
+                                    if (ln) {
+                                        gm[j] = a.gamma[a.in_off + gi + j];
+                                        bt[j] = a.beta[a.in_off + gi + j];
+                                    }
+                                }
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const float t = (a.act || ln) ? lrelu(x[j]) : x[j];
+                            v[u][j] = k + j < a.K ? (ln ? (t - mu) * rs * gm[j] + bt[j] : t) : 0.f;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = e0 + 256 * u;
+                if (e < nq) *reinterpret_cast<f4*>(band + (size_t)(e / cq) * TB_KS + 4 * (e % cq)) = v[u];
+            }
+        }
+        // weights of the chunk: [tap][gq = 4g + kq'][j][s], k = kc + 16g + 4kq' + s (every tap at once
+        // when they fit next to the band, else one tap at a time)
+        auto stage_w = [&](int t0, int nt) {
+            const int nwc = nt * 16 * NS * 4;
+            for (int e = threadIdx.x; e < nwc; e += 256) {
+                const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * 16 + gq
+                const int tap = t0 + (rest >> 4), gq = rest & 15;
+                const int k = kc + 4 * gq + s4, n = n0 + j;
+                wl[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+            }
+        };
+        if (all_taps) stage_w(0, 9);
+        __syncthreads();
+        const int G = (KC + 15) >> 4;
+#pragma unroll 1
+        for (int tap = 0; tap < 9; tap++) {
+            if (!all_taps) {
+                if (tap > 0) __syncthreads();   // the previous tap's weight reads are done
+                stage_w(tap, 1);
+                __syncthreads();
+            }
+            const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+            const int br = tr + d + a.sgn * d * dr, bc = tc + d + a.sgn * d * dc;
+            const float* ap = band + (size_t)(br * BW + bc) * TB_KS + 4 * kq;
+            const f4* wp = reinterpret_cast<const f4*>(wl) + (size_t)(all_taps ? tap : 0) * 16 * NS + (size_t)kq * NS + i16;
+            for (int g = 0; g < G; g++) {
+                const f4 x = pav ? *reinterpret_cast<const f4*>(ap + 16 * g) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < NR; m++) {
+                    const f4 bv = wp[(size_t)4 * g * NS + 16 * m];
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; s4++)
+                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s4], bv[s4], acc[m], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // acc[m][rr] = out[tile pixel 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+        const int q = wave * 16 + 4 * kq + rr;
+        const int orow = r0 + q / W, ocol = q % W;
+        if (q >= TH * W || orow >= H) continue;
+        const size_t ob = ((size_t)b * npx + (size_t)orow * W + ocol) * a.out_cs + a.out_off;
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const int n = n0 + 16 * m + i16;
+            if (n >= a.N) continue;
+            float v = acc[m][rr];
+            if (a.bias) v += a.bias[n];
+            if (a.res) v += a.res[ob + n];
+            if (a.accumulate) v += a.out[ob + n];
+            a.out[ob + n] = v;
+        }
+    }
+}
+
 static bool train_valu() {
     static const bool v = [] {   // A/B knob: the register-blocked VALU kernels
         const char* e = std::getenv("CNF_TRAIN_VALU");
@@ -220,23 +386,48 @@ static bool train_valu() {
     }();
     return v;
 }
+bool train_valu_kernels() { return train_valu(); }
 
 void launch_tconv(const TConvArgs& a, hipStream_t st) {
     const int npx = a.H * a.W;
+    static const bool band_off = [] {   // A/B knob: no band-staged 3x3 kernel
+        const char* e = std::getenv("CNF_TCONV_BAND");
+        return e && std::atoi(e) == 0;
+    }();
+    if (!train_valu() && !band_off && a.taps == 9 && a.dil <= 2 && a.W <= 64 && a.W >= 1) {
+        const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
+        const int NS = 16 * nr;
+        const int TH = std::max(1, std::min(a.H, 64 / a.W));
+        const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
+        const size_t w1 = (size_t)16 * NS * 4 * 4;   // one tap of a 64-channel chunk
+        const int all_taps = band + 9 * w1 <= 80 * 1024 ? 1 : 0;
+        const size_t lds = band + (all_taps ? 9 : 1) * w1;
+        if (lds <= 160 * 1024) {
+            const dim3 g((a.H + TH - 1) / TH, a.B, (a.N + NS - 1) / NS), blk(256);
+            if (nr == 1) hipLaunchKernelGGL(k_tconv_band<1>, g, blk, lds, st, a, TH, all_taps);
+            else if (nr == 2) hipLaunchKernelGGL(k_tconv_band<2>, g, blk, lds, st, a, TH, all_taps);
+            else if (nr == 3) hipLaunchKernelGGL(k_tconv_band<3>, g, blk, lds, st, a, TH, all_taps);
+            else hipLaunchKernelGGL(k_tconv_band<4>, g, blk, lds, st, a, TH, all_taps);
+            return;
+        }
+    }
     if (!train_valu()) {
         const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
         const int NS = 16 * nr;
         const int G = (a.K + 15) / 16;
-        const size_t lds = (size_t)G * 16 * NS * 4;
-        if (lds <= 64 * 1024) {
+        const size_t lds1 = (size_t)G * 16 * NS * 4;
+        if (lds1 <= 64 * 1024) {
+            // every tap's weights in LDS at once when they fit (no per-tap barriers), else per tap
+            const int all_taps = lds1 * a.taps <= 64 * 1024 ? 1 : 0;
+            const size_t lds = all_taps ? lds1 * a.taps : lds1;
             const bool vec = a.K % 4 == 0 && a.in_cs % 4 == 0 && a.in_off % 4 == 0;
             const dim3 g((npx + 63) / 64, a.B, (a.N + NS - 1) / NS), blk(256);
 #define CNF_TM(NR_)                                                                                   \
     if (nr == NR_) {                                                                                  \
         if (vec)                                                                                      \
-            hipLaunchKernelGGL((k_tconv_mfma<NR_, true>), g, blk, lds, st, a);                      \
+            hipLaunchKernelGGL((k_tconv_mfma<NR_, true>), g, blk, lds, st, a, all_taps);            \
         else                                                                                          \
-            hipLaunchKernelGGL((k_tconv_mfma<NR_, false>), g, blk, lds, st, a);                     \
+            hipLaunchKernelGGL((k_tconv_mfma<NR_, false>), g, blk, lds, st, a, all_taps);           \
         return;                                                                                       \
     }
             CNF_TM(1) CNF_TM(2) CNF_TM(3) CNF_TM(4)
@@ -421,48 +612,406 @@ __global__ __launch_bounds__(256) void k_wgrad_mfma(WGradArgs a) {
     if (do_bias && t < 64 && co0 + t < a.CO) a.bpart[(size_t)blockIdx.x * a.CO + co0 + t] = bacc;
 }
 
-void launch_wgrad(const WGradArgs& a, hipStream_t st) {
-    const dim3 g(a.chunks, a.taps, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
-    if (train_valu())
-        hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);
-    else
-        hipLaunchKernelGGL(k_wgrad_mfma, g, blk, 0, st, a);
+// ------------------------------------------------------------------------------------------------
+// k_wgrad_band: weight gradient of a 3x3 (TR = 3) or 1x1 (TR = 1) conv on MFMA with every tap of
+// one kernel row per workgroup. Work units are (image, band of RB rows); a workgroup of grid
+// column `chunk` takes units chunk, chunk + chunks, ... For each unit it stages the X rows its
+// tap row reads (dilation halo columns, zero padding, LN + LeakyReLU applied once per element)
+// and the dY rows into LDS, then runs K = the unit's pixels through the MFMAs: the B operand
+// (dY) is read once per k-step and shared by the TR taps. Wave w owns ci rows 16w.. of the
+// 64 x 64 (ci, co) tile: acc[t][m][r] = dW[tap row, t][ci 16w+4kq+r][co 16m+i16]. The bias
+// gradient (sum of dY) goes after the weights in the same partial row, so one scatter launch
+// reduces both.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ constexpr int wg_stride(int c) {   // LDS row stride == 16 (mod 32) floats
+    return ((c + 15) / 16 * 16) % 32 == 0 ? (c + 15) / 16 * 16 + 16 : (c + 15) / 16 * 16;
 }
 
-__global__ __launch_bounds__(256) void k_grad_scatter(const float* __restrict__ part, int chunks, long long n,
-                                                      const int64_t* __restrict__ map, float* __restrict__ dparams) {
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+template <int TR>
+__global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nunits, int abl) {
+    extern __shared__ __attribute__((aligned(16))) float wsm[];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int H = a.H, W = a.W, npx = H * W;
+    const int nco = (a.CO + 63) / 64;
+    const int ci0 = (blockIdx.z / nco) * 64, co0 = (blockIdx.z % nco) * 64;
+    const int CIB = min(64, a.CI - ci0), COB = min(64, a.CO - co0);
+    const int XS = wg_stride(CIB), DS = wg_stride(COB);
+    const int MB = (COB + 15) >> 4;   // 16-column blocks holding outputs
+    // waves -> (ci block, k slice): NCW ci blocks of 16 rows; the waves left over split the k-steps
+    // (pixel quads) of every unit and their partial sums are added at the end in a fixed order
+    const int NCW = (CIB + 15) >> 4, WPG = NCW == 1 ? 4 : NCW == 2 ? 2 : 1;
+    const int cw = wave % NCW, ks = wave / NCW;
+    const bool kact = ks < WPG;
+    const int hx = TR == 3 ? a.dil : 0;     // halo columns
+    const int WB = W + 2 * hx;
+    const int dr = TR == 3 ? (int)blockIdx.y - 1 : 0;
+    float* Xs = wsm;                          // [RB][WB][XS]
+    float* Ds = wsm + (size_t)RB * WB * XS;   // [RB][W][DS]
+    const bool do_bias = a.bpart != nullptr && blockIdx.y == (TR == 3 ? 1u : 0u) && ci0 == 0;
+    f4 acc[TR][4];
+#pragma unroll
+    for (int u = 0; u < TR; u++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[u][m] = f4{0.f, 0.f, 0.f, 0.f};
+    float bacc = 0.f;
+    const int bands = (H + RB - 1) / RB;
+    const bool ln = a.stats != nullptr;
+    const bool qx = (CIB & 3) == 0 && (a.x_cs & 3) == 0 && ((a.x_off + ci0) & 3) == 0;
+    const bool qd = (COB & 3) == 0 && (a.dy_cs & 3) == 0 && ((a.dy_off + co0) & 3) == 0;
+    for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
+        const int b = unit / bands, r0 = (unit - b * bands) * RB;
+        const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+        __syncthreads();   // the previous unit's LDS reads are done
+        // X rows r0 + dil*dr .. (+RB), columns -hx .. W + hx; dY rows r0 .. r0 + RB. Channel quads
+        // (float4 loads, 8 quads in flight per thread) when the windows are quad aligned.
+        const float* xb = a.x + (size_t)b * npx * a.x_cs + a.x_off + ci0;
+        const float* db = a.dy + (size_t)b * npx * a.dy_cs + a.dy_off + co0;
+        if (abl & 1) {
+        } else if (qx) {
+            const int cq = CIB >> 2, nxq = RB * WB * cq;
+            for (int e0 = t; e0 < nxq; e0 += 256 * 8) {
+                f4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                    if (e < nxq) {
+                        const int c = (e % cq) * 4, pb = e / cq;
+                        const int br = pb / WB, bc = pb - br * WB;
+                        const int r = r0 + a.dil * dr + br, cc = bc - hx;
+                        if (r >= 0 && r < H && cc >= 0 && cc < W) {
+                            const size_t gi = ((size_t)r * W + cc) * a.x_cs + c;
+                            const f4 xv = *reinterpret_cast<const f4*>(xb + gi);
+                            if (ln) {
+                                const size_t gg = gi + a.x_off + ci0;
+                                const f4 gmv = *reinterpret_cast<const f4*>(a.gamma + gg);
+                                const f4 btv = *reinterpret_cast<const f4*>(a.beta + gg);
+#pragma unroll
+                                for (int j = 0; j < 4; j++) v[u][j] = (lrelu(xv[j]) - mu) * rs * gmv[j] + btv[j];
+                            } else {
+#pragma unroll
+                                for (int j = 0; j < 4; j++) v[u][j] = a.act ? lrelu(xv[j]) : xv[j];
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    if (e < nxq) *reinterpret_cast<f4*>(Xs + (e / cq) * XS + (e % cq) * 4) = v[u];
+                }
+            }
+        } else {
+            const int nx = RB * WB * CIB;
+            for (int e0 = t; e0 < nx; e0 += 256 * 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    v[u] = 0.f;
+                    if (e < nx) {
+                        const int c = e % CIB, pb = e / CIB;
+                        const int br = pb / WB, bc = pb - br * WB;
+                        const int r = r0 + a.dil * dr + br, cc = bc - hx;
+                        if (r >= 0 && r < H && cc >= 0 && cc < W) {
+                            const size_t gi = ((size_t)r * W + cc) * a.x_cs + c;
+                            const float xv = xb[gi];
+                            if (ln) {
+                                const size_t gg = gi + a.x_off + ci0;
+                                v[u] = (lrelu(xv) - mu) * rs * a.gamma[gg] + a.beta[gg];
+                            } else {
+                                v[u] = a.act ? lrelu(xv) : xv;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    if (e < nx) Xs[(e / CIB) * XS + e % CIB] = v[u];
+                }
+            }
+        }
+        if (abl & 1) {
+        } else if (qd) {
+            const int cq = COB >> 2, ndq = RB * W * cq;
+            for (int e0 = t; e0 < ndq; e0 += 256 * 8) {
+                f4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                    if (e < ndq) {
+                        const int c = (e % cq) * 4, p = e / cq;
+                        if (r0 + p / W < H) v[u] = *reinterpret_cast<const f4*>(db + ((size_t)r0 * W + p) * a.dy_cs + c);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    if (e < ndq) *reinterpret_cast<f4*>(Ds + (e / cq) * DS + (e % cq) * 4) = v[u];
+                }
+            }
+        } else {
+            const int nd = RB * W * COB;
+            for (int e0 = t; e0 < nd; e0 += 256 * 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    v[u] = 0.f;
+                    if (e < nd) {
+                        const int c = e % COB, p = e / COB;
+                        if (r0 + p / W < H) v[u] = db[((size_t)r0 * W + p) * a.dy_cs + c];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int e = e0 + 256 * u;
+                    if (e < nd) Ds[(e / COB) * DS + e % COB] = v[u];
+                }
+            }
+        }
+        {   // zero the dY rows past the unit's last pixel up to the next multiple of 4
+            const int nk = RB * W, nk4 = (nk + 3) & ~3;
+            for (int e = t; e < (nk4 - nk) * DS; e += 256) Ds[(size_t)nk * DS + e] = 0.f;
+        }
+        __syncthreads();
+        // K = the unit's pixels, 4 per k-step: lane (i16, kq) reads pixel s + kq = (pr, pc), tracked
+        // incrementally (W >= 4: at most one row wrap per step, no division); past the unit's last
+        // pixel dY is zero (padded rows) and X any staged value
+        if (kact && !(abl & 2)) {   // column blocks past the outputs have nothing to compute
+            const int nk = RB * W, nk4 = (nk + 3) & ~3;
+            int pr = 0, pc = kq + 4 * ks;
+            while (pc >= W) {
+                pc -= W;
+                pr++;
+            }
+            const float* xl = Xs + 16 * cw + i16;
+            const float* dl = Ds + (size_t)kq * DS + i16;
+            for (int s = 4 * ks; s < nk4; s += 4 * WPG) {
+                const int xo = s + kq < nk ? (pr * WB + pc) * XS : 0;
+                float bv[4];
+#pragma unroll
+                for (int m = 0; m < 4; m++) bv[m] = m < MB ? dl[s * DS + 16 * m] : 0.f;
+#pragma unroll
+                for (int u = 0; u < TR; u++) {
+                    const float av = xl[xo + u * hx * XS];
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        if (m < MB) acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[m], acc[u][m], 0, 0, 0);
+                }
+                pc += 4 * WPG;
+                while (pc >= W) {
+                    pc -= W;
+                    pr++;
+                }
+            }
+        }
+        if (do_bias && (t & 63) < COB) {   // 4 interleaved pixel slices per column
+            const int nk = RB * W;
+            for (int p = t >> 6; p < nk; p += 4) bacc += Ds[p * DS + (t & 63)];
+        }
+    }
+    if (do_bias) {   // fixed-order sum of the 4 slices (deterministic)
+        __syncthreads();
+        Ds[t] = bacc;
+        __syncthreads();
+        if (t < 64) bacc = Ds[t] + Ds[t + 64] + Ds[t + 128] + Ds[t + 192];
+    }
+    if (WPG > 1) {   // k slices of one ci block: slice 0 adds the others' sums, in slice order
+        float* red = wsm;   // [ks][cw][TR * 16][64 lanes]
+        __syncthreads();
+        if (ks > 0 && kact) {
+#pragma unroll
+            for (int u = 0; u < TR; u++)
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        red[((size_t)(wave * TR + u) * 16 + m * 4 + r) * 64 + lane] = acc[u][m][r];
+        }
+        __syncthreads();
+        if (ks == 0) {
+            for (int k2 = 1; k2 < WPG; k2++) {
+                const int w2 = k2 * NCW + cw;
+#pragma unroll
+                for (int u = 0; u < TR; u++)
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) acc[u][m][r] += red[((size_t)(w2 * TR + u) * 16 + m * 4 + r) * 64 + lane];
+            }
+        }
+    }
+    // partial row of this chunk: [taps][CI][CO] weights, then [CO] bias
+    float* part = a.part + (size_t)blockIdx.x * ((size_t)a.taps * a.CI * a.CO + a.CO);
+#pragma unroll
+    for (int u = 0; u < TR; u++) {
+        const int tap = TR == 3 ? (int)blockIdx.y * 3 + u : 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int ci = ci0 + 16 * cw + 4 * kq + r;
+            if (ks != 0 || ci >= ci0 + CIB) continue;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const int co = co0 + 16 * m + i16;
+                if (co < a.CO) part[((size_t)tap * a.CI + ci) * a.CO + co] = acc[u][m][r];
+            }
+        }
+    }
+    if (do_bias && t < COB) part[(size_t)a.taps * a.CI * a.CO + co0 + t] = bacc;
+}
+
+// rows per work unit (about 128 pixels) and the unit count of a wgrad launch
+static void wgrad_units(const WGradArgs& a, int& RB, int& nunits) {
+    RB = a.W >= 128 ? 1 : 128 / a.W;
+    if (RB > a.H) RB = a.H;
+    if (RB < 1) RB = 1;
+    nunits = a.B * ((a.H + RB - 1) / RB);
+}
+
+int wgrad_band_chunks(int B, int H, int W, int taps, int CI, int CO) {
+    WGradArgs a{};
+    a.B = B;
+    a.H = H;
+    a.W = W;
+    int RB, nunits;
+    wgrad_units(a, RB, nunits);
+    const int blocks = ((CI + 63) / 64) * ((CO + 63) / 64) * (taps == 9 ? 3 : 1);
+    int c = (768 + blocks - 1) / blocks;   // three 4-wave workgroups per CU
+    if (c > WGRAD_MAX_CHUNKS) c = WGRAD_MAX_CHUNKS;
+    if (c > nunits) c = nunits;
+    return c < 1 ? 1 : c;
+}
+
+size_t wgrad_band_lds(int H, int W, int taps, int dil, int CI, int CO) {
+    WGradArgs a{};
+    a.B = 1;
+    a.H = H;
+    a.W = W;
+    int RB, nunits;
+    wgrad_units(a, RB, nunits);
+    const int hx = taps == 9 ? dil : 0;
+    const int CIB = CI < 64 ? CI : 64, COB = CO < 64 ? CO : 64;
+    const size_t stage = ((size_t)RB * (W + 2 * hx) * wg_stride(CIB) + (size_t)((RB * W + 3) & ~3) * wg_stride(COB)) * 4;
+    const size_t red = CIB <= 32 ? (size_t)4 * (taps == 9 ? 3 : 1) * 16 * 64 * 4 : 0;   // k-slice sums
+    return stage > red ? stage : red;
+}
+
+static int wg_abl() {   // diagnostics: CNF_WG_ABL bit 0 skips the X/dY staging, bit 1 the MFMA loop
+    static const int v = [] {
+        const char* e = std::getenv("CNF_WG_ABL");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+void launch_wgrad(const WGradArgs& a, hipStream_t st) {
+    if (train_valu()) {
+        const dim3 g(a.chunks, a.taps, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
+        hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);
+        return;
+    }
+    if (a.taps != 1 && a.taps != 9) throw std::invalid_argument("k_wgrad_band: taps must be 1 or 9");
+    if (a.W < 4) throw std::invalid_argument("k_wgrad_band: image width below 4");
+    int RB, nunits;
+    wgrad_units(a, RB, nunits);
+    const size_t lds = wgrad_band_lds(a.H, a.W, a.taps, a.dil, a.CI, a.CO);
+    if (lds > 160 * 1024) throw std::invalid_argument("k_wgrad_band: band exceeds the LDS budget");
+    const dim3 g(a.chunks, a.taps == 9 ? 3 : 1, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
+    if (a.taps == 9)
+        hipLaunchKernelGGL(k_wgrad_band<3>, g, blk, lds, st, a, RB, nunits, wg_abl());
+    else
+        hipLaunchKernelGGL(k_wgrad_band<1>, g, blk, lds, st, a, RB, nunits, wg_abl());
+}
+
+// 64 elements per workgroup, 16 slices of the chunk rows per element (lane / slice), 8 loads in
+// flight per thread, then a fixed-order LDS sum over the slices: deterministic
+__global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__ part, int chunks, long long n,
+                                                       const int64_t* __restrict__ map, float* __restrict__ dparams) {
+    __shared__ double red[16][64];
+    const int t = threadIdx.x, el = t & 63, sl = t >> 6;
+    const long long i = (long long)blockIdx.x * 64 + el;
+    double s = 0.0;
+    if (i < n) {
+        for (int c0 = sl; c0 < chunks; c0 += 16 * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int c = c0 + 16 * u;
+                v[u] = c < chunks ? part[(size_t)c * n + i] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += (double)v[u];
+        }
+    }
+    red[sl][el] = s;
+    __syncthreads();
+    if (sl == 0 && i < n) {
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) tot += red[k][el];
         const int64_t dst = map[i];
-        if (dst < 0) continue;
-        double s = 0.0;
-        for (int c = 0; c < chunks; c++) s += (double)part[(size_t)c * n + i];
-        dparams[dst] += (float)s;
+        if (dst >= 0) dparams[dst] += (float)tot;
     }
 }
 
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st) {
-    long long gx = (n + 255) / 256;
-    if (gx > 4096) gx = 4096;
-    if (gx < 1) gx = 1;
-    hipLaunchKernelGGL(k_grad_scatter, dim3((unsigned)gx), dim3(256), 0, st, part, chunks, n, map, dparams);
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_grad_scatter, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, part, chunks, n, map, dparams);
 }
 
 // ------------------------------------------------------------------------------------------------
 // LayerNorm (over H*W*C per image, keras epsilon 1e-3, biased variance) of LeakyReLU(x)
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ln_stats(const float* __restrict__ x, long long n, int act,
+// One 1024-thread workgroup per image: float4 loads, four in flight per thread and pass, fp64
+// accumulation (the per-image reductions are latency-bound otherwise: one dependent load per
+// thread and step).
+constexpr int LNT = 1024;
+
+__device__ __forceinline__ double block_sum_ln(double v, double* red) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < LNT / 64; w++) t += red[w];
+    return t;
+}
+
+__global__ __launch_bounds__(LNT) void k_ln_stats(const float* __restrict__ x, long long n, int act,
                                                   float* __restrict__ stats) {
-    __shared__ double red[4];
+    __shared__ double red[LNT / 64];
     const int b = blockIdx.x;
     const float* xb = x + (size_t)b * n;
     double s1 = 0.0, s2 = 0.0;
-    for (long long e = threadIdx.x; e < n; e += 256) {
-        const double h = act ? lrelu(xb[e]) : xb[e];
-        s1 += h;
-        s2 += h * h;
+    if ((n & 3) == 0) {
+        const f4* x4 = reinterpret_cast<const f4*>(xb);
+        const long long n4 = n >> 2;
+        for (long long i0 = threadIdx.x; i0 < n4; i0 += 4LL * LNT) {
+            f4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = i0 + u * LNT < n4 ? x4[i0 + u * LNT] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const double h = act ? lrelu(v[u][j]) : v[u][j];
+                    s1 += h;
+                    s2 += h * h;
+                }
+        }
+    } else {
+        for (long long e = threadIdx.x; e < n; e += LNT) {
+            const double h = act ? lrelu(xb[e]) : xb[e];
+            s1 += h;
+            s2 += h * h;
+        }
     }
-    s1 = block_sum256(s1, red);
-    s2 = block_sum256(s2, red);
+    s1 = block_sum_ln(s1, red);
+    s2 = block_sum_ln(s2, red);
     if (threadIdx.x == 0) {
         const double m = s1 / (double)n;
         double var = s2 / (double)n - m * m;
@@ -473,73 +1022,162 @@ __global__ __launch_bounds__(256) void k_ln_stats(const float* __restrict__ x, l
 }
 
 void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st) {
-    hipLaunchKernelGGL(k_ln_stats, dim3(B), dim3(256), 0, st, x, n, act, stats);
+    hipLaunchKernelGGL(k_ln_stats, dim3(B), dim3(LNT), 0, st, x, n, act, stats);
 }
 
 // per image: sums[b] = (sum g, sum g*xhat), g = dxo * gamma
-__global__ __launch_bounds__(256) void k_lnb_reduce(const float* __restrict__ x, const float* __restrict__ dxo,
+__global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x, const float* __restrict__ dxo,
                                                     const float* __restrict__ gamma, const float* __restrict__ stats,
                                                     long long n, double* __restrict__ sums) {
-    __shared__ double red[4];
+    __shared__ double red[LNT / 64];
     const int b = blockIdx.x;
     const float* xb = x + (size_t)b * n;
     const float* db = dxo + (size_t)b * n;
     const float mu = stats[2 * b], rs = stats[2 * b + 1];
     double sg = 0.0, sgh = 0.0;
-    for (long long e = threadIdx.x; e < n; e += 256) {
-        const float xh = (lrelu(xb[e]) - mu) * rs;
-        const float g = db[e] * gamma[e];
-        sg += g;
-        sgh += (double)g * xh;
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(gamma) & 15) == 0) {
+        const long long n4 = n >> 2;
+        const f4* x4 = reinterpret_cast<const f4*>(xb);
+        const f4* d4 = reinterpret_cast<const f4*>(db);
+        const f4* g4 = reinterpret_cast<const f4*>(gamma);
+        for (long long i0 = threadIdx.x; i0 < n4; i0 += 2LL * LNT) {
+            f4 xv[2], dv[2], gv[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const long long i = i0 + u * LNT;
+                const bool ok = i < n4;
+                xv[u] = ok ? x4[i] : f4{0.f, 0.f, 0.f, 0.f};
+                dv[u] = ok ? d4[i] : f4{0.f, 0.f, 0.f, 0.f};
+                gv[u] = ok ? g4[i] : f4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float xh = (lrelu(xv[u][j]) - mu) * rs;
+                    const float g = dv[u][j] * gv[u][j];
+                    sg += g;
+                    sgh += (double)g * xh;
+                }
+        }
+    } else {
+        for (long long e = threadIdx.x; e < n; e += LNT) {
+            const float xh = (lrelu(xb[e]) - mu) * rs;
+            const float g = db[e] * gamma[e];
+            sg += g;
+            sgh += (double)g * xh;
+        }
     }
-    sg = block_sum256(sg, red);
-    sgh = block_sum256(sgh, red);
+    sg = block_sum_ln(sg, red);
+    sgh = block_sum_ln(sgh, red);
     if (threadIdx.x == 0) {
         sums[2 * b] = sg;
         sums[2 * b + 1] = sgh;
     }
 }
 
-// one lane per tensor element, looping over the batch: dx, and dgamma / dbeta summed in registers
+// four consecutive elements per lane (one float4), over the images of batch slice blockIdx.y (four
+// at a time, their loads in flight together): dx, and the slice's dgamma / dbeta partials summed in
+// registers; k_lnb_gsum adds the slices in a fixed order (no atomics: deterministic)
 __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, const float* __restrict__ dxo,
                                                    const float* __restrict__ gamma, const float* __restrict__ stats,
                                                    const double* __restrict__ sums, long long n, int B, int act,
-                                                   float* __restrict__ dx, int accumulate, float* __restrict__ dgamma,
-                                                   float* __restrict__ dbeta) {
+                                                   float* __restrict__ dx, int accumulate, float* __restrict__ gpart,
+                                                   float* __restrict__ bpart) {
+    const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (e0 >= n) return;
+    const int S = gridDim.y, sl = blockIdx.y;
+    const int bs = (B + S - 1) / S, b_lo = sl * bs, b_hi = min(B, b_lo + bs);
+    const bool vec = (n & 3) == 0;
+    const int ne = n - e0 < 4 ? (int)(n - e0) : 4;
+    f4 gm = f4{1.f, 1.f, 1.f, 1.f}, dg = f4{0.f, 0.f, 0.f, 0.f}, dbt = f4{0.f, 0.f, 0.f, 0.f};
+    if (stats)
+        for (int j = 0; j < ne; j++) gm[j] = gamma[e0 + j];
+    const float inv_n = 1.f / (float)n;
+    auto ld4 = [&](const float* p, size_t i) -> f4 {
+        if (vec) return *reinterpret_cast<const f4*>(p + i);
+        f4 v = f4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < ne; j++) v[j] = p[i + j];
+        return v;
+    };
+    constexpr int U = 4;
+    for (int b0 = b_lo; b0 < b_hi; b0 += U) {
+        f4 xv[U], d[U], o[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u;
+            const size_t i = (size_t)b * n + e0;
+            xv[u] = b < b_hi ? ld4(x, i) : f4{0.f, 0.f, 0.f, 0.f};
+            d[u] = b < b_hi ? ld4(dxo, i) : f4{0.f, 0.f, 0.f, 0.f};
+            o[u] = (accumulate && b < b_hi) ? ld4(dx, i) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u;
+            if (b >= b_hi) break;
+            float mu = 0.f, rs = 1.f, mg = 0.f, mgh = 0.f;
+            if (stats) {
+                mu = stats[2 * b];
+                rs = stats[2 * b + 1];
+                mg = (float)(sums[2 * b] * inv_n);
+                mgh = (float)(sums[2 * b + 1] * inv_n);
+            }
+            f4 g4;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float lr = (!act || xv[u][j] > 0.f) ? 1.f : LRELU_ALPHA;
+                float g;
+                if (stats) {
+                    const float xh = (lrelu(xv[u][j]) - mu) * rs;
+                    dg[j] = fmaf(d[u][j], xh, dg[j]);
+                    dbt[j] += d[u][j];
+                    g = rs * (d[u][j] * gm[j] - mg - xh * mgh) * lr;
+                } else {
+                    g = d[u][j] * lr;
+                }
+                g4[j] = o[u][j] + g;
+            }
+            const size_t i = (size_t)b * n + e0;
+            if (vec) {
+                *reinterpret_cast<f4*>(dx + i) = g4;
+            } else {
+                for (int j = 0; j < ne; j++) dx[i + j] = g4[j];
+            }
+        }
+    }
+    if (stats)
+        for (int j = 0; j < ne; j++) {
+            gpart[(size_t)sl * n + e0 + j] = dg[j];
+            bpart[(size_t)sl * n + e0 + j] = dbt[j];
+        }
+}
+
+__global__ __launch_bounds__(256) void k_lnb_gsum(const float* __restrict__ gpart, const float* __restrict__ bpart,
+                                                  int S, long long n, float* __restrict__ dgamma,
+                                                  float* __restrict__ dbeta) {
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
     if (e >= n) return;
-    const float gm = stats ? gamma[e] : 1.f;
-    const float inv_n = 1.f / (float)n;
-    float dg = 0.f, dbt = 0.f;
-    for (int b = 0; b < B; b++) {
-        const size_t i = (size_t)b * n + e;
-        const float xv = x[i], d = dxo[i];
-        const float lr = (!act || xv > 0.f) ? 1.f : LRELU_ALPHA;
-        float g;
-        if (stats) {
-            const float mu = stats[2 * b], rs = stats[2 * b + 1];
-            const float xh = (lrelu(xv) - mu) * rs;
-            dg = fmaf(d, xh, dg);
-            dbt += d;
-            const float mg = (float)(sums[2 * b] * inv_n), mgh = (float)(sums[2 * b + 1] * inv_n);
-            g = rs * (d * gm - mg - xh * mgh) * lr;
-        } else {
-            g = d * lr;
-        }
-        dx[i] = accumulate ? dx[i] + g : g;
+    float g = 0.f, b = 0.f;
+    for (int s = 0; s < S; s++) {
+        g += gpart[(size_t)s * n + e];
+        b += bpart[(size_t)s * n + e];
     }
-    if (stats) {
-        dgamma[e] += dg;
-        dbeta[e] += dbt;
-    }
+    dgamma[e] += g;
+    dbeta[e] += b;
 }
 
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        hipStream_t st) {
-    if (stats) hipLaunchKernelGGL(k_lnb_reduce, dim3(B), dim3(256), 0, st, x, dxo, gamma, stats, n, sums);
-    hipLaunchKernelGGL(k_lnb_apply, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, dxo, gamma, stats, sums, n,
-                       B, act, dx, accumulate, dgamma, dbeta);
+                        float* scratch, hipStream_t st) {
+    if (stats) hipLaunchKernelGGL(k_lnb_reduce, dim3(B), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
+    const int S = B < LNB_SLICES ? B : LNB_SLICES;
+    float* gpart = scratch;
+    float* bpart = scratch + (size_t)LNB_SLICES * n;
+    hipLaunchKernelGGL(k_lnb_apply, dim3((unsigned)((n + 1023) / 1024), S), dim3(256), 0, st, x, dxo, gamma, stats,
+                       sums, n, B, act, dx, accumulate, gpart, bpart);
+    if (stats)
+        hipLaunchKernelGGL(k_lnb_gsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gpart, bpart, S, n, dgamma,
+                           dbeta);
 }
 
 // ------------------------------------------------------------------------------------------------
