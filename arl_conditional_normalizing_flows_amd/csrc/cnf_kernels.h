@@ -25,15 +25,18 @@ constexpr int MAXPROB = 12;
 // events: no extra packets between the kernels, so the stream runs as it does untimed.
 struct LaunchTiming {
     hipEvent_t start = nullptr, stop = nullptr;
+    int used = 0;   // kernels that wrote the pair (the last one's times are kept)
 };
 LaunchTiming& launch_timing();   // per host thread (cnf_runtime.cpp)
 #define CNF_LAUNCH(K, G, B, L, S, ...)                                                              \
     do {                                                                                            \
-        const ::cnf::LaunchTiming& lt_ = ::cnf::launch_timing();                                    \
-        if (lt_.start != nullptr)                                                                   \
+        ::cnf::LaunchTiming& lt_ = ::cnf::launch_timing();                                          \
+        if (lt_.start != nullptr) {                                                                 \
             hipExtLaunchKernelGGL(K, G, B, L, S, lt_.start, lt_.stop, 0, __VA_ARGS__);              \
-        else                                                                                        \
+            lt_.used++;                                                                             \
+        } else {                                                                                    \
             hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                         \
+        }                                                                                           \
     } while (0)
 
 // packed weight-image formats (see cnf_plan.h PackedConv)
@@ -183,6 +186,7 @@ struct GcBranch {
 struct GcShape {
     GcBranch br[GC_MAXBR];
     int nbr, H, W, in_cs, out_cs, TH, tiles_per_img;
+    int TW, tiles_x;             // tile width (W, or a divisor of W for wide images) and column tiles
     int band_bytes;              // offset of the second band buffer (double-buffered staging)
     int lnst;                    // bit 0: LN2 on load (in_part set), bit 1: LN3 partials out (out_part set)
 };
@@ -194,7 +198,7 @@ struct GcArgs {
     float* out_part[2];          // LN3 partials of LeakyReLU(t2)
     const float* gamma[2];       // LN2 gamma/beta [HW][in_cs]
     const float* beta[2];
-    const float* w[2][GC_MAXBR];
+    const float* w[2][GC_MAXBR];   // per k_gc branch (GcShape.br order)
     const float* b[2][GC_MAXBR];
     GcShape s;                   // launch-independent part (compile-time in the shape-specialised kernels)
     int B, ipw, in_nparts, part_stride;

@@ -2,6 +2,7 @@
 // of the coupling-layer geometry (:355-498, :1087-1104, conv_cINN_base_functions.py:364-413, 501-627).
 #include "cnf_plan.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <functional>
@@ -400,56 +401,105 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 }
                 if (c.use_lds) c.lds = g;
             }
-            // streamed layers: the grouped stage as one k_gc launch when its LDS image fits 80 KiB (2 per CU)
+            // streamed layers: the grouped stage as k_gc launches. Each group of branches gets the first
+            // tile that fits the LDS and staging budgets: full-width row tiles of 256 pixels, then 2-D
+            // tiles (TW = 64 .. 8 columns, W % TW == 0) of 256, 128, 64 pixels. The branches are taken
+            // in order of dilation and added to the current group while it still fits, else they open
+            // a new group; a branch that fits no tile on its own is left out (tap mode when its
+            // dilation is >= 4 and its im2col row fits, k_conv<3> otherwise).
             for (auto& c : p.couplings) {
+                c.gcg.clear();
                 c.gc_fused = false;
-                if (c.use_lds || c.R == 0 || c.br.empty() || c.br.size() > (size_t)GC_MAXBR || c.wc > 128) continue;
-                int TH = std::max(1, std::min(c.hc, 256 / c.wc));   // 256-pixel tiles (8 waves x 2 subtiles)
-                if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
-                int64_t off = 512;   // [256, 384): per-image LN table
-                std::vector<GcBranch> gb;
-                bool ok = true;
-                for (const Branch& b : c.br) {
-                    GcBranch g{};
-                    g.cin_off = b.cin_off;
-                    g.cin = b.cin;
-                    g.cinp = (b.cin + 3) / 4 * 4;
-                    g.cout = b.cout;
-                    g.out_off = b.out_off;
-                    g.dil = b.dil;
-                    g.G = (9 * (g.cinp / 4) + 3) / 4;
-                    g.BW = c.wc + 2 * b.dil;
-                    g.BH = TH + 2 * b.dil;
-                    g.S = stride8(g.cinp);
-                    // exact umulhi division for x < 2^16 (x * d < 2^32)
-                    g.cpq_mag = g.cinp == 4 ? 0u : (uint32_t)((((uint64_t)1 << 32) + (g.cinp / 4) - 1) / (g.cinp / 4));
-                    g.bw_mag = (uint32_t)((((uint64_t)1 << 32) + g.BW - 1) / g.BW);
-                    if ((int64_t)g.BH * g.BW * (g.cinp / 4) >= (1 << 16)) ok = false;
-                    if (b.cout > 64) ok = false;
-                    g.w_off = (int)off;
-                    off = align16(off + (int64_t)g.G * 16 * 16 * ((b.cout + 15) / 16) * 4);
-                    g.q_off = (int)off;
-                    off = align16(off + 16LL * g.G);
-                    g.band_off = (int)off;
-                    off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
-                    gb.push_back(g);
+                if (c.use_lds || c.R == 0 || c.br.empty() || c.br.size() > (size_t)GC_MAXBR || !allow_gc) continue;
+                auto fit = [&](const std::vector<int>& sel, int TW, int TP, Coupling::GcGroup& out) -> bool {
+                    int TH = std::max(1, std::min(c.hc, TP / TW));   // TP-pixel tiles
+                    if (TW == c.wc)
+                        if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
+                    int64_t off = 512;   // [256, 384): per-image LN table
+                    std::vector<GcBranch> gb;
+                    for (int bi : sel) {
+                        const Branch& b = c.br[bi];
+                        GcBranch g{};
+                        g.cin_off = b.cin_off;
+                        g.cin = b.cin;
+                        g.cinp = (b.cin + 3) / 4 * 4;
+                        g.cout = b.cout;
+                        g.out_off = b.out_off;
+                        g.dil = b.dil;
+                        g.G = (9 * (g.cinp / 4) + 3) / 4;
+                        g.BW = TW + 2 * b.dil;
+                        g.BH = TH + 2 * b.dil;
+                        g.S = stride8(g.cinp);
+                        // exact umulhi division for x < 2^16 (x * d < 2^32)
+                        g.cpq_mag = g.cinp == 4 ? 0u : (uint32_t)((((uint64_t)1 << 32) + (g.cinp / 4) - 1) / (g.cinp / 4));
+                        g.bw_mag = (uint32_t)((((uint64_t)1 << 32) + g.BW - 1) / g.BW);
+                        if ((int64_t)g.BH * g.BW * (g.cinp / 4) >= (1 << 16)) return false;
+                        if (b.cout > 64) return false;
+                        g.w_off = (int)off;
+                        off = align16(off + (int64_t)g.G * 16 * 16 * ((b.cout + 15) / 16) * 4);
+                        g.q_off = (int)off;
+                        off = align16(off + 16LL * g.G);
+                        g.band_off = (int)off;
+                        off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
+                        gb.push_back(g);
+                    }
+                    int64_t quads = 0;   // staged band quads: at most GC_STAGE_QUADS per workgroup
+                    for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
+                    // two band buffers: the next image is staged while the current one is computed
+                    const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
+                    off += band_bytes;
+                    for (GcBranch& g : gb) {   // biases (read from LDS in the epilogue: no global load there)
+                        g.b_off = (int)off;
+                        off = align16(off + 4LL * g.cout);
+                    }
+                    if (off > 160 * 1024 || quads > GC_STAGE_QUADS) return false;
+                    out.br = sel;
+                    out.gcb = gb;
+                    out.TH = TH;
+                    out.TW = TW;
+                    out.tiles_x = c.wc / TW;
+                    out.tiles_y = (c.hc + TH - 1) / TH;
+                    out.lds = (int)off;
+                    out.band_bytes = (int)band_bytes;
+                    out.TP = TP;
+                    return true;
+                };
+                auto fit_any = [&](const std::vector<int>& sel, Coupling::GcGroup& out) -> bool {
+                    if (c.wc <= 128 && fit(sel, c.wc, 256, out)) return true;
+                    for (int TP : {256, 128, 64})
+                        for (int TW : {64, 32, 16, 8})
+                            if (TW < c.wc && c.wc % TW == 0 && TW <= TP && fit(sel, TW, TP, out)) return true;
+                    return false;
+                };
+                std::vector<int> order;
+                for (size_t bi = 0; bi < c.br.size(); bi++) order.push_back((int)bi);
+                std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return c.br[x].dil < c.br[y].dil; });
+                Coupling::GcGroup cur;
+                bool have = false;
+                for (int bi : order) {
+                    Coupling::GcGroup g;
+                    // a large dilation that tap mode can take joins a group only at the group's own tile
+                    // (shrinking the tile for its halo costs more than a tap-mode launch)
+                    const bool tap_able = c.br[bi].dil >= 4 && ks == 3 && 9 * c.br[bi].cin <= 128 && c.br[bi].cout <= 64;
+                    if (have) {
+                        std::vector<int> sel = cur.br;
+                        sel.push_back(bi);
+                        if (tap_able ? fit(sel, cur.TW, cur.TP, g) : fit_any(sel, g)) {
+                            cur = g;
+                            continue;
+                        }
+                    }
+                    if (have && tap_able) continue;   // tap mode
+                    if (fit_any({bi}, g)) {
+                        if (have) c.gcg.push_back(cur);
+                        cur = g;
+                        have = true;
+                    }
                 }
-                int64_t quads = 0;   // staged band quads: at most GC_STAGE_QUADS per workgroup
-                for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
-                // two band buffers: the next image is staged while the current one is computed
-                const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
-                off += band_bytes;
-                for (GcBranch& g : gb) {   // biases (read from LDS in the epilogue: no global load there)
-                    g.b_off = (int)off;
-                    off = align16(off + 4LL * g.cout);
-                }
-                if (!ok || off > 160 * 1024 || quads > GC_STAGE_QUADS || !allow_gc) continue;
-                c.gc_fused = true;
-                c.gc_TH = TH;
-                c.gc_lds = (int)off;
-                c.gc_band_bytes = (int)band_bytes;
-                c.gcb = gb;
-                for (size_t i = 0; i < c.br.size(); i++) c.gc_fmt[i] = PK_Q4;
+                if (have) c.gcg.push_back(cur);
+                c.gc_fused = !c.gcg.empty();
+                for (const auto& g : c.gcg)
+                    for (int bi : g.br) c.gc_fmt[bi] = PK_Q4;
             }
         }
 
@@ -535,7 +585,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                           [=](int n) { return cib + n; });
                 // streamed layers: conv_in for k_pw's tap mode, the HWIO kernel read as its
                 // [9*dc1][nk] im2col matrix (k = tap * dc1 + c)
-                if (!c.use_lds && ks == 3 && 9 * c.dc1 <= 128 && nk <= 64)
+                // (dc1 <= 4: the im2col gathers are scalar mask-position loads, cheap only for narrow halves)
+                if (!c.use_lds && ks == 3 && c.dc1 <= 4 && nk <= 64)
                     pack(np.ci_pw, PK_1X1, 9 * c.dc1, nk, [=](int k, int n) { return cik + (int64_t)k * nk + n; },
                          [=](int n) { return cib + n; });
                 for (auto& rb : np.rb) {
@@ -574,7 +625,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         PackedConv pw;
                         int tap_dmin = 4;
                         if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin = std::atoi(e);   // tuning
-                        if (!c.use_lds && !c.gc_fused && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin)
+                        const bool in_gc = c.in_gc((int)bi);
+                        if (!c.use_lds && !in_gc && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin)
                             pack(pw, PK_1X1, 9 * b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gpw.push_back(pw);
                     }

@@ -82,10 +82,26 @@ struct Coupling {
     int ci_fmt = PK_KN, co_fmt = PK_KN;   // packed formats of conv_in / conv_out
     std::vector<int> gc_fmt;              // per grouped branch
     NetLdsGeom lds;                       // valid when use_lds
-    bool gc_fused = false;                // streamed layer: grouped stage as one k_gc launch (PK_Q4, padded cin)
-    int gc_TH = 0, gc_lds = 0;            // k_gc tile rows, LDS bytes per workgroup
-    int gc_band_bytes = 0;                // k_gc: bytes of one set of branch bands (buffer 1 follows buffer 0)
-    std::vector<GcBranch> gcb;            // k_gc branch geometry (offsets into LDS)
+    // streamed layer: the grouped stage as k_gc launches (PK_Q4, padded cin), each over a group of
+    // branches that fits one workgroup's LDS; branches in none run as k_pw tap-mode launches (k_conv<3>
+    // when their im2col row is too long)
+    struct GcGroup {
+        std::vector<int> br;              // indices into Coupling::br
+        std::vector<GcBranch> gcb;        // their geometry (offsets into LDS)
+        int TH = 0, TW = 0, tiles_x = 1;  // tile rows / columns (W, or a divisor of W), column tiles
+        int lds = 0, band_bytes = 0;      // LDS bytes per workgroup; bytes of one set of branch bands
+        int tiles() const { return tiles_y * tiles_x; }
+        int tiles_y = 1;
+        int TP = 0;                       // tile pixels the plan aimed at (TH = min(H, TP / TW))
+    };
+    std::vector<GcGroup> gcg;
+    bool gc_fused = false;                // gcg non-empty
+    bool in_gc(int bi) const {
+        for (const GcGroup& g : gcg)
+            for (int b : g.br)
+                if (b == bi) return true;
+        return false;
+    }
 };
 
 struct Layer {

@@ -123,7 +123,16 @@ WsLayout Plan::layout(int B) const {
         parts = std::max(parts, 4 * conv1_geo(c.hc, c.wc).tiles);
         parts = std::max(parts, 4 * ((c.hc * c.wc + 63) / 64));   // k_pw
         parts = std::max(parts, (int)c.br.size() * std::max(4 * g.tiles, 4 * ((c.hc * c.wc + 63) / 64)));   // mixed branches
-        if (c.gc_fused) parts = std::max(parts, GC_NW_MAX * ((c.hc + c.gc_TH - 1) / c.gc_TH));   // k_gc
+        if (c.gc_fused) {   // k_gc groups' slots, then the tap-mode / k_conv<3> branches' after them
+            int gp = 0, ing = 0;
+            for (const auto& gg : c.gcg) {
+                gp += GC_NW_MAX * gg.tiles();
+                ing += (int)gg.br.size();
+            }
+            const int rest = (int)c.br.size() - ing;
+            gp += rest * std::max(4 * g.tiles, 4 * ((c.hc * c.wc + 63) / 64));
+            parts = std::max(parts, gp);
+        }
         ldp = std::max(ldp, ld_parts_for((int)npx));
     }
     L.n_uv = n_uv;
@@ -194,6 +203,8 @@ struct Exec {
             launch_timing() = LaunchTiming{};
             throw;
         }
+        // timed only when exactly one kernel wrote the pair (a launch helper may issue none)
+        const bool wrote = timed && launch_timing().used == 1;
         launch_timing() = LaunchTiming{};
         if (p.record) {
             Recorded r;
@@ -201,7 +212,7 @@ struct Exec {
             r.flops = flops;
             r.bytes = bytes;
             r.relaunch = std::move(fn);
-            r.timed = timed;
+            r.timed = wrote;
             p.recorded.push_back(std::move(r));
         }
     }
@@ -355,9 +366,10 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
     for (const ProbSpec& s : probs)
         ln_uniform = ln_uniform && ((s.in_st.part != nullptr) == (probs[0].in_st.part != nullptr)) &&
                      ((s.res != nullptr) == (probs[0].res != nullptr));
-    bool fits32 = true;   // k_pw addresses each tensor with 32-bit byte offsets (buffer resources)
+    bool fits32 = true;   // k_pw addresses one image per buffer resource with 32-bit byte offsets
     for (const ProbSpec& s : probs)
-        fits32 = fits32 && (double)E.B * h * w * std::max(s.in_cs, s.out_cs) * 4.0 < 2147483648.0;
+        fits32 = fits32 && (double)h * w * std::max(s.in_cs, s.out_cs) * 4.0 < 2147483648.0 &&
+                 (tap == nullptr || (double)tap->img * 4.0 < 2147483648.0);
     const bool pw_ok = ks == 1 && vec && pw_gm > 0 && ln_uniform && fits32 && E.p.use_pw;
     if (ks == 3) {
         const int grid_x = E.B * g.tiles;
@@ -697,8 +709,14 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) used |= 1ull << ch;
             set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used));
         }
-        // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]
-        if (c.gc_fused) {
+        // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]. The k_gc
+        // launch (when planned) takes its branches first; every other branch runs as a k_pw tap-mode
+        // launch over its im2col row when that row fits (9 cin <= 128), the rest as one k_conv<3>.
+        // Each launch's LN3 partial slots follow the previous ones'.
+        int base = 0;
+        std::vector<char> done(nbr, 0);
+        for (const Coupling::GcGroup& gg : c.gcg) {
+            const int ng = (int)gg.br.size();
             GcArgs ga;
             std::memset(&ga, 0, sizeof(ga));
             for (int n = 0; n < 2; n++) {
@@ -706,52 +724,58 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 ga.in[n] = t1[n];
                 ga.out[n] = t2[n];
                 ga.in_part[n] = ln ? sl[n][1].part : nullptr;
-                ga.out_part[n] = ln ? sl[n][2].part : nullptr;
+                ga.out_part[n] = ln ? sl[n][2].part + (size_t)base * LNP : nullptr;   // after earlier launches' slots
                 ga.gamma[n] = ln ? P + rb.ln2g : nullptr;
                 ga.beta[n] = ln ? P + rb.ln2b : nullptr;
-                for (int bi = 0; bi < nbr; bi++) {
-                    ga.w[n][bi] = X + rb.gc[bi].w;
-                    ga.b[n][bi] = X + rb.gc[bi].b;
+                for (int k = 0; k < ng; k++) {
+                    ga.w[n][k] = X + rb.gc[gg.br[k]].w;
+                    ga.b[n][k] = X + rb.gc[gg.br[k]].b;
                 }
             }
-            for (int bi = 0; bi < nbr; bi++) ga.s.br[bi] = c.gcb[bi];
-            ga.s.nbr = nbr;
+            for (int k = 0; k < ng; k++) {
+                ga.s.br[k] = gg.gcb[k];
+                done[gg.br[k]] = 1;
+            }
+            ga.s.nbr = ng;
             ga.s.H = c.hc;
             ga.s.W = c.wc;
             ga.s.in_cs = c.nk;
             ga.s.out_cs = c.gc;
             ga.B = B;
-            ga.s.TH = c.gc_TH;
-            ga.s.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
+            ga.s.TH = gg.TH;
+            ga.s.TW = gg.TW;
+            ga.s.tiles_x = gg.tiles_x;
+            ga.s.tiles_per_img = gg.tiles();
             ga.in_nparts = sl[0][1].nparts;
             ga.part_stride = L.st_parts;
             // images per workgroup: one workgroup per CU, looping over its images with the next
             // image's band staged behind the current one's MFMAs
             const int64_t units = (int64_t)ga.s.tiles_per_img * 2 * B;
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
-            ga.s.band_bytes = c.gc_band_bytes;
+            ga.s.band_bytes = gg.band_bytes;
             ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
             const int gcw = gc_waves(ga);
-            if (gcw * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
+            if (base + gcw * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.s.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
-            const int ilds = c.gc_lds;
+            const int ilds = gg.lds;
             double fl = 0, by = 0;
-            for (const Branch& b : c.br) fl += 2.0 * B * c.hc * c.wc * 9.0 * b.cin * b.cout * 2;
             int win = 0;
-            for (const Branch& b : c.br) win += b.cin;
-            by = 4.0 * B * c.hc * c.wc * (win + c.gc) * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
+            for (int k = 0; k < ng; k++) {
+                const Branch& b = c.br[gg.br[k]];
+                fl += 2.0 * B * c.hc * c.wc * 9.0 * b.cin * b.cout * 2;
+                win += b.cin;
+                by += 4.0 * B * c.hc * c.wc * b.cout * 2;
+            }
+            by += 4.0 * B * c.hc * c.wc * win * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
-            set_parts(2, gcw * ga.s.tiles_per_img);   // one slot per k_gc wave
-        } else {
-            // branches whose im2col row fits k_pw (9 cin <= 128): tap-mode 1x1 over the row, gathered
-            // from t1 with LN2 on load (no staged band, so large dilations cost no halo); the rest
-            // as one k_conv<3> launch. Each launch's LN3 partial slots follow the previous ones'.
-            int base = 0;
+            base += gcw * ga.s.tiles_per_img;   // one slot per k_gc wave
+        }
+        {
             std::vector<ProbSpec> pr;
             for (int bi = 0; bi < nbr; bi++) {
                 const Branch& b = c.br[bi];
-                if (!(E.p.use_pw && c.net[0].rb[r].gpw[bi].size > 0)) continue;
+                if (done[bi] || !(E.p.use_pw && c.net[0].rb[r].gpw[bi].size > 0)) continue;
                 std::vector<ProbSpec> pt;
                 for (int n = 0; n < 2; n++) {
                     const RBParams& rb = c.net[n].rb[r];
@@ -763,6 +787,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 ts.dil = b.dil;
                 ts.off = b.cin_off;
                 base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts);
+                done[bi] = 1;
             }
             int nrest = 0;
             for (int n = 0; n < 2; n++) {
@@ -770,7 +795,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 int k = 0;
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
-                    if (E.p.use_pw && rb.gpw[bi].size > 0) continue;
+                    if (done[bi]) continue;
                     pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
                                           ln ? P + rb.ln2b : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base + k * nt3 * 4, b.dil});
@@ -1452,28 +1477,36 @@ int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap) {
 int cnf_debug_pw_nshapes() { return pw_num_shapes(); }
 int cnf_debug_pw_words() { return PWSHAPE_WORDS; }
 
-// shape words of coupling `coupling`'s k_gc launches (0 if it has none)
+// shape words of coupling `coupling`'s k_gc launches, one GcShape per group (0 if it has none)
 int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) {
-    if (!plan || !words || cap < GCSHAPE_WORDS) return -1;
+    if (!plan || !words) return -1;
     const Plan& p = *plan->p;
     if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
     const Coupling& c = p.couplings[coupling];
     if (c.use_lds || !c.gc_fused) return 0;
-    GcShape s;
-    std::memset(&s, 0, sizeof(s));
-    for (size_t bi = 0; bi < c.br.size(); bi++) s.br[bi] = c.gcb[bi];
-    s.nbr = (int)c.br.size();
-    s.H = c.hc;
-    s.W = c.wc;
-    s.in_cs = c.nk;
-    s.out_cs = c.gc;
-    s.TH = c.gc_TH;
-    s.tiles_per_img = (c.hc + c.gc_TH - 1) / c.gc_TH;
-    s.band_bytes = c.gc_band_bytes;
-    s.lnst = p.desc.layer_norm ? 3 : 0;   // the forward's k_gc: LN2 on load and LN3 partials iff LayerNorm
-    std::memcpy(words, &s, sizeof(s));
-    return GCSHAPE_WORDS;
+    if (cap < GCSHAPE_WORDS * (int)c.gcg.size()) return -1;
+    int n = 0;
+    for (const Coupling::GcGroup& gg : c.gcg) {
+        GcShape s;
+        std::memset(&s, 0, sizeof(s));
+        for (size_t k = 0; k < gg.br.size(); k++) s.br[k] = gg.gcb[k];
+        s.nbr = (int)gg.br.size();
+        s.H = c.hc;
+        s.W = c.wc;
+        s.in_cs = c.nk;
+        s.out_cs = c.gc;
+        s.TH = gg.TH;
+        s.TW = gg.TW;
+        s.tiles_x = gg.tiles_x;
+        s.tiles_per_img = gg.tiles();
+        s.band_bytes = gg.band_bytes;
+        s.lnst = p.desc.layer_norm ? 3 : 0;   // the forward's k_gc: LN2 on load and LN3 partials iff LayerNorm
+        std::memcpy(words + n, &s, sizeof(s));
+        n += GCSHAPE_WORDS;
+    }
+    return n;
 }
+int cnf_debug_gc_words() { return GCSHAPE_WORDS; }
 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }

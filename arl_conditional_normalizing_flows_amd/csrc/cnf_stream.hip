@@ -65,9 +65,11 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
     const uint32_t in_img = TAP ? (uint32_t)PA(uimg) * 4u : (uint32_t)HW * PP(in_cs) * 4u;
     const uint32_t out_img = (uint32_t)HW * PP(out_cs) * 4u;
-    const auto rin = buf_rsrc(P.in, (uint32_t)a.B * in_img);
-    const auto rout = buf_rsrc(P.out, (uint32_t)a.B * out_img);
-    const auto rres = buf_rsrc(RES ? P.res : P.out, (uint32_t)a.B * out_img);
+    // one buffer resource per image (64-bit image base, 32-bit offsets inside the image): the batch
+    // size never limits the addressing
+    auto img_rsrc = [](const float* base, int img, uint32_t bytes) {
+        return buf_rsrc(base + (size_t)img * (bytes >> 2), bytes);
+    };
 
     // A operand: lane (i16, kq) feeds pixel pa, channels 16g + 4kq + s at k-step s of group g. Masks
     // are evaluated per element from shape fields (folded to constants in the specialised
@@ -106,7 +108,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // row's channel quads never straddle two taps when cin % 4 == 0)
     const bool tquad = TAP && PA(umask) < 0 && PA(udc) % 4 == 0 && PA(uoff) % 4 == 0 && PA(uD) % 4 == 0;
     auto load_img = [&](int ii, f4 (&xd)[GM], float (&rd)[NR][4]) {
-        const uint32_t ib = (uint32_t)(img0 + ii) * in_img;
+        const auto rin = img_rsrc(P.in, img0 + ii, in_img);
+        constexpr uint32_t ib = 0;
         if constexpr (TAP) {
 #pragma unroll
             for (int g = 0; g < GM; g++) {
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
         }
         if (RES) {
-            const uint32_t ob = (uint32_t)(img0 + ii) * out_img;
+            const auto rres = img_rsrc(RES ? P.res : P.out, img0 + ii, out_img);
+            constexpr uint32_t ob = 0;
 #pragma unroll
             for (int n = 0; n < NR; n++)
 #pragma unroll
@@ -251,7 +255,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             }
         }
         // epilogue: bias, residual, masked store, per-wave LN partial of LeakyReLU(out)
-        const uint32_t ob = (uint32_t)img * out_img;
+        const auto rout = img_rsrc(P.out, img, out_img);
+        constexpr uint32_t ob = 0;
         float vals[NR * 4];
         bool valid[NR * 4];
 #pragma unroll
@@ -388,7 +393,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
         for (int h = 0; h < 2; h++) {
             const int pt = (h ? s1 : s0) * 16 + i16;
             const int ptc = pt < npx ? pt : 0;
-            const int tr = ptc / GS(W), tc = ptc - tr * GS(W);
+            const int tr = ptc / GS(TW), tc = ptc - tr * GS(TW);
             base[h] = band + (tr * br.BW + tc) * br.S;
         }
         f4 acc0[NR], acc1[NR];
@@ -432,7 +437,9 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             if (h == 1 && !v1) break;
             const int po = (h ? s1 : s0) * 16 + i16;
             const bool pv = po < npx;
-            float* orow = outp + (size_t)(px0 + po) * GS(out_cs) + br.out_off + 4 * kq;
+            // tile pixel po -> image pixel px0 + row * W + column (== px0 + po for full-width tiles)
+            const int por = po / GS(TW), poc = po - por * GS(TW);
+            float* orow = outp + (size_t)(px0 + por * GS(W) + poc) * GS(out_cs) + br.out_off + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NR; n++) {
                 f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
@@ -493,9 +500,11 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int H = GS(H), W = GS(W), HW = H * W;
-    const int r0 = tile * GS(TH);
+    // 2-D tiles: TH rows x TW columns (TW == W for all but the widest images; W % TW == 0)
+    const int ty = GS(tiles_x) == 1 ? tile : tile / GS(tiles_x), tx = tile - ty * GS(tiles_x);
+    const int r0 = ty * GS(TH), c0 = tx * GS(TW);
     const int rows = GS(H) % GS(TH) == 0 ? GS(TH) : min(GS(TH), H - r0);   // constant when tiles are full
-    const int npx = rows * W, px0 = r0 * W;
+    const int npx = rows * GS(TW), px0 = r0 * W + c0;
     const bool ln = SID >= 0 ? (GS(lnst) & 1) != 0 : a.in_part[net] != nullptr;
     const bool stats = SID >= 0 ? (GS(lnst) & 2) != 0 : a.out_part[net] != nullptr;
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
             if (e < nq) {
                 const int pix = cpq == 1 ? e : (int)__umulhi((unsigned)e, br.cpq_mag), cq = e - pix * cpq;
                 const int brr = (int)__umulhi((unsigned)pix, br.bw_mag), bc = pix - brr * br.BW;
-                const int y = r0 - br.dil + brr, x = bc - br.dil;
+                const int y = r0 - br.dil + brr, x = c0 + bc - br.dil;
                 loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
                 if (y >= 0 && y < H && x >= 0 && x < W) {
                     soff[u] = (y * W + x) * GS(in_cs) + br.cin_off + 4 * cq;

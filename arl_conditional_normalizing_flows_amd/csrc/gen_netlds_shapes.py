@@ -33,7 +33,7 @@ PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel 
 GC_BRANCH_WORDS = 16          # GcBranch: 14 ints, then the two uint32 division magics
 GC_MAXBR = 8
 CNF_LAYER_COUPLING = 0
-CAP = 512
+CAP = 2048
 W2 = 7   # words of [off_y, stamp_off): off_y, off_t1, off_t2, off_w, off_k, off_ks, maxnr
 M1 = 123  # int members in [offs_per_net, zero_bias) (any further word is alignment padding before zero_bias)
 
@@ -87,9 +87,11 @@ def gc_shapes(lib):
             n = lib.cnf_debug_gc_shape(plan, info.coupling_index, buf, CAP)
             if n < 0:
                 raise RuntimeError('cnf_debug_gc_shape failed')
-            w = tuple(buf[j] for j in range(n))
-            if n and w not in out:
-                out.append(w)
+            nw = lib.cnf_debug_gc_words()   # GCSHAPE_WORDS: one GcShape per k_gc group
+            for g0 in range(0, n, nw):
+                w = tuple(buf[g0 + j] for j in range(nw))
+                if w not in out:
+                    out.append(w)
         lib.cnf_plan_destroy(plan)
     return out
 
