@@ -290,8 +290,10 @@ void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPe
 void launch_squeeze(const float* in, float* out, int B, int H, int W, int C, int dir, hipStream_t st);
 void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_cs, int out_off, int C, long long npix,
                    hipStream_t st);
-void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, int B, int HW,
-                int D, int x_d, float lambda_y, hipStream_t st);
+// per-image NLL terms and the batch sums in one launch; done: a zero-initialised device counter
+// owned by the caller, left at 0 by every completed launch (concurrent launches need their own)
+void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, unsigned* done,
+                int B, int HW, int D, int x_d, float lambda_y, hipStream_t st);
 void launch_pack(const float* params, const int64_t* map, float* aux, long long n, hipStream_t st);
 
 

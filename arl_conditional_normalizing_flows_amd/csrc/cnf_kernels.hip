@@ -680,9 +680,37 @@ __global__ __launch_bounds__(256) void k_chcopy(const float* __restrict__ in, in
     }
 }
 
+// the four batch sums of the per-image terms, in image order (one wave): shared by k_nll's last
+// workgroup and the standalone k_nll_sums of the toy path
+__device__ __forceinline__ void nll_batch_sums(const float* per_image, float* sums, int B, int lane) {
+    double a = 0, bz = 0, by = 0, bl = 0;
+    for (int i = lane; i < B; i += 64) {
+        double llz = per_image[i * 3], lly = per_image[i * 3 + 1], ld = per_image[i * 3 + 2];
+        a += -(llz + lly + ld);
+        bz += -llz;
+        by += -lly;
+        bl += -ld;
+    }
+    a = wave_sum(a);
+    bz = wave_sum(bz);
+    by = wave_sum(by);
+    bl = wave_sum(bl);
+    if (lane == 0) {
+        sums[0] = (float)a;
+        sums[1] = (float)bz;
+        sums[2] = (float)by;
+        sums[3] = (float)bl;
+    }
+}
+
+__global__ void k_nll_sums(const float* __restrict__ per_image, float* __restrict__ sums, int B) {
+    nll_batch_sums(per_image, sums, B, threadIdx.x);   // 64 threads
+}
+
 // per-image NLL terms: llz = sum_{h,w} (-0.5|z|^2 - x_d/2 ln 2pi), lly = -lambda*sum|y-y'|, ld
 __global__ __launch_bounds__(256) void k_nll(const float* __restrict__ xy, const float* __restrict__ zy,
-                                             const float* __restrict__ ld, float* __restrict__ per_image, int HW,
+                                             const float* __restrict__ ld, float* __restrict__ per_image,
+                                             float* __restrict__ sums, unsigned* __restrict__ done, int HW,
                                              int D, int x_d, float lambda_y) {
     const int img = blockIdx.x;
     const float* xb = xy + (size_t)img * HW * D;
@@ -724,31 +752,23 @@ __global__ __launch_bounds__(256) void k_nll(const float* __restrict__ xy, const
         per_image[img * 3 + 1] = (float)lly;
         per_image[img * 3 + 2] = ld[img];
     }
+    // the batch sums in the same launch: the workgroup that finishes last (the wrapping counter
+    // reads B - 1 and returns to 0 for the next call) adds the per-image terms in image order, so
+    // the result does not depend on which workgroup that is. The agent-scope fences publish every
+    // workgroup's terms across the XCDs' L2s before the counter moves, and the last one's loads
+    // after it.
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicInc(done, (unsigned)gridDim.x - 1u) == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (last && threadIdx.x < 64) {
+        __threadfence();
+        nll_batch_sums(per_image, sums, gridDim.x, threadIdx.x);
+    }
 }
 
-__global__ void k_nll_sums(const float* __restrict__ per_image, float* __restrict__ sums, int B) {
-    __shared__ double s[4][64];
-    const int t = threadIdx.x;  // 64 threads
-    double a = 0, bz = 0, by = 0, bl = 0;
-    for (int i = t; i < B; i += 64) {
-        double llz = per_image[i * 3], lly = per_image[i * 3 + 1], ld = per_image[i * 3 + 2];
-        a += -(llz + lly + ld);
-        bz += -llz;
-        by += -lly;
-        bl += -ld;
-    }
-    a = wave_sum(a);
-    bz = wave_sum(bz);
-    by = wave_sum(by);
-    bl = wave_sum(bl);
-    if (t == 0) {
-        sums[0] = (float)a;
-        sums[1] = (float)bz;
-        sums[2] = (float)by;
-        sums[3] = (float)bl;
-    }
-    (void)s;
-}
 
 // aux[i] = map[i] >= 0 ? params[map[i]] : 0
 __global__ __launch_bounds__(256) void k_pack(const float* __restrict__ params, const int64_t* __restrict__ map,
@@ -852,10 +872,9 @@ void launch_chcopy(const float* in, int in_cs, int in_off, float* out, int out_c
                        npix);
 }
 
-void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, int B, int HW,
-                int D, int x_d, float lambda_y, hipStream_t st) {
-    CNF_LAUNCH(k_nll, dim3(B), dim3(256), 0, st, xy, zy, ld, per_image, HW, D, x_d, lambda_y);
-    CNF_LAUNCH(k_nll_sums, dim3(1), dim3(64), 0, st, per_image, sums, B);
+void launch_nll(const float* xy, const float* zy, const float* ld, float* per_image, float* sums, unsigned* done,
+                int B, int HW, int D, int x_d, float lambda_y, hipStream_t st) {
+    CNF_LAUNCH(k_nll, dim3(B), dim3(256), 0, st, xy, zy, ld, per_image, sums, done, HW, D, x_d, lambda_y);
 }
 
 void launch_nll_sums(const float* per_image, float* sums, int B, hipStream_t st) {

@@ -915,8 +915,10 @@ static void ensure_tables(Plan& p) {
     // uploading is not capturable: the first call on a device must run eagerly
     if (hipStreamIsCapturing(nullptr, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
         throw std::runtime_error("plan tables not uploaded yet (call cnf_pack_params before graph capture)");
-    size_t nb = std::max<size_t>(1, p.host_table.size()) * sizeof(int);
+    // one int past the table: cnf_nll's completion counter (zero between launches)
+    size_t nb = (p.host_table.size() + 1) * sizeof(int);
     hip_check(hipMalloc(&p.dev_table, nb), "hipMalloc(table)");
+    hip_check(hipMemset(p.dev_table, 0, nb), "hipMemset(table)");
     if (!p.host_table.empty())
         hip_check(hipMemcpy(p.dev_table, p.host_table.data(), p.host_table.size() * sizeof(int), hipMemcpyHostToDevice),
                   "hipMemcpy(table)");
@@ -1343,8 +1345,11 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
     if (!plan || !xy || !zy || !logdet_per_image || !per_image || !sums || B <= 0)
         return fail(CNF_E_INVALID, "null argument");
     CNF_TRY
-    const cnf_flow_desc& d = plan->p->desc;
-    launch_nll(xy, zy, logdet_per_image, per_image, sums, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y,
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    const cnf_flow_desc& d = p.desc;
+    unsigned* done = reinterpret_cast<unsigned*>(p.dev_table + p.host_table.size());
+    launch_nll(xy, zy, logdet_per_image, per_image, sums, done, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y,
                (hipStream_t)stream);
     check_launch();
     return CNF_OK;

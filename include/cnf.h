@@ -143,7 +143,9 @@ int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out
  * llz = sum_{h,w} log N(z; 0, I_{x_d}), lly = -lambda_y * sum |y - y'|;
  * sums[4] = (sum_i loss_i, sum_i -llz_i, sum_i -lly_i, sum_i -logdet_i),
  * loss_i = -(llz_i + lly_i + logdet_i). Dividing sums by the (global) batch
- * gives the reference's (loss, z_loss, y_loss, detJ_loss). */
+ * gives the reference's (loss, z_loss, y_loss, detJ_loss). One kernel launch;
+ * it uses a completion counter owned by the plan, so calls on one plan must not
+ * run concurrently on different streams (a plan is single-stream anyway). */
 int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image,
             float* per_image, float* sums, int B, void* stream);
 
