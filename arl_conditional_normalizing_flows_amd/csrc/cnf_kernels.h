@@ -264,6 +264,9 @@ void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, i
                        hipStream_t st);
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st);
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st);
+// LN partial slots [B][part_stride][LNP] of one tensor (two nets: part0, part1 or null) merged into
+// slot 0 of each image (k_ln_merge): consumers then read nparts = 1
+void launch_ln_merge(float* part0, float* part1, int nparts, int part_stride, int B, hipStream_t st);
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st);
 void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
                         int B, hipStream_t st);

@@ -529,6 +529,56 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
     }
 }
 
+// Merge of one tensor's per-wave LN partial slots into slot 0 (in place), for tensors of the large
+// streamed layers whose producers write more slots per image than a consumer wave folds in one pass
+// (> 64): every consumer workgroup would otherwise re-read all of them for each of its images.
+// One workgroup per (image, net): each thread folds its strided slots (Chan merge, as ln_fold), the
+// waves merge their lanes in the parallel-axis form, thread 0 the four waves in order; the result is
+// stored as the single slot (mean, 0, M2, N), which ln_fold reads back as exactly that (mean, M2, N).
+// Fixed order throughout: deterministic.
+__global__ __launch_bounds__(256) void k_ln_merge(float* __restrict__ part0, float* __restrict__ part1, int nparts,
+                                                   int part_stride) {
+    const int img = blockIdx.x;
+    float* q = (blockIdx.y == 0 ? part0 : part1) + (size_t)img * part_stride * LNP;
+    float n = 0.f, m = 0.f, M2 = 0.f;
+    for (int i0 = threadIdx.x; i0 < nparts; i0 += 4 * 256) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = i0 + u * 256;
+            v[u] = i < nparts ? *reinterpret_cast<const f4*>(q + (size_t)LNP * i) : f4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) ln_fold(v[u], n, m, M2);
+    }
+    // wave: N = sum n, mean = sum n m / N, M2 = sum (M2 + n (m - mean)^2)
+    const float N = wave_sum_f(n);
+    const float mean = N > 0.f ? wave_sum_f(n * m) / N : 0.f;
+    const float d = m - mean;
+    const float M = wave_sum_f(fmaf(n * d, d, M2));
+    __shared__ float wv[4][3];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        wv[wave][0] = N;
+        wv[wave][1] = mean;
+        wv[wave][2] = M;
+    }
+    __syncthreads();   // every slot has been read: slot 0 may be overwritten
+    if (threadIdx.x == 0) {
+        float tn = 0.f, tm = 0.f, tM = 0.f;
+        for (int w = 0; w < 4; w++) {
+            const float wn = wv[w][0];
+            if (wn > 0.f) {
+                const float nn = tn + wn, dl = wv[w][1] - tm, f = wn / nn;
+                tm = fmaf(dl, f, tm);
+                tM = tM + wv[w][2] + dl * dl * tn * f;
+                tn = nn;
+            }
+        }
+        *reinterpret_cast<f4*>(q) = f4{tm, 0.f, tM, tn};
+    }
+}
+
 // out[img] (=|+=) sum over nl layers, np parts of part[((l*B)+img)*np + j]: one wave per image,
 // lane k folds entries k, k+64, ... (all its loads in flight together), then a fixed-order wave sum
 __global__ __launch_bounds__(64) void k_ld_reduce(const double* __restrict__ part, float* __restrict__ out, int B,
@@ -826,6 +876,10 @@ void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, i
 
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
     CNF_LAUNCH(k_coupling, dim3(nparts, B), dim3(256), 0, st, a);
+}
+
+void launch_ln_merge(float* part0, float* part1, int nparts, int part_stride, int B, hipStream_t st) {
+    CNF_LAUNCH(k_ln_merge, dim3(B, part1 != nullptr ? 2 : 1), dim3(256), 0, st, part0, part1, nparts, part_stride);
 }
 
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st) {

@@ -471,6 +471,12 @@ Plan* build_plan(const cnf_flow_desc* d) {
                             if (TW < c.wc && c.wc % TW == 0 && TW <= TP && fit(sel, TW, TP, out)) return true;
                     return false;
                 };
+                // a large dilation that does not fit the current group opens a group of its own
+                // (cfg5: 485 -> 437 ms/step against tap mode; CNF_GC_TAPGROUP=0 is the A/B knob)
+                static const int tap_group = [] {
+                    const char* e = std::getenv("CNF_GC_TAPGROUP");
+                    return e ? std::atoi(e) : 1;
+                }();
                 std::vector<int> order;
                 for (size_t bi = 0; bi < c.br.size(); bi++) order.push_back((int)bi);
                 std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return c.br[x].dil < c.br[y].dil; });
@@ -478,8 +484,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 bool have = false;
                 for (int bi : order) {
                     Coupling::GcGroup g;
-                    // a large dilation that tap mode can take joins a group only at the group's own tile
-                    // (shrinking the tile for its halo costs more than a tap-mode launch)
+                    // a large dilation joins the current group only at the group's own tile (shrinking
+                    // the tile for its halo costs more than a launch of its own)
                     const bool tap_able = c.br[bi].dil >= 4 && ks == 3 && 9 * c.br[bi].cin <= 128 && c.br[bi].cout <= 64;
                     if (have) {
                         std::vector<int> sel = cur.br;
@@ -489,7 +495,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                             continue;
                         }
                     }
-                    if (have && tap_able) continue;   // tap mode
+                    if (have && tap_able && !tap_group) continue;   // tap mode
                     if (fit_any({bi}, g)) {
                         if (have) c.gcg.push_back(cur);
                         cur = g;

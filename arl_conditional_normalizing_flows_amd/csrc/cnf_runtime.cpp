@@ -346,7 +346,16 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
             if (off < 512) off = 512;   // k_pw keeps its per-image LN table at bytes [256, 384)
             q.lds_w_off = (int)off;
             off = align_up(off + (size_t)G * 16 * 16 * q.nr * 4, 16);
-            if (!tap && (s.cin % 4 || s.in_cs % 4 || s.in_off % 4)) vec = false;   // tap mode gathers scalars
+            // k_pw loads every channel quad the input window starts with 16 bytes at a time: a window
+            // that is not quad-aligned (conv_b over the 62- / 30-channel concat of cfg5's grouped
+            // stages) reads past its last channel into the next pixel (or 0 past the image), which
+            // meets zero weight rows (the packed image pads K with zeros). CNF_PW_ALIGNED=1: the
+            // quad-aligned windows only (the rest as k_conv1)
+            static const bool pw_aligned = [] {
+                const char* e = std::getenv("CNF_PW_ALIGNED");
+                return e && std::atoi(e) != 0;
+            }();
+            if (!tap && pw_aligned && (s.cin % 4 || s.in_cs % 4 || s.in_off % 4)) vec = false;
             pw_nr = std::max(pw_nr, q.nr);
             pw_gm = std::max(pw_gm, G);
         }
@@ -669,7 +678,21 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // a producing launch reports the partial slots it wrote per image (set_parts); in_slab hands
     // that count on to the consumer
     auto out_slab = [&](int n, int k, int) { return ln ? sl[n][k] : Slab{}; };
+    // more slots than one consumer wave folds in a pass (the 64x64 and 128x128 layers): merged once
+    // per image by k_ln_merge instead of by every consumer workgroup for each of its images
+    static const bool ln_merge = [] {   // A/B knob
+        const char* e = std::getenv("CNF_LN_MERGE");
+        return !(e && std::atoi(e) == 0);
+    }();
     auto set_parts = [&](int k, int nparts) {
+        if (ln && ln_merge && nparts > 64) {
+            float* p0 = sl[0][k].part;
+            float* p1 = sl[1][k].part;
+            const int np = nparts, ps = L.st_parts;
+            E.record("k_ln_merge", 0, 16.0 * B * np * 2 + 32.0 * B,
+                     [=](void* st) { launch_ln_merge(p0, p1, np, ps, B, (hipStream_t)st); });
+            nparts = 1;
+        }
         for (int n = 0; n < 2; n++) sl[n][k].nparts = nparts;
     };
     auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };

@@ -24,7 +24,8 @@ sys.path.insert(0, str(ROOT))
 from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
 from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 
-SPECIALISE = ('cfg2', 'cfg3', 'ref_default')   # BASELINE.json configs[1] (the benchmark), configs[2], the reference's default
+# BASELINE.json configs[1] (the benchmark), configs[2], the reference's default, configs[3], configs[4]
+SPECIALISE = ('cfg2', 'cfg3', 'ref_default', 'cfg4', 'cfg5')
 OUT = HERE / 'cnf_netlds_shapes.inc'
 OUT_GC = HERE / 'cnf_gc_shapes.inc'
 OUT_PW = HERE / 'cnf_pw_shapes.inc'
