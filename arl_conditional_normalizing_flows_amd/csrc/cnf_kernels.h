@@ -64,7 +64,38 @@ struct ConvProb {
     int S, Kpad, NS, nr;                   // LDS pixel stride, padded K, B row stride, N-subtiles
     uint32_t cin_mag, wp_mag;              // magic multipliers: x / cin == umulhi(x, cin_mag) (3x3 staging)
     uint32_t st_mask_lo, st_mask_hi;       // output channels actually stored (bit per channel < 64)
+    int st_compact;                        // 1: stored channels packed by compact_ch (k_pw only)
 };
+
+// Compact channel layout of a tensor of which only the channels in mask m are ever read (t1 of the
+// streamed layers: the grouped branches read only their input windows, in the reference's group
+// mode the last _d-channel slice of each, conv_cINN_base_functions.py:397-402): every maximal run
+// of set bits, in channel order, starts at the next 16-byte (quad) boundary. compact_ch(m, c) is
+// channel c's index in that layout (-1 if c is not in m), compact_width(m) the padded width.
+__host__ __device__ inline int compact_ch(uint64_t m, int c) {
+    if (c < 0 || c >= 64 || ((m >> c) & 1ull) == 0) return -1;
+    int off = 0;
+    while (m != 0) {
+        const int s = __builtin_ctzll(m);
+        const uint64_t t = m >> s;
+        const int len = ~t == 0 ? 64 - s : __builtin_ctzll(~t);
+        if (c < s + len) return off + (c - s);
+        off += (len + 3) & ~3;
+        m &= len + s >= 64 ? 0ull : ~0ull << (s + len);
+    }
+    return -1;
+}
+__host__ __device__ inline int compact_width(uint64_t m) {
+    int off = 0;
+    while (m != 0) {
+        const int s = __builtin_ctzll(m);
+        const uint64_t t = m >> s;
+        const int len = ~t == 0 ? 64 - s : __builtin_ctzll(~t);
+        off += (len + 3) & ~3;
+        m &= len + s >= 64 ? 0ull : ~0ull << (s + len);
+    }
+    return off;
+}
 
 struct ConvArgs {
     ConvProb p[MAXPROB];
@@ -237,6 +268,7 @@ struct PwShape {
     int in_cs, in_off, cin, out_cs, out_off, cout, lds_w_off, part_stride;
     int umask, uW, uD, udc, uimg, udil, uoff;   // tap mode (0 otherwise)
     uint32_t st_mask_lo, st_mask_hi;
+    int st_compact;
 };
 constexpr int PWSHAPE_WORDS = (int)(sizeof(PwShape) / 4);
 // the shape of a k_pw launch; false when its problems differ in a shape field
@@ -246,12 +278,12 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvA
                 q.cin, q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride,
                 tap ? a.umask : 0, tap ? a.uW : 0, tap ? a.uD : 0, tap ? a.udc : 0, tap ? a.uimg : 0,
                 tap ? a.udil : 0, tap ? a.uoff : 0,
-                q.st_mask_lo, q.st_mask_hi};
+                q.st_mask_lo, q.st_mask_hi, q.st_compact};
     for (int i = 1; i < a.nprob; i++) {
         const ConvProb& r = a.p[i];
         if (r.in_cs != q.in_cs || r.in_off != q.in_off || r.cin != q.cin || r.out_cs != q.out_cs ||
             r.out_off != q.out_off || r.cout != q.cout || r.lds_w_off != q.lds_w_off || r.part_stride != q.part_stride ||
-            r.st_mask_lo != q.st_mask_lo || r.st_mask_hi != q.st_mask_hi)
+            r.st_mask_lo != q.st_mask_lo || r.st_mask_hi != q.st_mask_hi || r.st_compact != q.st_compact)
             return false;
     }
     return true;

@@ -507,6 +507,30 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 for (const auto& g : c.gcg)
                     for (int bi : g.br) c.gc_fmt[bi] = PK_Q4;
             }
+            // streamed layers: compact t1 when the branches read fewer channels than conv_a writes
+            // (the reference group mode: one _d-channel window per branch). conv_a runs as k_pw for it
+            // (CNF_PW=0 selects k_conv1, which stores the full layout); CNF_T1_COMPACT=0 is the A/B knob
+            bool allow_c = true;
+            if (const char* e = std::getenv("CNF_PW")) allow_c = allow_c && std::atoi(e) != 0;
+            if (const char* e = std::getenv("CNF_T1_COMPACT")) allow_c = allow_c && std::atoi(e) != 0;
+            for (auto& c : p.couplings) {
+                c.t1_cs = c.nk;
+                c.t1_compact = false;
+                c.t1_used = 0;
+                c.t1_off.clear();
+                for (const Branch& b : c.br) {
+                    c.t1_off.push_back(b.cin_off);
+                    for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) c.t1_used |= 1ull << ch;
+                }
+                if (c.use_lds || c.R == 0 || c.br.empty() || c.nk > 64 || !allow_c) continue;
+                const int wdt = compact_width(c.t1_used);
+                if (wdt >= c.nk) continue;
+                c.t1_compact = true;
+                c.t1_cs = wdt;
+                for (size_t bi = 0; bi < c.br.size(); bi++) c.t1_off[bi] = compact_ch(c.t1_used, c.br[bi].cin_off);
+                for (auto& g : c.gcg)
+                    for (size_t k = 0; k < g.br.size(); k++) g.gcb[k].cin_off = c.t1_off[g.br[k]];
+            }
         }
 
         // kernel image (aux): every conv's weights + bias packed in its kernel's LDS layout
@@ -635,6 +659,21 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         if (!c.use_lds && !in_gc && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin)
                             pack(pw, PK_1X1, 9 * b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gpw.push_back(pw);
+                    }
+                    if (c.t1_compact && ln) {   // LN2 gamma/beta in the compact t1 layout (0 on padding)
+                        const int64_t hw = (int64_t)c.hc * c.wc, cs = c.t1_cs;
+                        int cmap[64];
+                        for (int j = 0; j < 64; j++) cmap[j] = -1;
+                        for (int ch = 0; ch < 64; ch++)
+                            if (compact_ch(c.t1_used, ch) >= 0) cmap[compact_ch(c.t1_used, ch)] = ch;
+                        for (int which = 0; which < 2; which++) {
+                            const int64_t src = which == 0 ? rb.ln2g : rb.ln2b;
+                            (which == 0 ? rb.ln2c_g : rb.ln2c_b) = p.n_aux;
+                            for (int64_t px = 0; px < hw; px++)
+                                for (int64_t j = 0; j < cs; j++)
+                                    p.aux_map.push_back(cmap[j] >= 0 ? src + px * nk + cmap[j] : -1);
+                            p.n_aux += hw * cs;
+                        }
                     }
                     pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
                          [=](int n) { return bb + n; });

@@ -47,6 +47,7 @@ struct RBParams {
     PackedConv ca, cb;                         // conv_a, conv_b (PK_1X1)
     std::vector<PackedConv> gc;                // grouped branches as dense 3x3 convs (PK_KN)
     std::vector<PackedConv> gpw;               // streamed, k_gc not fused: branch as a 1x1 over its 9*cin im2col row (size 0: none)
+    int64_t ln2c_g = -1, ln2c_b = -1;          // aux: LN2 gamma/beta gathered to the compact t1 layout (t1_compact)
 };
 
 struct NetParams {
@@ -96,6 +97,13 @@ struct Coupling {
     };
     std::vector<GcGroup> gcg;
     bool gc_fused = false;                // gcg non-empty
+    // streamed layers: t1 (conv_a's output) stored compactly, only the channels the grouped branches
+    // read (t1_used), laid out by compact_ch (cnf_kernels.h); t1_cs = its channel stride (nk when not
+    // compact) and t1_off[bi] = branch bi's input window offset in it
+    uint64_t t1_used = 0;
+    int t1_cs = 0;
+    bool t1_compact = false;
+    std::vector<int> t1_off;
     bool in_gc(int bi) const {
         for (const GcGroup& g : gcg)
             for (int b : g.br)
@@ -192,6 +200,7 @@ struct Plan {
     bool record = true;
     bool dry = false;         // host-only dry run: record launches without issuing them (shape dumps)
     std::vector<PwShape> pw_shapes;   // k_pw launch shapes seen by a dry run
+    std::vector<GcShape> gc_launch;   // dry runs: the k_gc launch shapes (GcArgs::s) as run_coupling issues them
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
     std::vector<Recorded> recorded;

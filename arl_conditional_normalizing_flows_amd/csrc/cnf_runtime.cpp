@@ -268,7 +268,7 @@ struct TapSrc {
 
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
 static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
-                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr) {
+                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, bool st_compact = false) {
     if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
     ConvArgs a;
@@ -318,6 +318,9 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         q.act = s.act;
         q.st_mask_lo = (uint32_t)(store_mask & 0xffffffffull);
         q.st_mask_hi = (uint32_t)(store_mask >> 32);
+        q.st_compact = st_compact ? 1 : 0;
+        if (st_compact && (s.res != nullptr || s.out_cs != compact_width(store_mask)))
+            throw std::logic_error("compact stores: no residual, out_cs == compact_width(mask)");
         if (s.cout > 64) throw std::invalid_argument("conv with more than 64 output channels");
         const int K = ks * ks * s.cin;
         q.nr = (s.cout + 15) / 16;
@@ -380,6 +383,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         fits32 = fits32 && (double)h * w * std::max(s.in_cs, s.out_cs) * 4.0 < 2147483648.0 &&
                  (tap == nullptr || (double)tap->img * 4.0 < 2147483648.0);
     const bool pw_ok = ks == 1 && vec && pw_gm > 0 && ln_uniform && fits32 && E.p.use_pw;
+    if (st_compact && !pw_ok) throw std::logic_error("compact stores need the k_pw path");
     if (ks == 3) {
         const int grid_x = E.B * g.tiles;
         const int mr = g.MR;
@@ -697,6 +701,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     };
     auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };
     const float* none = nullptr;
+    // LN2 gamma/beta in t1's layout: the aux copies gathered to the compact layout, or the parameters
+    auto ln2g = [&](const RBParams& rb) { return c.t1_compact ? X + rb.ln2c_g : P + rb.ln2g; };
+    auto ln2b = [&](const RBParams& rb) { return c.t1_compact ? X + rb.ln2c_b : P + rb.ln2b; };
 
     // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
     if (cin_tap) {
@@ -724,13 +731,12 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
                 pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + rb.ln1g : none,
-                                      ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.nk, 0, c.nk,
+                                      ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.t1_cs, 0, c.nk,
                                       none, out_slab(n, 1, 4 * nt1), 0, 1});
             }
-            uint64_t used = 0;
-            for (const Branch& b : c.br)
-                for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) used |= 1ull << ch;
-            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, used));
+            // only the channels the branches read are stored (packed by compact_ch when t1_compact);
+            // the LN2 statistics still cover all nk channels
+            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, c.t1_compact));
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]. The k_gc
         // launch (when planned) takes its branches first; every other branch runs as a k_pw tap-mode
@@ -748,8 +754,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 ga.out[n] = t2[n];
                 ga.in_part[n] = ln ? sl[n][1].part : nullptr;
                 ga.out_part[n] = ln ? sl[n][2].part + (size_t)base * LNP : nullptr;   // after earlier launches' slots
-                ga.gamma[n] = ln ? P + rb.ln2g : nullptr;
-                ga.beta[n] = ln ? P + rb.ln2b : nullptr;
+                ga.gamma[n] = ln ? ln2g(rb) : nullptr;
+                ga.beta[n] = ln ? ln2b(rb) : nullptr;
                 for (int k = 0; k < ng; k++) {
                     ga.w[n][k] = X + rb.gc[gg.br[k]].w;
                     ga.b[n][k] = X + rb.gc[gg.br[k]].b;
@@ -762,7 +768,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.s.nbr = ng;
             ga.s.H = c.hc;
             ga.s.W = c.wc;
-            ga.s.in_cs = c.nk;
+            ga.s.in_cs = c.t1_cs;
             ga.s.out_cs = c.gc;
             ga.B = B;
             ga.s.TH = gg.TH;
@@ -791,6 +797,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 by += 4.0 * B * c.hc * c.wc * b.cout * 2;
             }
             by += 4.0 * B * c.hc * c.wc * win * 2 + (ln ? 4.0 * 2 * c.hc * c.wc * win * 2 : 0.0);
+            if (E.p.dry) {
+                bool seen = false;
+                for (const GcShape& o : E.p.gc_launch) seen = seen || std::memcmp(&o, &ga.s, sizeof(GcShape)) == 0;
+                if (!seen) E.p.gc_launch.push_back(ga.s);
+            }
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
             base += gcw * ga.s.tiles_per_img;   // one slot per k_gc wave
         }
@@ -802,13 +813,13 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 std::vector<ProbSpec> pt;
                 for (int n = 0; n < 2; n++) {
                     const RBParams& rb = c.net[n].rb[r];
-                    pt.push_back(ProbSpec{t1[n], 9 * b.cin, 0, 9 * b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
-                                          ln ? P + rb.ln2b : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.gc,
+                    pt.push_back(ProbSpec{t1[n], 9 * b.cin, 0, 9 * b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
+                                          ln ? ln2b(rb) : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base, 1});
                 }
-                TapSrc ts{-1, c.wc, c.nk, b.cin, c.hc * c.wc * c.nk};
+                TapSrc ts{-1, c.wc, c.t1_cs, b.cin, c.hc * c.wc * c.t1_cs};
                 ts.dil = b.dil;
-                ts.off = b.cin_off;
+                ts.off = c.t1_off[bi];
                 base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts);
                 done[bi] = 1;
             }
@@ -819,8 +830,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
                     if (done[bi]) continue;
-                    pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? P + rb.ln2g : none,
-                                          ln ? P + rb.ln2b : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
+                    pr.push_back(ProbSpec{t1[n], c.t1_cs, c.t1_off[bi], b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
+                                          ln ? ln2b(rb) : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base + k * nt3 * 4, b.dil});
                     k++;
                 }
@@ -1478,12 +1489,25 @@ int cnf_debug_netlds_nshapes() { return netlds_num_shapes(); }
 
 // k_pw launch shapes of a B-image forward, from a host-only dry run (nothing is launched or
 // dereferenced: the tensors are placeholder addresses); returns the number of words written
+int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap);
+// k_gc launch shapes of a B-image forward (host-only dry run, as cnf_debug_pw_shapes)
+int cnf_debug_gc_launch_shapes(cnf_plan* plan, int B, int* words, int cap) {
+    if (!plan || !words || B <= 0) return -1;
+    const int n = cnf_debug_pw_shapes(plan, B, words, cap);   // the dry run also records the k_gc shapes
+    if (n < 0) return -1;
+    const std::vector<GcShape>& g = plan->p->gc_launch;
+    if ((int64_t)g.size() * GCSHAPE_WORDS > cap) return -1;
+    for (size_t i = 0; i < g.size(); i++) std::memcpy(words + i * GCSHAPE_WORDS, &g[i], sizeof(GcShape));
+    return (int)g.size() * GCSHAPE_WORDS;
+}
+
 int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap) {
     if (!plan || !words || B <= 0) return -1;
     Plan& p = *plan->p;
     CNF_TRY
     p.dry = true;
     p.pw_shapes.clear();
+    p.gc_launch.clear();
     char* fake = reinterpret_cast<char*>(uintptr_t(1) << 40);   // never dereferenced
     try {
         flow_forward(p, (const float*)fake, (const float*)fake, (const float*)fake, (float*)fake, (float*)fake, fake, B,
@@ -1521,7 +1545,7 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
         s.nbr = (int)gg.br.size();
         s.H = c.hc;
         s.W = c.wc;
-        s.in_cs = c.nk;
+        s.in_cs = c.t1_cs;   // as run_coupling launches it
         s.out_cs = c.gc;
         s.TH = gg.TH;
         s.TW = gg.TW;

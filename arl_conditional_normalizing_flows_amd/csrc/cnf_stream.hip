@@ -46,6 +46,18 @@ int read_pw_stamps(long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pw_stamps), sizeof(g_pw_stamps)) == hipSuccess ? 0 : -1;
 }
 
+// images of a wave in flight ahead of the one being computed (a ring of D buffers): one. Deeper
+// rings for the narrow non-residual convs measured slower at cfg2 B=64 (CNF_PW_DEPTH=2 / 4: conv_a
+// 19.1 -> 20.8 / 21.0 us, conv_out 11.9 -> 14.1 us; issuing them with the prologue's loads,
+// CNF_PW_EARLY=1, slower still), and for the residual conv_b in round 2
+#ifndef CNF_PW_DEPTH
+#define CNF_PW_DEPTH 1
+#endif
+#ifndef CNF_PW_EARLY
+#define CNF_PW_EARLY 0
+#endif
+constexpr int pw_depth(int gm, bool res) { return res ? 1 : gm <= 4 ? CNF_PW_DEPTH : (CNF_PW_DEPTH < 2 ? CNF_PW_DEPTH : 2); }
+
 template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false>
 __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -85,14 +97,24 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     const bool all_st = PP(st_mask_lo) == ~0u && PP(st_mask_hi) == ~0u;
     auto chv = [&](int n) { return cout % 16 == 0 || n * 16 + i16 < cout; };
     auto pv = [&](int r) { return full_px || po0 + r < HW; };
+    // compact stores (conv_a -> t1 of the streamed layers): the lane's channel of group n at its
+    // compact_ch index, -1 when not stored
+    int cch[NR];
+#pragma unroll
+    for (int n = 0; n < NR; n++)
+        cch[n] = PP(st_compact) ? compact_ch(((uint64_t)PP(st_mask_hi) << 32) | PP(st_mask_lo), n * 16 + i16) : 0;
+    const uint32_t cbase = ((uint32_t)po0 * PP(out_cs) + PP(out_off)) * 4u;
     auto ooff = [&](int n, int r) -> uint32_t {   // byte offset inside one image, BUF_OOB when not stored
         const int ch = n * 16 + i16;
+        if (PP(st_compact))
+            return (pv(r) && chv(n) && cch[n] >= 0) ? cbase + (uint32_t)(r * PP(out_cs) + cch[n]) * 4u : BUF_OOB;
         const bool st = all_st || ((ch < 32 ? (PP(st_mask_lo) >> ch) : (PP(st_mask_hi) >> (ch - 32))) & 1u) != 0u;
         return (pv(r) && chv(n) && st) ? obase + (uint32_t)(r * PP(out_cs) + 16 * n) * 4u : BUF_OOB;
     };
-    // image activations (+ residual) in registers, one image ahead (two ahead measured slower)
-    f4 x[GM];
-    float rv[NR][4];
+    // image activations (+ residual) in registers, a ring of D images (pw_depth)
+    constexpr int D = pw_depth(GM, RES);
+    f4 x[D][GM];
+    float rv[D][NR][4];
     // tap mode: element k = 16g + 4kq + j of the lane's im2col row -> offset inside one image of u
     auto toff = [&](int g, int j) -> uint32_t {
         const int k = 16 * g + 4 * kq + j;
@@ -140,7 +162,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
                 }
         }
     };
-    load_img(0, x, rv);
+    load_img(0, x[0], rv[0]);
     f4 gm[GM], bt[GM];
     if (LN) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
@@ -174,6 +196,13 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // memory round trip as the loads above and the weights below (folded after the weight copy)
     const bool lnpre = LN && wave < nimg && P.in_nparts <= 64;
     const f4 slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
+    // the rest of the ring's first images: in flight with the prologue's loads (CNF_PW_EARLY) or
+    // issued once the weights are in LDS
+    if (CNF_PW_EARLY) {
+#pragma unroll
+        for (int j = 1; j < D; j++)
+            if (j < nimg) load_img(j, x[j], rv[j]);
+    }
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
     int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
     asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
@@ -194,6 +223,11 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     PWSTAMP(1);
     __syncthreads();
     PWSTAMP(2);
+    if (!CNF_PW_EARLY) {
+#pragma unroll
+        for (int j = 1; j < D; j++)
+            if (j < nimg) load_img(j, x[j], rv[j]);
+    }
 
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
     // one image: A operand from xc / rc, which then receive image pf (when it exists)
@@ -276,9 +310,13 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             ln_partial(vals, valid,
                        P.out_part + ((size_t)img * PP(part_stride) + P.out_part_base + tile * NW + wave) * LNP);
     };
-    for (int ii = 0; ii < nimg; ii++) {
-        step(ii, x, rv, ii + 1);
-        PWSTAMP(3 + ii);
+    for (int i0 = 0; i0 < nimg; i0 += D) {
+#pragma unroll
+        for (int j = 0; j < D; j++) {
+            if (i0 + j >= nimg) break;
+            step(i0 + j, x[j], rv[j], i0 + j + D);   // buffer j then receives image i0 + j + D
+            PWSTAMP(3 + i0 + j);
+        }
     }
 }
 

@@ -30,7 +30,7 @@ OUT = HERE / 'cnf_netlds_shapes.inc'
 OUT_GC = HERE / 'cnf_gc_shapes.inc'
 OUT_PW = HERE / 'cnf_pw_shapes.inc'
 PW_BATCH = 64                 # the benchmark batch (k_pw shapes do not depend on it: ipw and B stay runtime)
-PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel masks
+PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel masks and st_compact
 GC_BRANCH_WORDS = 16          # GcBranch: 14 ints, then the two uint32 division magics
 GC_MAXBR = 8
 CNF_LAYER_COUPLING = 0
@@ -74,25 +74,21 @@ def shapes(lib):
 
 
 def gc_shapes(lib):
-    lib.cnf_debug_gc_shape.restype = C.c_int
-    lib.cnf_debug_gc_shape.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
+    """k_gc shapes as a dry run of the B-image forward launches them (GcArgs::s)"""
+    lib.cnf_debug_gc_launch_shapes.restype = C.c_int
+    lib.cnf_debug_gc_launch_shapes.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
     out = []
     for name in SPECIALISE:
         plan, _keep = _plan(lib, PRESETS[name])
-        info = _lib.cnf_layer_info()
-        buf = (C.c_int * CAP)()
-        for i in range(lib.cnf_plan_num_layers(plan)):
-            _lib.check(lib.cnf_plan_layer_info(plan, i, C.byref(info)), 'layer info')
-            if info.kind != CNF_LAYER_COUPLING:
-                continue
-            n = lib.cnf_debug_gc_shape(plan, info.coupling_index, buf, CAP)
-            if n < 0:
-                raise RuntimeError('cnf_debug_gc_shape failed')
-            nw = lib.cnf_debug_gc_words()   # GCSHAPE_WORDS: one GcShape per k_gc group
-            for g0 in range(0, n, nw):
-                w = tuple(buf[g0 + j] for j in range(nw))
-                if w not in out:
-                    out.append(w)
+        buf = (C.c_int * (CAP * 8))()
+        n = lib.cnf_debug_gc_launch_shapes(plan, PW_BATCH, buf, CAP * 8)
+        if n < 0:
+            raise RuntimeError('cnf_debug_gc_launch_shapes failed: ' + lib.cnf_last_error().decode())
+        nw = lib.cnf_debug_gc_words()   # GCSHAPE_WORDS
+        for g0 in range(0, n, nw):
+            w = tuple(buf[g0 + j] for j in range(nw))
+            if w not in out:
+                out.append(w)
         lib.cnf_plan_destroy(plan)
     return out
 
@@ -125,8 +121,9 @@ def render_pw(sh):
         if w is None:
             lines.append('    {},')
             continue
-        k = len(w) - PW_MASK_WORDS
-        lines.append('    {' + ', '.join([str(x) for x in w[:k]] + [f'{x & 0xffffffff}u' for x in w[k:]]) + '},')
+        k = len(w) - PW_MASK_WORDS - 1
+        lines.append('    {' + ', '.join([str(x) for x in w[:k]] + [f'{x & 0xffffffff}u' for x in w[k:-1]] +
+                                       [str(w[-1])]) + '},')
     lines.append('};')
     return '\n'.join(lines) + '\n'
 

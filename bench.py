@@ -132,6 +132,15 @@ def roofline_for(launches):
         k: dict(roofline_of(v['flops'], v['bytes'], v['ms']), ms_per_step=round(v['ms'], 4), launches=v['launches'],
                 avg_launch_us=round(v['ms'] * 1e3 / v['launches'], 3))
         for k, v in sorted(per.items(), key=lambda kv: -kv[1]['ms'])}
+    # the same by launch name (kernel + role, e.g. k_pw<4,4,conv_a>): the ResNeXt stages of one symbol apart
+    roles = {}
+    for nm, fl, by, ms in launches:
+        if nm.startswith('k_'):
+            d = roles.setdefault(nm, [0.0, 0])
+            d[0] += ms
+            d[1] += 1
+    rf['per_role'] = {k: {'ms_per_step': round(v[0], 4), 'launches': v[1], 'avg_launch_us': round(v[0] * 1e3 / v[1], 3)}
+                      for k, v in sorted(roles.items(), key=lambda kv: -kv[1][0])}
     return rf, per
 
 

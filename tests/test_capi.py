@@ -167,6 +167,7 @@ def test_grouped_conv_images_are_the_per_group_kernels(lib, name, gm):
         # the packed kernel image: conv elements only, each grouped kernel element equally often
         aux = _weight_map(lib, p, 0)
         assert aux.size == lib.cnf_plan_aux_floats(p)
+        specs = {f'c{c.index}': c for c in o.coupling_specs}
         cnt = np.bincount(aux[aux >= 0], minlength=o.num_params())
         for n_, (k0, s_) in offs.items():
             size = int(np.prod(s_)) if s_ else 1
@@ -175,6 +176,16 @@ def test_grouped_conv_images_are_the_per_group_kernels(lib, name, gm):
                 assert seg.min() >= 1, n_
                 if '.gc.' in n_:
                     assert seg.min() == seg.max(), n_
+            elif '.ln2.' in n_ and seg.max() > 0:
+                # streamed layers store t1 compactly (only the grouped branches' input windows): their
+                # LN2 gamma/beta are gathered once into that layout, the same channels at every pixel
+                c = specs[n_.split('.')[0]]
+                used = np.zeros(c.nk, np.int64)
+                for br in c.branches:
+                    for off in br.in_offsets:
+                        used[off:off + br.width] = 1
+                rows = seg.reshape(-1, c.nk)
+                assert used.sum() < c.nk and np.array_equal(rows, np.broadcast_to(used, rows.shape)), n_
             else:
                 assert seg.max() == 0, n_
     finally:
