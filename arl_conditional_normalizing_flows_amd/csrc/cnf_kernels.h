@@ -64,7 +64,8 @@ struct ConvProb {
     int S, Kpad, NS, nr;                   // LDS pixel stride, padded K, B row stride, N-subtiles
     uint32_t cin_mag, wp_mag;              // magic multipliers: x / cin == umulhi(x, cin_mag) (3x3 staging)
     uint32_t st_mask_lo, st_mask_hi;       // output channels actually stored (bit per channel < 64)
-    int st_compact;                        // 1: stored channels packed by compact_ch (k_pw only)
+    int st_compact;                        // 1: stores through st_map (k_pw only)
+    const int* st_map;                     // [64][2]: channel -> (offset of pixel 0 inside the image, pixel stride) in floats, offset < 0: not stored
 };
 
 // Compact channel layout of a tensor of which only the channels in mask m are ever read (t1 of the
@@ -208,10 +209,11 @@ constexpr int GC_MAXBR = 8;
 constexpr int GC_NW_GEN = 8, GC_NW_SPEC = 16, GC_NW_MAX = 16;
 constexpr int GC_STAGE_QUADS = 2048;   // staged band quads per workgroup
 struct GcBranch {
-    int cin_off, cin, cinp, cout, out_off, dil;   // input window, padded channels, outputs
+    int cin_off, cin, cinp, cout, out_off, dil;   // input window (cin_off: floats from the image start to pixel 0's window), padded channels, outputs
     int G;                                        // quad groups of the PK_Q4 image
     int band_off, BW, BH, S;                      // LDS band: byte offset, width, height, pixel stride
     int w_off, q_off, b_off;                      // LDS byte offsets: packed weights, quad offsets, bias
+    int pcs;                                      // pixel stride of the input window (floats)
     uint32_t cpq_mag, bw_mag;                     // x / (cinp/4) == umulhi(x, cpq_mag) (cinp > 4), x / BW likewise
 };
 struct GcShape {

@@ -507,29 +507,81 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 for (const auto& g : c.gcg)
                     for (int bi : g.br) c.gc_fmt[bi] = PK_Q4;
             }
-            // streamed layers: compact t1 when the branches read fewer channels than conv_a writes
-            // (the reference group mode: one _d-channel window per branch). conv_a runs as k_pw for it
-            // (CNF_PW=0 selects k_conv1, which stores the full layout); CNF_T1_COMPACT=0 is the A/B knob
+            // streamed layers: t1 as one dense sub-tensor per consumer of it (Coupling::t1_map): each
+            // k_gc group (and each branch launched on its own) reads only its windows, 16-byte aligned,
+            // instead of a few channels out of every 256-byte pixel. conv_a runs as k_pw for it (CNF_PW=0
+            // selects k_conv1, which stores the plain layout), and no branch may be left to k_conv<3>
+            // (plain layout only); CNF_T1_COMPACT=0 is the A/B knob
             bool allow_c = true;
             if (const char* e = std::getenv("CNF_PW")) allow_c = allow_c && std::atoi(e) != 0;
             if (const char* e = std::getenv("CNF_T1_COMPACT")) allow_c = allow_c && std::atoi(e) != 0;
+            int tap_dmin = 4;
+            if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin = std::atoi(e);   // as the packing below
             for (auto& c : p.couplings) {
                 c.t1_cs = c.nk;
                 c.t1_compact = false;
                 c.t1_used = 0;
                 c.t1_off.clear();
+                c.t1_pcs.clear();
+                c.t1_map.clear();
                 for (const Branch& b : c.br) {
                     c.t1_off.push_back(b.cin_off);
+                    c.t1_pcs.push_back(c.nk);
                     for (int ch = b.cin_off; ch < b.cin_off + b.cin && ch < 64; ch++) c.t1_used |= 1ull << ch;
                 }
-                if (c.use_lds || c.R == 0 || c.br.empty() || c.nk > 64 || !allow_c) continue;
-                const int wdt = compact_width(c.t1_used);
-                if (wdt >= c.nk) continue;
-                c.t1_compact = true;
-                c.t1_cs = wdt;
-                for (size_t bi = 0; bi < c.br.size(); bi++) c.t1_off[bi] = compact_ch(c.t1_used, c.br[bi].cin_off);
                 for (auto& g : c.gcg)
-                    for (size_t k = 0; k < g.br.size(); k++) g.gcb[k].cin_off = c.t1_off[g.br[k]];
+                    for (size_t k = 0; k < g.br.size(); k++) {
+                        g.gcb[k].cin_off = c.br[g.br[k]].cin_off;
+                        g.gcb[k].pcs = c.nk;
+                    }
+                if (c.use_lds || c.R == 0 || c.br.empty() || c.nk > 64 || !allow_c) continue;
+                // consumers: the k_gc groups, then every other branch (k_pw tap mode) on its own
+                std::vector<std::vector<int>> units;
+                for (const auto& g : c.gcg) units.push_back(g.br);
+                bool ok = true;
+                for (size_t bi = 0; bi < c.br.size(); bi++) {
+                    if (c.in_gc((int)bi)) continue;
+                    const Branch& b = c.br[bi];
+                    ok = ok && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin;
+                    units.push_back({(int)bi});
+                }
+                if (!ok) continue;
+                std::vector<uint64_t> um;
+                uint64_t seen = 0;
+                int total = 0;
+                for (const auto& u : units) {
+                    uint64_t m = 0;
+                    for (int bi : u)
+                        for (int ch = c.br[bi].cin_off; ch < c.br[bi].cin_off + c.br[bi].cin; ch++) m |= 1ull << ch;
+                    ok = ok && (m & seen) == 0;   // a channel stored twice: plain layout
+                    seen |= m;
+                    um.push_back(m);
+                    total += compact_width(m);
+                }
+                if (!ok || (units.size() == 1 && total >= c.nk)) continue;
+                const int hw = c.hc * c.wc;
+                c.t1_compact = true;
+                c.t1_cs = total;
+                c.t1_map.assign(128, -1);
+                int base = 0;   // floats from the image start to the sub-tensor
+                for (size_t u = 0; u < units.size(); u++) {
+                    const int cs = compact_width(um[u]);
+                    for (int ch = 0; ch < 64; ch++)
+                        if ((um[u] >> ch) & 1ull) {
+                            c.t1_map[2 * ch] = base + compact_ch(um[u], ch);
+                            c.t1_map[2 * ch + 1] = cs;
+                        }
+                    for (int bi : units[u]) {
+                        c.t1_off[bi] = c.t1_map[2 * c.br[bi].cin_off];
+                        c.t1_pcs[bi] = cs;
+                    }
+                    base += hw * cs;
+                }
+                for (auto& g : c.gcg)
+                    for (size_t k = 0; k < g.br.size(); k++) {
+                        g.gcb[k].cin_off = c.t1_off[g.br[k]];
+                        g.gcb[k].pcs = c.t1_pcs[g.br[k]];
+                    }
             }
         }
 
@@ -660,19 +712,17 @@ Plan* build_plan(const cnf_flow_desc* d) {
                             pack(pw, PK_1X1, 9 * b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });
                         rb.gpw.push_back(pw);
                     }
-                    if (c.t1_compact && ln) {   // LN2 gamma/beta in the compact t1 layout (0 on padding)
-                        const int64_t hw = (int64_t)c.hc * c.wc, cs = c.t1_cs;
-                        int cmap[64];
-                        for (int j = 0; j < 64; j++) cmap[j] = -1;
+                    if (c.t1_compact && ln) {   // LN2 gamma/beta in t1's layout (0 on padding)
+                        const int64_t hw = (int64_t)c.hc * c.wc;
+                        std::vector<int64_t> at((size_t)hw * c.t1_cs, -1);   // image float -> t1 channel's param
                         for (int ch = 0; ch < 64; ch++)
-                            if (compact_ch(c.t1_used, ch) >= 0) cmap[compact_ch(c.t1_used, ch)] = ch;
+                            if (c.t1_map[2 * ch] >= 0)
+                                for (int64_t px = 0; px < hw; px++) at[c.t1_map[2 * ch] + px * c.t1_map[2 * ch + 1]] = px * nk + ch;
                         for (int which = 0; which < 2; which++) {
                             const int64_t src = which == 0 ? rb.ln2g : rb.ln2b;
                             (which == 0 ? rb.ln2c_g : rb.ln2c_b) = p.n_aux;
-                            for (int64_t px = 0; px < hw; px++)
-                                for (int64_t j = 0; j < cs; j++)
-                                    p.aux_map.push_back(cmap[j] >= 0 ? src + px * nk + cmap[j] : -1);
-                            p.n_aux += hw * cs;
+                            for (int64_t v : at) p.aux_map.push_back(v >= 0 ? src + v : -1);
+                            p.n_aux += (int64_t)at.size();
                         }
                     }
                     pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
@@ -785,6 +835,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
         for (auto& c : p.couplings) {
             c.dev_lds_offs = (int)p.host_table.size();
             p.host_table.insert(p.host_table.end(), c.lds_offs.begin(), c.lds_offs.end());
+            if (c.t1_compact) {
+                c.dev_t1_map = (int)p.host_table.size();
+                p.host_table.insert(p.host_table.end(), c.t1_map.begin(), c.t1_map.end());
+            }
         }
         p.dev_final_orig = (int)p.host_table.size();
         p.host_table.insert(p.host_table.end(), p.final_orig.begin(), p.final_orig.end());

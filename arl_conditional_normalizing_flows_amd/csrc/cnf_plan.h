@@ -97,13 +97,17 @@ struct Coupling {
     };
     std::vector<GcGroup> gcg;
     bool gc_fused = false;                // gcg non-empty
-    // streamed layers: t1 (conv_a's output) stored compactly, only the channels the grouped branches
-    // read (t1_used), laid out by compact_ch (cnf_kernels.h); t1_cs = its channel stride (nk when not
-    // compact) and t1_off[bi] = branch bi's input window offset in it
+    // streamed layers: t1 (conv_a's output) holds only the channels the grouped branches read, one
+    // dense sub-tensor per consumer (a k_gc group, or a branch launched on its own) inside each
+    // image: sub-tensor u = [HW][cs_u] at float offset HW * (cs_0 + ... + cs_{u-1}), its windows
+    // packed by compact_ch (quad-aligned runs). t1_cs = floats per pixel of an image (nk when plain),
+    // t1_off[bi] / t1_pcs[bi] = branch bi's window: offset of pixel 0 inside the image, pixel
+    // stride; t1_map[2c], [2c+1] = the same for channel c (-1: not stored)
     uint64_t t1_used = 0;
     int t1_cs = 0;
     bool t1_compact = false;
-    std::vector<int> t1_off;
+    std::vector<int> t1_off, t1_pcs, t1_map;
+    int dev_t1_map = -1;   // offset of t1_map in the device table
     bool in_gc(int bi) const {
         for (const GcGroup& g : gcg)
             for (int b : g.br)

@@ -268,7 +268,8 @@ struct TapSrc {
 
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
 static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
-                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, bool st_compact = false) {
+                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, const int* st_map = nullptr) {
+    const bool st_compact = st_map != nullptr;
     if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
     ConvArgs a;
@@ -319,8 +320,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         q.st_mask_lo = (uint32_t)(store_mask & 0xffffffffull);
         q.st_mask_hi = (uint32_t)(store_mask >> 32);
         q.st_compact = st_compact ? 1 : 0;
-        if (st_compact && (s.res != nullptr || s.out_cs != compact_width(store_mask)))
-            throw std::logic_error("compact stores: no residual, out_cs == compact_width(mask)");
+        q.st_map = st_map;
+        if (st_compact && (s.res != nullptr || s.cout > 64)) throw std::logic_error("mapped stores: no residual, <= 64 outputs");
         if (s.cout > 64) throw std::invalid_argument("conv with more than 64 output channels");
         const int K = ks * ks * s.cin;
         q.nr = (s.cout + 15) / 16;
@@ -734,9 +735,12 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                       ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.t1_cs, 0, c.nk,
                                       none, out_slab(n, 1, 4 * nt1), 0, 1});
             }
-            // only the channels the branches read are stored (packed by compact_ch when t1_compact);
-            // the LN2 statistics still cover all nk channels
-            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, c.t1_compact));
+            // only the channels the branches read are stored (into their consumers' sub-tensors when
+            // t1_compact); the LN2 statistics still cover all nk channels
+            const int* t1map = c.t1_compact ? (E.p.dry ? reinterpret_cast<const int*>(uintptr_t(1) << 40)
+                                                       : E.p.dev_table + c.dev_t1_map)
+                                            : nullptr;
+            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map));
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]. The k_gc
         // launch (when planned) takes its branches first; every other branch runs as a k_pw tap-mode
@@ -817,7 +821,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                                           ln ? ln2b(rb) : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base, 1});
                 }
-                TapSrc ts{-1, c.wc, c.t1_cs, b.cin, c.hc * c.wc * c.t1_cs};
+                TapSrc ts{-1, c.wc, c.t1_pcs[bi], b.cin, c.hc * c.wc * c.t1_cs};
                 ts.dil = b.dil;
                 ts.off = c.t1_off[bi];
                 base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts);
@@ -830,7 +834,8 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
                     if (done[bi]) continue;
-                    pr.push_back(ProbSpec{t1[n], c.t1_cs, c.t1_off[bi], b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
+                    if (c.t1_compact) throw std::logic_error("k_conv<3> branch on a mapped t1 layout");
+                    pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
                                           ln ? ln2b(rb) : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base + k * nt3 * 4, b.dil});
                     k++;

@@ -97,17 +97,18 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     const bool all_st = PP(st_mask_lo) == ~0u && PP(st_mask_hi) == ~0u;
     auto chv = [&](int n) { return cout % 16 == 0 || n * 16 + i16 < cout; };
     auto pv = [&](int r) { return full_px || po0 + r < HW; };
-    // compact stores (conv_a -> t1 of the streamed layers): the lane's channel of group n at its
-    // compact_ch index, -1 when not stored
-    int cch[NR];
+    // mapped stores (conv_a -> t1 of the streamed layers, Coupling::t1_map): the lane's channel of
+    // group n goes to (offset of pixel 0, pixel stride) inside the image; offset < 0: not stored
+    int cmo[NR], cms[NR];
 #pragma unroll
-    for (int n = 0; n < NR; n++)
-        cch[n] = PP(st_compact) ? compact_ch(((uint64_t)PP(st_mask_hi) << 32) | PP(st_mask_lo), n * 16 + i16) : 0;
-    const uint32_t cbase = ((uint32_t)po0 * PP(out_cs) + PP(out_off)) * 4u;
+    for (int n = 0; n < NR; n++) {
+        cmo[n] = PP(st_compact) && n * 16 + i16 < 64 ? P.st_map[2 * (n * 16 + i16)] : -1;
+        cms[n] = PP(st_compact) && n * 16 + i16 < 64 ? P.st_map[2 * (n * 16 + i16) + 1] : 0;
+    }
     auto ooff = [&](int n, int r) -> uint32_t {   // byte offset inside one image, BUF_OOB when not stored
         const int ch = n * 16 + i16;
         if (PP(st_compact))
-            return (pv(r) && chv(n) && cch[n] >= 0) ? cbase + (uint32_t)(r * PP(out_cs) + cch[n]) * 4u : BUF_OOB;
+            return (pv(r) && chv(n) && cmo[n] >= 0) ? (uint32_t)(cmo[n] + (po0 + r) * cms[n]) * 4u : BUF_OOB;
         const bool st = all_st || ((ch < 32 ? (PP(st_mask_lo) >> ch) : (PP(st_mask_hi) >> (ch - 32))) & 1u) != 0u;
         return (pv(r) && chv(n) && st) ? obase + (uint32_t)(r * PP(out_cs) + 16 * n) * 4u : BUF_OOB;
     };
@@ -568,9 +569,9 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
                 const int y = r0 - br.dil + brr, x = c0 + bc - br.dil;
                 loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
                 if (y >= 0 && y < H && x >= 0 && x < W) {
-                    soff[u] = (y * W + x) * GS(in_cs) + br.cin_off + 4 * cq;
+                    soff[u] = (y * W + x) * br.pcs + br.cin_off + 4 * cq;
                     const int v = min(4, br.cin - 4 * cq);
-                    const bool vec = v == 4 && ((br.cin_off | GS(in_cs)) & 3) == 0;
+                    const bool vec = v == 4 && ((br.cin_off | br.pcs) & 3) == 0;
                     nv[u] = v | (vec ? 8 : 0);
                 }
                 break;

@@ -31,7 +31,7 @@ OUT_GC = HERE / 'cnf_gc_shapes.inc'
 OUT_PW = HERE / 'cnf_pw_shapes.inc'
 PW_BATCH = 64                 # the benchmark batch (k_pw shapes do not depend on it: ipw and B stay runtime)
 PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel masks and st_compact
-GC_BRANCH_WORDS = 16          # GcBranch: 14 ints, then the two uint32 division magics
+GC_BRANCH_WORDS = 17          # GcBranch: 15 ints, then the two uint32 division magics
 GC_MAXBR = 8
 CNF_LAYER_COUPLING = 0
 CAP = 2048
