@@ -222,6 +222,14 @@ struct GcShape {
     int TW, tiles_x;             // tile width (W, or a divisor of W for wide images) and column tiles
     int band_bytes;              // offset of the second band buffer (double-buffered staging)
     int lnst;                    // bit 0: LN2 on load (in_part set), bit 1: LN3 partials out (out_part set)
+    // polyphase tiles (ps > 1, one branch of dilation ps): the image splits into ps*ps phase grids
+    // (pixels a + i*ps, b + j*ps) of (H/ps) x (W/ps), on which the dilated conv is a dilation-1 conv;
+    // a tile is nbk whole phase grids (TH x TW each, nbk > 1) or a TH-row slice of one (tpp slices per
+    // grid), its band one (TH+2) x (TW+2) block per grid: the halo of the dilation no longer scales
+    // with ps
+    int ps, nbk, tpp;
+    int nw;                      // waves per workgroup of the shape-specialised instantiation (16, or 4 for
+                                 // small bands: four workgroups per CU hide each other's per-image latency)
 };
 constexpr int GCSHAPE_WORDS = (int)(sizeof(GcShape) / 4);
 struct GcArgs {

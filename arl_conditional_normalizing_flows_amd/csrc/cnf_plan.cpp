@@ -411,10 +411,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.gcg.clear();
                 c.gc_fused = false;
                 if (c.use_lds || c.R == 0 || c.br.empty() || c.br.size() > (size_t)GC_MAXBR || !allow_gc) continue;
-                auto fit = [&](const std::vector<int>& sel, int TW, int TP, Coupling::GcGroup& out) -> bool {
-                    int TH = std::max(1, std::min(c.hc, TP / TW));   // TP-pixel tiles
-                    if (TW == c.wc)
-                        if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
+                // band geometry of a group at tile TH x TW: one band per branch, nblk blocks of
+                // (TH + 2 dil) x (TW + 2 dil) stacked by rows (nblk > 1 / dil_eff: polyphase tiles)
+                auto fit_geo = [&](const std::vector<int>& sel, int TH, int TW, int dil_eff, int nblk,
+                                   Coupling::GcGroup& out, int nw = GC_NW_SPEC) -> bool {
                     int64_t off = 512;   // [256, 384): per-image LN table
                     std::vector<GcBranch> gb;
                     for (int bi : sel) {
@@ -425,10 +425,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         g.cinp = (b.cin + 3) / 4 * 4;
                         g.cout = b.cout;
                         g.out_off = b.out_off;
-                        g.dil = b.dil;
+                        g.dil = dil_eff > 0 ? dil_eff : b.dil;
                         g.G = (9 * (g.cinp / 4) + 3) / 4;
-                        g.BW = TW + 2 * b.dil;
-                        g.BH = TH + 2 * b.dil;
+                        g.BW = TW + 2 * g.dil;
+                        g.BH = nblk * (TH + 2 * g.dil);
                         g.S = stride8(g.cinp);
                         // exact umulhi division for x < 2^16 (x * d < 2^32)
                         g.cpq_mag = g.cinp == 4 ? 0u : (uint32_t)((((uint64_t)1 << 32) + (g.cinp / 4) - 1) / (g.cinp / 4));
@@ -443,7 +443,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
                         gb.push_back(g);
                     }
-                    int64_t quads = 0;   // staged band quads: at most GC_STAGE_QUADS per workgroup
+                    int64_t quads = 0;   // staged band quads: at most 128 per wave (2 per thread)
                     for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
                     // two band buffers: the next image is staged while the current one is computed
                     const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
@@ -452,7 +452,9 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         g.b_off = (int)off;
                         off = align16(off + 4LL * g.cout);
                     }
-                    if (off > 160 * 1024 || quads > GC_STAGE_QUADS) return false;
+                    // nw < 16: 16 / nw workgroups share a CU, so its LDS
+                    if (off > 160 * 1024 / (GC_NW_SPEC / nw) || quads > 128LL * nw) return false;
+                    out.nw = nw;
                     out.br = sel;
                     out.gcb = gb;
                     out.TH = TH;
@@ -461,6 +463,14 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     out.tiles_y = (c.hc + TH - 1) / TH;
                     out.lds = (int)off;
                     out.band_bytes = (int)band_bytes;
+                    out.TP = TH * TW;
+                    return true;
+                };
+                auto fit = [&](const std::vector<int>& sel, int TW, int TP, Coupling::GcGroup& out) -> bool {
+                    int TH = std::max(1, std::min(c.hc, TP / TW));   // TP-pixel tiles
+                    if (TW == c.wc)
+                        if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
+                    if (!fit_geo(sel, TH, TW, 0, 1, out)) return false;
                     out.TP = TP;
                     return true;
                 };
@@ -503,6 +513,61 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     }
                 }
                 if (have) c.gcg.push_back(cur);
+                // a group of one large-dilation branch on polyphase tiles when its phase grids are whole
+                // (H, W divisible by the dilation): bands of (TH+2) x (TW+2) per grid instead of
+                // (TH + 2d) x (TW + 2d) (cfg5's dilation-16 branch: 400 staged pixels per 256 outputs
+                // instead of 1920 per 128); CNF_GC_POLY=0 is the A/B knob
+                static const bool poly = [] {
+                    const char* e = std::getenv("CNF_GC_POLY");
+                    return !(e && std::atoi(e) == 0);
+                }();
+                for (auto& gg : c.gcg) {
+                    if (!poly || gg.br.size() != 1) continue;
+                    const Branch& b = c.br[gg.br[0]];
+                    const int d = b.dil;
+                    if (d < 4 || c.hc % d || c.wc % d) continue;
+                    const int hs = c.hc / d, wsb = c.wc / d;
+                    if (wsb > 256 || hs * wsb < 1) continue;
+                    // tiles of TP pixels: nbk whole grids, or TH-row slices of one grid
+                    auto tile_for = [&](int TP, int& nbk, int& TH, int& tpp) {
+                        nbk = 1;
+                        TH = hs;
+                        tpp = 1;
+                        if (hs * wsb <= TP) {
+                            while (nbk * 2 * hs * wsb <= TP && (d * d) % (nbk * 2) == 0) nbk *= 2;
+                        } else {
+                            TH = std::max(1, TP / wsb);
+                            while (hs % TH) TH--;
+                            tpp = hs / TH;
+                        }
+                    };
+                    // four 4-wave workgroups per CU when the band is small (these branches have little
+                    // MFMA work per image: their time is per-image latency, which co-resident
+                    // workgroups hide; tiles down to 128 pixels for it), else one 16-wave workgroup
+                    static const int poly_nw = [] {
+                        const char* e = std::getenv("CNF_GC_POLY_NW");   // A/B knob
+                        return e ? std::atoi(e) : 4;
+                    }();
+                    Coupling::GcGroup g;
+                    int nbk = 1, TH = hs, tpp = 1;
+                    bool ok = false;
+                    for (int TP : {256, 128}) {
+                        if (poly_nw != 4) break;
+                        tile_for(TP, nbk, TH, tpp);
+                        if ((ok = fit_geo(gg.br, TH, wsb, 1, nbk, g, 4))) break;
+                    }
+                    if (!ok) {
+                        tile_for(256, nbk, TH, tpp);
+                        ok = fit_geo(gg.br, TH, wsb, 1, nbk, g);
+                    }
+                    if (!ok) continue;
+                    g.ps = d;
+                    g.nbk = nbk;
+                    g.tpp = tpp;
+                    g.tiles_x = 1;
+                    g.tiles_y = (d * d / nbk) * tpp;
+                    gg = g;
+                }
                 c.gc_fused = !c.gcg.empty();
                 for (const auto& g : c.gcg)
                     for (int bi : g.br) c.gc_fmt[bi] = PK_Q4;

@@ -94,6 +94,8 @@ struct Coupling {
         int tiles() const { return tiles_y * tiles_x; }
         int tiles_y = 1;
         int TP = 0;                       // tile pixels the plan aimed at (TH = min(H, TP / TW))
+        int ps = 1, nbk = 1, tpp = 1;     // polyphase tiles (GcShape): phase stride, grids per tile, slices per grid
+        int nw = GC_NW_SPEC;              // waves per workgroup (GcShape::nw)
     };
     std::vector<GcGroup> gcg;
     bool gc_fused = false;                // gcg non-empty

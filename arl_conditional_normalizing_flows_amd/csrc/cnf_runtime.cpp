@@ -779,12 +779,18 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.s.TW = gg.TW;
             ga.s.tiles_x = gg.tiles_x;
             ga.s.tiles_per_img = gg.tiles();
+            ga.s.ps = gg.ps;
+            ga.s.nbk = gg.nbk;
+            ga.s.tpp = gg.tpp;
+            ga.s.nw = gg.nw;
             ga.in_nparts = sl[0][1].nparts;
             ga.part_stride = L.st_parts;
             // images per workgroup: one workgroup per CU, looping over its images with the next
             // image's band staged behind the current one's MFMAs
+            // (16 / nw workgroups per CU)
             const int64_t units = (int64_t)ga.s.tiles_per_img * 2 * B;
-            ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 255) / 256));
+            const int64_t slots = 256LL * (GC_NW_SPEC / gg.nw);
+            ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + slots - 1) / slots));
             ga.s.band_bytes = gg.band_bytes;
             ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
             if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
@@ -1556,6 +1562,10 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
         s.TW = gg.TW;
         s.tiles_x = gg.tiles_x;
         s.tiles_per_img = gg.tiles();
+        s.ps = gg.ps;
+        s.nbk = gg.nbk;
+        s.tpp = gg.tpp;
+        s.nw = gg.nw;
         s.band_bytes = gg.band_bytes;
         s.lnst = p.desc.layer_norm ? 3 : 0;   // the forward's k_gc: LN2 on load and LN3 partials iff LayerNorm
         std::memcpy(words + n, &s, sizeof(s));

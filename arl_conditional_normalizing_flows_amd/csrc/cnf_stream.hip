@@ -387,17 +387,32 @@ namespace cnf {
 // dense 3x3 dilated conv -> t2 slices, plus the per-wave LN3 partials of LeakyReLU(t2).
 // ---------------------------------------------------------------------------------------------
 // waves / threads of the instantiation for table entry SID (-1: generic)
-#define GC_NWS (SID >= 0 ? GC_NW_SPEC : GC_NW_GEN)
+#define GC_NWS (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].nw : GC_NW_GEN)
 #define GC_NTS (64 * GC_NWS)
 
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
 #define GS(f) (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].f : a.s.f)
 
 // BI >= 0 (specialised instantiations): branch BI of table entry SID, every field a constant
+// tile pixel -> image pixel: full-width / 2-D tiles (ps == 1: px0 + row * W + column), or polyphase
+// tiles (block blk of the tile = phase grid ph0 + blk, pixel (r0 + row, column) of that grid)
+template <int SID>
+__device__ __forceinline__ int gc_out_pixel(const GcArgs& a, int po, int px0, int r0, int ph0) {
+    const int tpx = GS(TH) * GS(TW);
+    const int blk = GS(nbk) > 1 ? po / tpx : 0;
+    const int rem = po - blk * tpx;
+    const int por = rem / GS(TW), poc = rem - por * GS(TW);
+    if (GS(ps) > 1) {
+        const int ph = ph0 + blk, pa = ph / GS(ps), pb = ph - pa * GS(ps);
+        return (pa + (r0 + por) * GS(ps)) * GS(W) + pb + poc * GS(ps);
+    }
+    return px0 + por * GS(W) + poc;
+}
+
 template <int NR, int SID, int BI>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, const unsigned char* smem,
                                           const float* bias, float* __restrict__ outp, int npx,
-                                          int px0, LnAcc& st, bool& first, bool stats, int boff) {
+                                          int px0, int r0, int ph0, LnAcc& st, bool& first, bool stats, int boff) {
     const GcBranch& br = BI >= 0 ? kGcShapes[SID >= 0 ? SID : 0].br[BI >= 0 ? BI : 0] : brx;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
@@ -432,8 +447,12 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
         for (int h = 0; h < 2; h++) {
             const int pt = (h ? s1 : s0) * 16 + i16;
             const int ptc = pt < npx ? pt : 0;
-            const int tr = ptc / GS(TW), tc = ptc - tr * GS(TW);
-            base[h] = band + (tr * br.BW + tc) * br.S;
+            // block blk of a polyphase tile: band rows [blk (TH + 2 dil), ...)
+            const int tpx = GS(TH) * GS(TW);
+            const int blk = GS(nbk) > 1 ? ptc / tpx : 0;
+            const int rem = ptc - blk * tpx;
+            const int tr = rem / GS(TW), tc = rem - tr * GS(TW);
+            base[h] = band + ((blk * (GS(TH) + 2 * br.dil) + tr) * br.BW + tc) * br.S;
         }
         f4 acc0[NR], acc1[NR];
 #pragma unroll
@@ -476,9 +495,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             if (h == 1 && !v1) break;
             const int po = (h ? s1 : s0) * 16 + i16;
             const bool pv = po < npx;
-            // tile pixel po -> image pixel px0 + row * W + column (== px0 + po for full-width tiles)
-            const int por = po / GS(TW), poc = po - por * GS(TW);
-            float* orow = outp + (size_t)(px0 + por * GS(W) + poc) * GS(out_cs) + br.out_off + 4 * kq;
+            float* orow = outp + (size_t)gc_out_pixel<SID>(a, pv ? po : 0, px0, r0, ph0) * GS(out_cs) + br.out_off + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NR; n++) {
                 f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
@@ -498,17 +515,20 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     }
 }
 
-#define GC_GQS (GC_STAGE_QUADS / GC_NTS)   // staged band quads per thread (the plan checks the total fits)
+// staged band quads per thread: 2 in the specialised instantiations (the plan keeps a group's bands
+// within 128 quads per wave), GC_STAGE_QUADS over the generic kernel's threads
+#define GC_GQS (SID >= 0 ? 2 : GC_STAGE_QUADS / GC_NTS)
 
 // the branches of table entry SID, unrolled at compile time
 template <int SID, int BI>
 __device__ __forceinline__ void gc_branches(const GcArgs& a, const unsigned char* smem, float* __restrict__ outp,
-                                            int npx, int px0, LnAcc& st, bool& first, bool stats, int boff) {
+                                            int npx, int px0, int r0, int ph0, LnAcc& st, bool& first, bool stats,
+                                            int boff) {
     if constexpr (BI < kGcShapes[SID].nbr) {
         constexpr GcBranch br = kGcShapes[SID].br[BI];
         const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
-        gc_branch<(br.cout + 15) / 16, SID, BI>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff);
-        gc_branches<SID, BI + 1>(a, smem, outp, npx, px0, st, first, stats, boff);
+        gc_branch<(br.cout + 15) / 16, SID, BI>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff);
+        gc_branches<SID, BI + 1>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff);
     }
 }
 
@@ -530,7 +550,7 @@ __device__ long long g_gc_stamps[64];
 // MFMAs and written (LN2 + LeakyReLU applied) into the other buffer after them, so the staging
 // latency hides behind the compute; the tile's LN2 gamma/beta stay in registers for all images.
 template <int SID>
-__global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
+__global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArgs a) {
     constexpr int GC_NW = GC_NWS, GC_NT = GC_NTS, GC_GQ = GC_GQS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
@@ -539,11 +559,14 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int H = GS(H), W = GS(W), HW = H * W;
-    // 2-D tiles: TH rows x TW columns (TW == W for all but the widest images; W % TW == 0)
+    // 2-D tiles: TH rows x TW columns (TW == W for all but the widest images; W % TW == 0); polyphase
+    // tiles (ps > 1): nbk phase grids from ph0, rows [r0, r0 + TH) of each (tpp row slices per grid)
+    const bool poly = GS(ps) > 1;
     const int ty = GS(tiles_x) == 1 ? tile : tile / GS(tiles_x), tx = tile - ty * GS(tiles_x);
-    const int r0 = ty * GS(TH), c0 = tx * GS(TW);
-    const int rows = GS(H) % GS(TH) == 0 ? GS(TH) : min(GS(TH), H - r0);   // constant when tiles are full
-    const int npx = rows * GS(TW), px0 = r0 * W + c0;
+    const int ph0 = poly ? (tile / GS(tpp)) * GS(nbk) : 0;
+    const int r0 = poly ? (tile - (tile / GS(tpp)) * GS(tpp)) * GS(TH) : ty * GS(TH), c0 = poly ? 0 : tx * GS(TW);
+    const int rows = poly || GS(H) % GS(TH) == 0 ? GS(TH) : min(GS(TH), H - r0);
+    const int npx = GS(nbk) * rows * GS(TW), px0 = r0 * W + c0;
     const bool ln = SID >= 0 ? (GS(lnst) & 1) != 0 : a.in_part[net] != nullptr;
     const bool stats = SID >= 0 ? (GS(lnst) & 2) != 0 : a.out_part[net] != nullptr;
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
@@ -566,9 +589,17 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
             if (e < nq) {
                 const int pix = cpq == 1 ? e : (int)__umulhi((unsigned)e, br.cpq_mag), cq = e - pix * cpq;
                 const int brr = (int)__umulhi((unsigned)pix, br.bw_mag), bc = pix - brr * br.BW;
-                const int y = r0 - br.dil + brr, x = c0 + bc - br.dil;
+                int y = r0 - br.dil + brr, x = c0 + bc - br.dil;
+                bool inb = y >= 0 && y < H && x >= 0 && x < W;
+                if (poly) {   // band row brr of block blk -> row of phase grid ph0 + blk
+                    const int bh = GS(TH) + 2, blk = brr / bh, sy = r0 - 1 + brr - blk * bh, sx = bc - 1;
+                    const int ph = ph0 + blk, pa = ph / GS(ps), pb = ph - pa * GS(ps);
+                    inb = sy >= 0 && sy < H / GS(ps) && sx >= 0 && sx < W / GS(ps);
+                    y = pa + sy * GS(ps);
+                    x = pb + sx * GS(ps);
+                }
                 loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
-                if (y >= 0 && y < H && x >= 0 && x < W) {
+                if (inb) {
                     soff[u] = (y * W + x) * br.pcs + br.cin_off + 4 * cq;
                     const int v = min(4, br.cin - 4 * cq);
                     const bool vec = v == 4 && ((br.cin_off | br.pcs) & 3) == 0;
@@ -679,16 +710,16 @@ __global__ __launch_bounds__(GC_NTS, 1) void k_gc(GcArgs a) {
         float* outp = a.out[net] + (size_t)img * HW * GS(out_cs);
         const int boff = (ii & 1) * GS(band_bytes);
         if constexpr (SID >= 0) {
-            gc_branches<SID, 0>(a, smem, outp, npx, px0, st, first, stats, boff);
+            gc_branches<SID, 0>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff);
         } else {
             for (int bi = 0; bi < GS(nbr); bi++) {
                 const GcBranch& br = GS(br)[bi];
                 const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
                 switch ((br.cout + 15) >> 4) {
-                    case 1: gc_branch<1, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                    case 2: gc_branch<2, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                    case 3: gc_branch<3, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
-                    default: gc_branch<4, SID, -1>(a, br, smem, bias, outp, npx, px0, st, first, stats, boff); break;
+                    case 1: gc_branch<1, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
+                    case 2: gc_branch<2, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
+                    case 3: gc_branch<3, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
+                    default: gc_branch<4, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
                 }
                 GSTAMP(gs++);
             }
@@ -711,7 +742,7 @@ template <int S>
 bool launch_gc_shape(int sid, const GcArgs& a, dim3 grid, int lds, hipStream_t st) {
     if constexpr (S < CNF_GC_NSHAPES) {
         if (sid == S) {
-            CNF_LAUNCH((k_gc<S>), grid, dim3(64 * GC_NW_SPEC), lds, st, a);
+            CNF_LAUNCH((k_gc<S>), grid, dim3(64 * kGcShapes[S].nw), lds, st, a);
             return true;
         }
         return launch_gc_shape<S + 1>(sid, a, grid, lds, st);
@@ -733,7 +764,10 @@ static int gc_shape_id(const GcArgs& a) {
     return -1;
 }
 
-int gc_waves(const GcArgs& a) { return gc_shape_id(a) >= 0 ? GC_NW_SPEC : GC_NW_GEN; }
+int gc_waves(const GcArgs& a) {
+    const int sid = gc_shape_id(a);
+    return sid >= 0 ? kGcShapes[sid].nw : GC_NW_GEN;
+}
 
 void launch_gc(const GcArgs& a, int grid_x, int lds, hipStream_t st) {
     const dim3 grid(grid_x, 2);

@@ -4,7 +4,7 @@
 log=$1; to=$2; shift 2
 for i in 1 2 3 4 5 6; do
   /usr/local/graft/bin/gpurun --timeout $to -- "$@" > $log 2>&1
-  if grep -q "status=transient\|backing off\|slot(s) on this pod are busy" $log && ! grep -q "status=ok" $log; then
+  if grep -q "status=transient\|stopped responding\|backing off\|slot(s) on this pod are busy" $log && ! grep -q "status=ok" $log; then
     sleep 60; continue
   fi
   break
