@@ -174,8 +174,10 @@ struct TrainLayout {
     std::vector<size_t> save_u;   // per coupling index: its input u [B][H][W][D]
     size_t bw = 0;
     size_t ys[2] = {}, t1s[2] = {}, t2s[2] = {}, so[2] = {}, dso[2] = {}, stats[2] = {};
-    size_t dy = 0, dln = 0, dbuf = 0, dt1 = 0, dc = 0, dt2 = 0, u1c = 0, du1c = 0, duv[2] = {}, dzy = 0;
-    size_t lnsum = 0, wpart = 0, bpart = 0, dwpart = 0, lnpart = 0;
+    // per-net scratch ([net]): the two nets' backward chains run on two streams
+    size_t dy[2] = {}, dln[2] = {}, dbuf[2] = {}, dt1[2] = {}, dc[2] = {}, dt2[2] = {}, du1c[2] = {};
+    size_t u1c = 0, duv[2] = {}, dzy = 0;
+    size_t lnsum[2] = {}, wpart[2] = {}, bpart[2] = {}, lnpart[2] = {}, dwpart = 0;
 };
 
 struct Plan {
@@ -213,6 +215,10 @@ struct Plan {
     // in-stream launch timing (bench.py): a HIP event pair around every recorded launch
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 2 per recorded launch, grown on demand, owned by the plan
+    // training: net b's recompute / backward chain runs on a second stream (fork / join events)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int side_device = -1;
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;
 };

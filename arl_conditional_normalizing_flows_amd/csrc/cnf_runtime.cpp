@@ -1015,6 +1015,9 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->dev_aux_map) (void)hipFree(plan->p->dev_aux_map);
         if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
         for (hipEvent_t e : plan->p->ev) (void)hipEventDestroy(e);
+        if (plan->p->ev_fork) (void)hipEventDestroy(plan->p->ev_fork);
+        if (plan->p->ev_join) (void)hipEventDestroy(plan->p->ev_join);
+        if (plan->p->side) (void)hipStreamDestroy(plan->p->side);
         delete plan->p;
     }
     delete plan;

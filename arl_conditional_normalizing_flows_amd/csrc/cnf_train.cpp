@@ -87,24 +87,30 @@ TrainLayout Plan::train_layout(int B) const {
         T.dso[n] = take(Bz * m_so * 4);
         T.stats[n] = take(Bz * m_st * 2 * 4);
     }
-    T.dy = take(Bz * m_nk * 4);
-    T.dln = take(Bz * m_nk * 4);
-    T.dbuf = take(Bz * m_nk * 4);
-    T.dt1 = take(Bz * m_nk * 4);
-    T.dc = take(Bz * m_gc * 4);
-    T.dt2 = take(Bz * m_gc * 4);
+    for (int n = 0; n < 2; n++) {
+        T.dy[n] = take(Bz * m_nk * 4);
+        T.dln[n] = take(Bz * m_nk * 4);
+        T.dbuf[n] = take(Bz * m_nk * 4);
+        T.dt1[n] = take(Bz * m_nk * 4);
+        T.dc[n] = take(Bz * m_gc * 4);
+        T.dt2[n] = take(Bz * m_gc * 4);
+        T.du1c[n] = take(Bz * m_u1 * 4);
+    }
     T.u1c = take(Bz * m_u1 * 4);
-    T.du1c = take(Bz * m_u1 * 4);
     for (int k = 0; k < 2; k++) T.duv[k] = take(Bz * L.n_uv * 4);
     T.dzy = take(Bz * L.n_uv * 4);
-    T.lnsum = take(Bz * 2 * 8);
-    // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
-    T.lnpart = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
+    for (int n = 0; n < 2; n++) {
+        T.lnsum[n] = take(Bz * 2 * 8);
+        // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
+        T.lnpart[n] = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
+    }
     int chunks = 1;
     for (const Coupling& c : couplings) chunks = std::max(chunks, wgrad_chunks(B, c.hc * c.wc));
     // the MFMA weight gradient writes up to WGRAD_MAX_CHUNKS rows of [weights | bias]
-    T.wpart = take((size_t)std::max(chunks, WGRAD_MAX_CHUNKS) * (m_dense + m_co) * 4);
-    T.bpart = take((size_t)chunks * m_co * 4);
+    for (int n = 0; n < 2; n++) {
+        T.wpart[n] = take((size_t)std::max(chunks, WGRAD_MAX_CHUNKS) * (m_dense + m_co) * 4);
+        T.bpart[n] = take((size_t)chunks * m_co * 4);
+    }
     T.dwpart = take(Bz * std::max(1, L.ld_parts) * 8);
     T.total = off;
     return T;
@@ -122,6 +128,7 @@ struct TExec {
     int B;
     hipStream_t st;
     float inv_batch_ = 0.f;
+    int net = 0;   // which per-net scratch set (and stream) this executor's launches use
     const float* bw() const { return reinterpret_cast<const float*>(ws + T.bw); }
     template <class X>
     X* at(size_t off) const {
@@ -203,8 +210,8 @@ void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int
     a.dy_cs = dy_cs;
     a.dy_off = dy_off;
     a.CO = cout;
-    a.part = E.at<float>(E.T.wpart);
-    a.bpart = E.at<float>(E.T.bpart);
+    a.part = E.at<float>(E.T.wpart[E.net]);
+    a.bpart = E.at<float>(E.T.bpart[E.net]);
     a.H = h;
     a.W = w;
     a.taps = pc.taps;
@@ -231,16 +238,48 @@ void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int
 
 void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
             int64_t g_off, int64_t b_off) {
-    launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum), n, E.B, 1, dx, accumulate,
+    launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum[E.net]), n, E.B, 1, dx, accumulate,
                        ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr,
-                       E.at<float>(E.T.lnpart), E.st);
+                       E.at<float>(E.T.lnpart[E.net]), E.st);
 }
 
+// the plan's side stream and fork / join events (created on first use on the current device)
+void ensure_side(Plan& p) {
+    int dev = 0;
+    hchk(hipGetDevice(&dev), "hipGetDevice");
+    if (p.side != nullptr && p.side_device == dev) return;
+    if (p.side != nullptr) {
+        (void)hipEventDestroy(p.ev_fork);
+        (void)hipEventDestroy(p.ev_join);
+        (void)hipStreamDestroy(p.side);
+        p.side = nullptr;
+    }
+    hchk(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking), "hipStreamCreate");
+    hchk(hipEventCreateWithFlags(&p.ev_fork, hipEventDisableTiming), "hipEventCreate");
+    hchk(hipEventCreateWithFlags(&p.ev_join, hipEventDisableTiming), "hipEventCreate");
+    p.side_device = dev;
+}
+
+// `to` waits for everything enqueued on `from` so far
+void stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
+    hchk(hipEventRecord(ev, from), "hipEventRecord");
+    hchk(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent");
+}
+
+// One coupling layer's backward (conv_cINN_make_model.py:1850-1880 through the layer): the two s,t
+// nets are independent until the coupling law joins them, so net b's recompute and backward chain run
+// on the plan's side stream (its own scratch set) while net A's run on the caller's stream: the many
+// small, latency-bound launches of the two chains overlap.
 void coupling_backward(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
     const int B = E.B, h = c.hc, w = c.wc, nk = c.nk, gc = c.gc, R = c.R;
     const int64_t npx = (int64_t)h * w;
     const bool ln = E.p.desc.layer_norm != 0;
     const float* P = E.params;
+    ensure_side(E.p);
+    TExec E1 = E;
+    E1.net = 1;
+    E1.st = E.p.side;
+    TExec* X[2] = {&E, &E1};
     float* u1c = E.at<float>(E.T.u1c);
     launch_gather_u1c(u, u1c, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
     // activations of both nets: y_r (r = 0..R), t1_r, t2_r; LN stats st[0..R] (y), st[R+1+r] (t1),
@@ -260,27 +299,30 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         return l;
     };
     const LnIn raw{};
+    stream_wait(E.st, E1.st, E.p.ev_fork);   // u1c gathered
     for (int n = 0; n < 2; n++) {
+        TExec& En = *X[n];
         const NetParams& np = c.net[n];
-        conv_fwd(E, h, w, u1c, c.dc1, 0, c.dc1, raw, np.ci, nk, 1, nullptr, Y(n, 0), nk, 0);
-        if (ln) launch_ln_stats(Y(n, 0), npx * nk, B, 1, ST(n, 0), E.st);
+        conv_fwd(En, h, w, u1c, c.dc1, 0, c.dc1, raw, np.ci, nk, 1, nullptr, Y(n, 0), nk, 0);
+        if (ln) launch_ln_stats(Y(n, 0), npx * nk, B, 1, ST(n, 0), En.st);
         for (int r = 0; r < R; r++) {
             const RBParams& rb = np.rb[r];
-            conv_fwd(E, h, w, Y(n, r), nk, 0, nk, lnin(n, r, rb.ln1g, rb.ln1b), rb.ca, nk, 1, nullptr, T1(n, r), nk, 0);
-            if (ln) launch_ln_stats(T1(n, r), npx * nk, B, 1, ST(n, R + 1 + r), E.st);
+            conv_fwd(En, h, w, Y(n, r), nk, 0, nk, lnin(n, r, rb.ln1g, rb.ln1b), rb.ca, nk, 1, nullptr, T1(n, r), nk, 0);
+            if (ln) launch_ln_stats(T1(n, r), npx * nk, B, 1, ST(n, R + 1 + r), En.st);
             for (size_t bi = 0; bi < c.br.size(); bi++) {
                 const Branch& b = c.br[bi];
-                conv_fwd(E, h, w, T1(n, r), nk, b.cin_off, b.cin, lnin(n, R + 1 + r, rb.ln2g, rb.ln2b), rb.gc[bi],
+                conv_fwd(En, h, w, T1(n, r), nk, b.cin_off, b.cin, lnin(n, R + 1 + r, rb.ln2g, rb.ln2b), rb.gc[bi],
                          b.cout, b.dil, nullptr, T2(n, r), gc, b.out_off);
             }
-            if (ln) launch_ln_stats(T2(n, r), npx * gc, B, 1, ST(n, 2 * R + 1 + r), E.st);
-            conv_fwd(E, h, w, T2(n, r), gc, 0, gc, lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b), rb.cb, nk, 1, Y(n, r),
+            if (ln) launch_ln_stats(T2(n, r), npx * gc, B, 1, ST(n, 2 * R + 1 + r), En.st);
+            conv_fwd(En, h, w, T2(n, r), gc, 0, gc, lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b), rb.cb, nk, 1, Y(n, r),
                      Y(n, r + 1), nk, 0);
-            if (ln) launch_ln_stats(Y(n, r + 1), npx * nk, B, 1, ST(n, r + 1), E.st);
+            if (ln) launch_ln_stats(Y(n, r + 1), npx * nk, B, 1, ST(n, r + 1), En.st);
         }
-        conv_fwd(E, h, w, Y(n, R), nk, 0, nk, lnin(n, R, np.ln_out_g, np.ln_out_b), np.co, c.dc2, 1, nullptr,
+        conv_fwd(En, h, w, Y(n, R), nk, 0, nk, lnin(n, R, np.ln_out_g, np.ln_out_b), np.co, c.dc2, 1, nullptr,
                  E.at<float>(E.T.so[n]), c.dc2, 0);
     }
+    stream_wait(E1.st, E.st, E.p.ev_join);   // both nets' outputs
     // coupling law backward -> du (u2 part, u1 copy), dL/d s_pre, dL/dt, dL/dw
     {
         CoupBwArgs a{};
@@ -306,46 +348,51 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         launch_coupling_backward(a, B, np, E.st);
         launch_dsum(a.dw_part, (long long)B * np, E.dparams + c.net[0].tanh_w, E.st);
     }
-    float* dy = E.at<float>(E.T.dy);
-    float* dln = E.at<float>(E.T.dln);
-    float* dbuf = E.at<float>(E.T.dbuf);
-    float* dt1 = E.at<float>(E.T.dt1);
-    float* dcb = E.at<float>(E.T.dc);
-    float* dt2 = E.at<float>(E.T.dt2);
-    float* du1c = E.at<float>(E.T.du1c);
+    stream_wait(E.st, E1.st, E.p.ev_fork);   // dL/d s_pre, dL/dt
     for (int n = 0; n < 2; n++) {
+        TExec& En = *X[n];
+        float* dy = E.at<float>(E.T.dy[n]);
+        float* dln = E.at<float>(E.T.dln[n]);
+        float* dbuf = E.at<float>(E.T.dbuf[n]);
+        float* dt1 = E.at<float>(E.T.dt1[n]);
+        float* dcb = E.at<float>(E.T.dc[n]);
+        float* dt2 = E.at<float>(E.T.dt2[n]);
+        float* du1c = E.at<float>(E.T.du1c[n]);
         const NetParams& np = c.net[n];
         const float* dso = E.at<float>(E.T.dso[n]);
         const LnIn lo = lnin(n, R, np.ln_out_g, np.ln_out_b);
-        conv_wgrad(E, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
-        conv_dgrad(E, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
-        ln_bwd(E, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+        conv_wgrad(En, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
+        conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
+        ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
         for (int r = R - 1; r >= 0; r--) {
             const RBParams& rb = np.rb[r];
             // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
             const LnIn l3 = lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b);
-            conv_wgrad(E, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
-            conv_dgrad(E, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
-            ln_bwd(E, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
+            conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
+            conv_dgrad(En, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
+            ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
             // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
-            hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, E.st), "hipMemsetAsync");
+            hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
             for (size_t bi = 0; bi < c.br.size(); bi++) {
                 const Branch& b = c.br[bi];
-                conv_wgrad(E, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.dil);
-                conv_dgrad(E, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
+                conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.dil);
+                conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
             }
-            ln_bwd(E, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
+            ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
             // conv_a
             const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
-            conv_wgrad(E, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
-            conv_dgrad(E, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
-            ln_bwd(E, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
+            conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
+            conv_dgrad(En, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
+            ln_bwd(En, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
         }
-        conv_wgrad(E, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
-        conv_dgrad(E, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, n > 0 ? 1 : 0);
+        conv_wgrad(En, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
+        conv_dgrad(En, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, 0);
     }
-    launch_scatter_add_u1c(du1c, du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
+    stream_wait(E1.st, E.st, E.p.ev_join);   // net b's chain done
+    // du += the two nets' u1 gradients, net A's first (fixed order: bitwise reproducible)
+    launch_scatter_add_u1c(E.at<float>(E.T.du1c[0]), du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
+    launch_scatter_add_u1c(E.at<float>(E.T.du1c[1]), du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
 }
 
 }  // namespace
