@@ -219,6 +219,11 @@ struct Plan {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_device = -1;
+    // ... and each net's weight gradients on a stream of their own (wside[net]), ordered against the
+    // chain by events from tev (reused once a coupling's streams have joined)
+    hipStream_t wside[2] = {nullptr, nullptr};
+    std::vector<hipEvent_t> tev;
+    size_t tev_next = 0;
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;
 };

@@ -1018,6 +1018,9 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->ev_fork) (void)hipEventDestroy(plan->p->ev_fork);
         if (plan->p->ev_join) (void)hipEventDestroy(plan->p->ev_join);
         if (plan->p->side) (void)hipStreamDestroy(plan->p->side);
+        for (hipStream_t s : plan->p->wside)
+            if (s) (void)hipStreamDestroy(s);
+        for (hipEvent_t e : plan->p->tev) (void)hipEventDestroy(e);
         delete plan->p;
     }
     delete plan;

@@ -129,6 +129,7 @@ struct TExec {
     hipStream_t st;
     float inv_batch_ = 0.f;
     int net = 0;   // which per-net scratch set (and stream) this executor's launches use
+    hipStream_t wst = nullptr;   // weight-gradient stream (null: on st)
     const float* bw() const { return reinterpret_cast<const float*>(ws + T.bw); }
     template <class X>
     X* at(size_t off) const {
@@ -195,8 +196,42 @@ void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, 
 }
 
 // dW, db of a conv: X (cin channels at x_cs/x_off, LN-on-load) and dY (cout at dy_cs/dy_off)
-void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int cin, const LnIn& ln, const float* dy,
-                int dy_cs, int dy_off, int cout, const PackedConv& pc, int dil) {
+hipEvent_t tevent(Plan& p) {
+    if (p.tev_next == p.tev.size()) {
+        hipEvent_t e;
+        hchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        p.tev.push_back(e);
+    }
+    return p.tev[p.tev_next++];
+}
+
+// dW, db of a conv (below) on E's weight-gradient stream when it has one: it waits for the chain's
+// launches so far (its X and dY are ready) and returns the event of its completion, which the chain
+// waits for before it overwrites that dY buffer
+hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int cin, const LnIn& ln,
+                           const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int dil);
+hipEvent_t conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int cin, const LnIn& ln,
+                      const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int dil) {
+    if (E.wst == nullptr) {
+        conv_wgrad_impl(E, h, w, x, x_cs, x_off, cin, ln, dy, dy_cs, dy_off, cout, pc, dil);
+        return nullptr;
+    }
+    hipEvent_t in = tevent(E.p), done = tevent(E.p);
+    hchk(hipEventRecord(in, E.st), "hipEventRecord");
+    hchk(hipStreamWaitEvent(E.wst, in, 0), "hipStreamWaitEvent");
+    TExec G = E;
+    G.st = E.wst;
+    conv_wgrad_impl(G, h, w, x, x_cs, x_off, cin, ln, dy, dy_cs, dy_off, cout, pc, dil);
+    hchk(hipEventRecord(done, E.wst), "hipEventRecord");
+    return done;
+}
+
+void chain_wait(TExec& E, hipEvent_t done) {
+    if (done != nullptr) hchk(hipStreamWaitEvent(E.st, done, 0), "hipStreamWaitEvent");
+}
+
+hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int cin, const LnIn& ln,
+                           const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int dil) {
     WGradArgs a{};
     a.x = x;
     a.x_cs = x_cs;
@@ -226,7 +261,7 @@ void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int
         launch_wgrad(a, E.st);
         launch_grad_scatter(a.part, a.chunks, nw, map + pc.dw, E.dparams, E.st);
         launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
-        return;
+        return nullptr;
     }
     // k_wgrad_band: rows of [weights | bias]; the dense image keeps the bias right after the
     // weights (pc.db == pc.dw + taps * cin * cout), so one scatter reduces both
@@ -234,6 +269,7 @@ void conv_wgrad(TExec& E, int h, int w, const float* x, int x_cs, int x_off, int
     launch_wgrad(a, E.st);
     if (pc.db != pc.dw + nw) throw std::logic_error("dense image: bias not after the weights");
     launch_grad_scatter(a.part, a.chunks, nw + cout, map + pc.dw, E.dparams, E.st);
+    return nullptr;
 }
 
 void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
@@ -252,11 +288,13 @@ void ensure_side(Plan& p) {
         (void)hipEventDestroy(p.ev_fork);
         (void)hipEventDestroy(p.ev_join);
         (void)hipStreamDestroy(p.side);
+        for (hipStream_t& s : p.wside) (void)hipStreamDestroy(s);
         p.side = nullptr;
     }
     hchk(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking), "hipStreamCreate");
     hchk(hipEventCreateWithFlags(&p.ev_fork, hipEventDisableTiming), "hipEventCreate");
     hchk(hipEventCreateWithFlags(&p.ev_join, hipEventDisableTiming), "hipEventCreate");
+    for (hipStream_t& s : p.wside) hchk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
     p.side_device = dev;
 }
 
@@ -276,10 +314,18 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     const bool ln = E.p.desc.layer_norm != 0;
     const float* P = E.params;
     ensure_side(E.p);
+    E.p.tev_next = 0;   // every event of the previous coupling has been waited for (the join below)
+    static const bool wstreams = [] {   // A/B knob: weight gradients on the chain streams
+        const char* e = std::getenv("CNF_TRAIN_WSTREAM");
+        return !(e && std::atoi(e) == 0);
+    }();
+    TExec E0 = E;
+    E0.wst = wstreams ? E.p.wside[0] : nullptr;
     TExec E1 = E;
     E1.net = 1;
     E1.st = E.p.side;
-    TExec* X[2] = {&E, &E1};
+    E1.wst = wstreams ? E.p.wside[1] : nullptr;
+    TExec* X[2] = {&E0, &E1};
     float* u1c = E.at<float>(E.T.u1c);
     launch_gather_u1c(u, u1c, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
     // activations of both nets: y_r (r = 0..R), t1_r, t2_r; LN stats st[0..R] (y), st[R+1+r] (t1),
@@ -364,32 +410,41 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         conv_wgrad(En, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
         conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
         ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+        // the weight gradients run behind the chain on En.wst; before the chain overwrites a dY buffer
+        // it waits for the weight gradients reading it (of the block before: dt2, dt1; this block: dy)
+        hipEvent_t ev_gc = nullptr, ev_ca = nullptr;
         for (int r = R - 1; r >= 0; r--) {
             const RBParams& rb = np.rb[r];
             // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
             const LnIn l3 = lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b);
-            conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
+            const hipEvent_t ev_cb = conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
             conv_dgrad(En, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
+            chain_wait(En, ev_gc);
             ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
             // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
             hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
             for (size_t bi = 0; bi < c.br.size(); bi++) {
                 const Branch& b = c.br[bi];
-                conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.dil);
+                ev_gc = conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi],
+                                   b.dil);
                 conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
             }
+            chain_wait(En, ev_ca);
             ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
             // conv_a
             const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
-            conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
+            ev_ca = conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
             conv_dgrad(En, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
+            chain_wait(En, ev_cb);
             ln_bwd(En, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
         }
         conv_wgrad(En, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
         conv_dgrad(En, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, 0);
     }
     stream_wait(E1.st, E.st, E.p.ev_join);   // net b's chain done
+    for (int n = 0; n < 2; n++)                  // and both nets' weight gradients
+        if (X[n]->wst) stream_wait(X[n]->wst, E.st, tevent(E.p));
     // du += the two nets' u1 gradients, net A's first (fixed order: bitwise reproducible)
     launch_scatter_add_u1c(E.at<float>(E.T.du1c[0]), du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
     launch_scatter_add_u1c(E.at<float>(E.T.du1c[1]), du, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
