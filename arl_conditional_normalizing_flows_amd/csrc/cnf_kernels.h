@@ -68,36 +68,6 @@ struct ConvProb {
     const int* st_map;                     // [64][2]: channel -> (offset of pixel 0 inside the image, pixel stride) in floats, offset < 0: not stored
 };
 
-// Compact channel layout of a tensor of which only the channels in mask m are ever read (t1 of the
-// streamed layers: the grouped branches read only their input windows, in the reference's group
-// mode the last _d-channel slice of each, conv_cINN_base_functions.py:397-402): every maximal run
-// of set bits, in channel order, starts at the next 16-byte (quad) boundary. compact_ch(m, c) is
-// channel c's index in that layout (-1 if c is not in m), compact_width(m) the padded width.
-__host__ __device__ inline int compact_ch(uint64_t m, int c) {
-    if (c < 0 || c >= 64 || ((m >> c) & 1ull) == 0) return -1;
-    int off = 0;
-    while (m != 0) {
-        const int s = __builtin_ctzll(m);
-        const uint64_t t = m >> s;
-        const int len = ~t == 0 ? 64 - s : __builtin_ctzll(~t);
-        if (c < s + len) return off + (c - s);
-        off += (len + 3) & ~3;
-        m &= len + s >= 64 ? 0ull : ~0ull << (s + len);
-    }
-    return -1;
-}
-__host__ __device__ inline int compact_width(uint64_t m) {
-    int off = 0;
-    while (m != 0) {
-        const int s = __builtin_ctzll(m);
-        const uint64_t t = m >> s;
-        const int len = ~t == 0 ? 64 - s : __builtin_ctzll(~t);
-        off += (len + 3) & ~3;
-        m &= len + s >= 64 ? 0ull : ~0ull << (s + len);
-    }
-    return off;
-}
-
 struct ConvArgs {
     ConvProb p[MAXPROB];
     int H, W, TH, tiles_per_img, nprob, B;

@@ -517,7 +517,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 // (H, W divisible by the dilation): bands of (TH+2) x (TW+2) per grid instead of
                 // (TH + 2d) x (TW + 2d) (cfg5's dilation-16 branch: 400 staged pixels per 256 outputs
                 // instead of 1920 per 128); CNF_GC_POLY=0 is the A/B knob
-                static const bool poly = [] {
+                const bool poly = [] {   // read per plan: tests compare both tilings in one process
                     const char* e = std::getenv("CNF_GC_POLY");
                     return !(e && std::atoi(e) == 0);
                 }();
@@ -544,7 +544,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     // four 4-wave workgroups per CU when the band is small (these branches have little
                     // MFMA work per image: their time is per-image latency, which co-resident
                     // workgroups hide; tiles down to 128 pixels for it), else one 16-wave workgroup
-                    static const int poly_nw = [] {
+                    const int poly_nw = [] {
                         const char* e = std::getenv("CNF_GC_POLY_NW");   // A/B knob
                         return e ? std::atoi(e) : 4;
                     }();
@@ -611,17 +611,31 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     units.push_back({(int)bi});
                 }
                 if (!ok) continue;
-                std::vector<uint64_t> um;
+                // every window of a unit at the next 16-byte boundary (in channel order), so each
+                // branch's quads stay aligned; windows of one unit must not overlap (one channel, one
+                // place), nor may two units share a channel
+                std::vector<std::vector<std::pair<int, int>>> uw;   // per unit: (cin_off, branch) sorted
+                std::vector<int> ucs;
                 uint64_t seen = 0;
                 int total = 0;
                 for (const auto& u : units) {
+                    std::vector<std::pair<int, int>> ws;
+                    for (int bi : u) ws.push_back({c.br[bi].cin_off, bi});
+                    std::sort(ws.begin(), ws.end());
                     uint64_t m = 0;
-                    for (int bi : u)
-                        for (int ch = c.br[bi].cin_off; ch < c.br[bi].cin_off + c.br[bi].cin; ch++) m |= 1ull << ch;
-                    ok = ok && (m & seen) == 0;   // a channel stored twice: plain layout
+                    int cs = 0;
+                    for (const auto& wv : ws) {
+                        const Branch& b = c.br[wv.second];
+                        for (int ch = b.cin_off; ch < b.cin_off + b.cin; ch++) {
+                            ok = ok && ((m | seen) >> ch & 1ull) == 0;
+                            m |= 1ull << ch;
+                        }
+                        cs += (b.cin + 3) / 4 * 4;
+                    }
                     seen |= m;
-                    um.push_back(m);
-                    total += compact_width(m);
+                    uw.push_back(ws);
+                    ucs.push_back(cs);
+                    total += cs;
                 }
                 if (!ok || (units.size() == 1 && total >= c.nk)) continue;
                 const int hw = c.hc * c.wc;
@@ -630,15 +644,17 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.t1_map.assign(128, -1);
                 int base = 0;   // floats from the image start to the sub-tensor
                 for (size_t u = 0; u < units.size(); u++) {
-                    const int cs = compact_width(um[u]);
-                    for (int ch = 0; ch < 64; ch++)
-                        if ((um[u] >> ch) & 1ull) {
-                            c.t1_map[2 * ch] = base + compact_ch(um[u], ch);
+                    const int cs = ucs[u];
+                    int wo = 0;
+                    for (const auto& wv : uw[u]) {
+                        const Branch& b = c.br[wv.second];
+                        for (int ch = b.cin_off; ch < b.cin_off + b.cin; ch++) {
+                            c.t1_map[2 * ch] = base + wo + (ch - b.cin_off);
                             c.t1_map[2 * ch + 1] = cs;
                         }
-                    for (int bi : units[u]) {
-                        c.t1_off[bi] = c.t1_map[2 * c.br[bi].cin_off];
-                        c.t1_pcs[bi] = cs;
+                        c.t1_off[wv.second] = base + wo;
+                        c.t1_pcs[wv.second] = cs;
+                        wo += (b.cin + 3) / 4 * 4;
                     }
                     base += hw * cs;
                 }

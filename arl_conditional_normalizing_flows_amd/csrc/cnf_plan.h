@@ -102,7 +102,7 @@ struct Coupling {
     // streamed layers: t1 (conv_a's output) holds only the channels the grouped branches read, one
     // dense sub-tensor per consumer (a k_gc group, or a branch launched on its own) inside each
     // image: sub-tensor u = [HW][cs_u] at float offset HW * (cs_0 + ... + cs_{u-1}), its windows
-    // packed by compact_ch (quad-aligned runs). t1_cs = floats per pixel of an image (nk when plain),
+    // packed in channel order, each from a 16-byte boundary. t1_cs = floats per pixel of an image (nk when plain),
     // t1_off[bi] / t1_pcs[bi] = branch bi's window: offset of pixel 0 inside the image, pixel
     // stride; t1_map[2c], [2c+1] = the same for channel c (-1: not stored)
     uint64_t t1_used = 0;

@@ -1581,6 +1581,26 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
 }
 int cnf_debug_gc_words() { return GCSHAPE_WORDS; }
 
+// t1 layout of a coupling (Coupling::t1_map): [compact, floats per pixel of the image, then per branch
+// (window offset of pixel 0, pixel stride, cin_off, cin), then 128 words of t1_map (compact only)]
+int cnf_debug_t1_layout(const cnf_plan* plan, int coupling, int* words, int cap) {
+    if (!plan || !words) return -1;
+    const Plan& p = *plan->p;
+    if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
+    const Coupling& c = p.couplings[coupling];
+    std::vector<int> w = {c.t1_compact ? 1 : 0, c.t1_cs};
+    for (size_t bi = 0; bi < c.br.size(); bi++) {
+        w.push_back(bi < c.t1_off.size() ? c.t1_off[bi] : -1);
+        w.push_back(bi < c.t1_pcs.size() ? c.t1_pcs[bi] : -1);
+        w.push_back(c.br[bi].cin_off);
+        w.push_back(c.br[bi].cin);
+    }
+    w.insert(w.end(), c.t1_map.begin(), c.t1_map.end());
+    if ((int)w.size() > cap) return -1;
+    std::memcpy(words, w.data(), w.size() * sizeof(int));
+    return (int)w.size();
+}
+
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }
 int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }

@@ -341,7 +341,7 @@ int pw_num_shapes() { return CNF_PW_NSHAPES; }
 
 void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
-    static const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob
+    const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob (read per launch: tests switch it)
     PwShape sh;
     if (!generic && pw_shape_of(nr, gm, ln, res, tap, a, sh))
         for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
@@ -754,10 +754,8 @@ int gc_num_shapes() { return CNF_GC_NSHAPES; }
 
 // table entry matching a's shape, -1 for the generic instantiation
 static int gc_shape_id(const GcArgs& a) {
-    static const bool generic = [] {   // A/B knob: never the shape-specialised instantiations
-        const char* e = std::getenv("CNF_GC_GENERIC");
-        return e && std::atoi(e) != 0;
-    }();
+    const char* e = std::getenv("CNF_GC_GENERIC");   // A/B knob (read per launch: tests switch it)
+    const bool generic = e && std::atoi(e) != 0;
     if (!generic)
         for (int sid = 0; sid < CNF_GC_NSHAPES; sid++)
             if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0) return sid;

@@ -252,3 +252,48 @@ def test_forward_rejects_aliased_xy_zy(lib):
         assert lib.cnf_flow_forward_train(p, a, a, b, b, a, a, 2, None) == -1
     finally:
         lib.cnf_plan_destroy(p)
+
+
+@pytest.mark.parametrize('name', ['cfg2', 'cfg3', 'ref_default', 'cfg4', 'cfg5', 'small'])
+def test_t1_layout_is_dense_per_consumer(lib, name):
+    """Streamed layers store t1 as one sub-tensor per consumer (cnf_plan.cpp, Coupling::t1_map): every
+    branch window starts 16-byte aligned with its sub-tensor's pixel stride, the per-channel store map
+    agrees with the branch windows, exactly the channels the branches read are stored, and every
+    (pixel, channel) of the image has its own float inside the image's t1_cs floats per pixel."""
+    kw = PRESETS[name].kwargs()
+    kw.pop('group_mode')
+    rc, p, keep = _plan(lib, kw)
+    assert rc == 0
+    lib.cnf_debug_t1_layout.restype = C.c_int
+    lib.cnf_debug_t1_layout.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
+    o = OracleCFlow(**kw)
+    compact_seen = 0
+    try:
+        for c in o.coupling_specs:
+            buf = (C.c_int * 512)()
+            n = lib.cnf_debug_t1_layout(p, c.index, buf, 512)
+            assert n >= 2
+            w = list(buf[:n])
+            compact, cs = w[0], w[1]
+            nb = len(c.branches)
+            br = [w[2 + 4 * i: 6 + 4 * i] for i in range(nb)]
+            if not compact:
+                assert cs == c.nk and all(b[0] == b[2] and b[1] == c.nk for b in br)
+                continue
+            compact_seen += 1
+            tmap = np.array(w[2 + 4 * nb:2 + 4 * nb + 128]).reshape(64, 2)
+            used = set()
+            for off, pcs, cin_off, cin in br:
+                assert off % 4 == 0 and pcs % 4 == 0 and 0 < cin <= pcs
+                for ch in range(cin_off, cin_off + cin):
+                    assert tuple(tmap[ch]) == (off + ch - cin_off, pcs)
+                    used.add(ch)
+            assert set(np.nonzero(tmap[:, 0] >= 0)[0].tolist()) == used
+            hw = c.hc * c.wc
+            idx = np.concatenate([tmap[ch, 0] + np.arange(hw) * tmap[ch, 1] for ch in sorted(used)])
+            assert idx.min() >= 0 and idx.max() < hw * cs
+            assert np.unique(idx).size == idx.size
+    finally:
+        lib.cnf_plan_destroy(p)
+    if name in ('cfg2', 'cfg5'):
+        assert compact_seen > 0

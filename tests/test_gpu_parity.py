@@ -170,6 +170,46 @@ def test_layerwise_equals_fused(gpu, name, B):
     assert torch.equal(xi1, xi2)
 
 
+@pytest.mark.parametrize('name,B', [('cfg2', 3), ('cfg4', 2), ('cfg5', 1)])
+def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
+    """The streamed layers' t1 sub-tensor layout (CNF_T1_COMPACT) changes where t1's values live, never
+    the arithmetic: with the generic k_gc / k_pw in both runs (the plain layout has no specialised
+    instantiation, and those partition the LN statistics over their own wave counts) zy, the per-image
+    log-det and the inverse are equal bit for bit. The polyphase tiles of large dilations (CNF_GC_POLY,
+    cfg4/cfg5) compute every conv output in the same order but gather the LN3 statistics over other
+    pixel sets: equal to rounding."""
+    import os
+    flow, ora, P, xy = _setup(name, B)
+    x = torch.from_numpy(xy).to(gpu)
+    for knob in ('CNF_T1_COMPACT', 'CNF_GC_POLY'):
+        os.environ[knob] = '0'
+        try:
+            f2, _, _, _ = _setup(name, B)
+        finally:
+            os.environ.pop(knob, None)
+        os.environ['CNF_GC_GENERIC'] = '1'
+        os.environ['CNF_PW_GENERIC'] = '1'
+        try:
+            zy0, ld0 = flow(x, 1, per_image_logdet=True)
+            xi0 = flow(zy0, -1)
+            zy, ld = f2(x, 1, per_image_logdet=True)
+            xi = f2(zy0, -1)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop('CNF_GC_GENERIC', None)
+            os.environ.pop('CNF_PW_GENERIC', None)
+        if knob == 'CNF_T1_COMPACT':
+            assert torch.equal(zy, zy0) and torch.equal(ld, ld0) and torch.equal(xi, xi0), knob
+        else:
+            # two fp32 summation orders of every LN3 statistic: a few ulp per layer, well inside the
+            # 1e-5 both meet against the float64 oracle (test_full_size_forward_inverse_match_oracle)
+            e = (zy - zy0).abs().max().item() / zy0.abs().max().item()
+            ei = (xi - xi0).abs().max().item() / xi0.abs().max().item()
+            print(f'{name} polyphase vs plain tiles: zy rel diff {e:.2e}, inverse {ei:.2e}')
+            assert e < 4e-6 and ei < 4e-6
+            assert torch.allclose(ld, ld0, rtol=1e-6, atol=1e-5)
+
+
 def test_roundtrip_cfg2_full_batch(gpu):
     """BASELINE configs[1] at its full batch (64): size-independent round-trip property."""
     flow, ora, P, xy = _setup('cfg2', 64)
