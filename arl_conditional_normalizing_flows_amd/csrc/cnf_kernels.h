@@ -366,6 +366,9 @@ void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, 
 // dgamma/dbeta (+=) per element; stats == null: LeakyReLU backward only
 // (the batch runs in LNB_SLICES slices: scratch holds their [2][LNB_SLICES][n] gamma / beta partials)
 constexpr int LNB_SLICES = 8;
+// k_lnb_reduce splits each image over up to LNB_RS workgroups (partial sums [B][rs][2], summed in slice
+// order where they are read)
+constexpr int LNB_RS = 8;
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
                         float* scratch, hipStream_t st);

@@ -100,7 +100,7 @@ TrainLayout Plan::train_layout(int B) const {
     for (int k = 0; k < 2; k++) T.duv[k] = take(Bz * L.n_uv * 4);
     T.dzy = take(Bz * L.n_uv * 4);
     for (int n = 0; n < 2; n++) {
-        T.lnsum[n] = take(Bz * 2 * 8);
+        T.lnsum[n] = take(Bz * LNB_RS * 2 * 8);
         // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
         T.lnpart[n] = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
     }

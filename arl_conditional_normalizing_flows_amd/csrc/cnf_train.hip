@@ -1030,22 +1030,22 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
                                                     const float* __restrict__ gamma, const float* __restrict__ stats,
                                                     long long n, double* __restrict__ sums) {
     __shared__ double red[LNT / 64];
-    const int b = blockIdx.x;
+    const int b = blockIdx.x, sl = blockIdx.y, RS = gridDim.y;   // slice sl of image b's elements
     const float* xb = x + (size_t)b * n;
     const float* db = dxo + (size_t)b * n;
     const float mu = stats[2 * b], rs = stats[2 * b + 1];
     double sg = 0.0, sgh = 0.0;
     if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(gamma) & 15) == 0) {
-        const long long n4 = n >> 2;
+        const long long n4 = n >> 2, q = (n4 + RS - 1) / RS, lo = sl * q, hi = min(n4, lo + q);
         const f4* x4 = reinterpret_cast<const f4*>(xb);
         const f4* d4 = reinterpret_cast<const f4*>(db);
         const f4* g4 = reinterpret_cast<const f4*>(gamma);
-        for (long long i0 = threadIdx.x; i0 < n4; i0 += 2LL * LNT) {
+        for (long long i0 = lo + threadIdx.x; i0 < hi; i0 += 2LL * LNT) {
             f4 xv[2], dv[2], gv[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 const long long i = i0 + u * LNT;
-                const bool ok = i < n4;
+                const bool ok = i < hi;
                 xv[u] = ok ? x4[i] : f4{0.f, 0.f, 0.f, 0.f};
                 dv[u] = ok ? d4[i] : f4{0.f, 0.f, 0.f, 0.f};
                 gv[u] = ok ? g4[i] : f4{0.f, 0.f, 0.f, 0.f};
@@ -1061,7 +1061,8 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
                 }
         }
     } else {
-        for (long long e = threadIdx.x; e < n; e += LNT) {
+        const long long q = (n + RS - 1) / RS, lo = sl * q, hi = min(n, lo + q);
+        for (long long e = lo + threadIdx.x; e < hi; e += LNT) {
             const float xh = (lrelu(xb[e]) - mu) * rs;
             const float g = db[e] * gamma[e];
             sg += g;
@@ -1071,8 +1072,8 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
     sg = block_sum_ln(sg, red);
     sgh = block_sum_ln(sgh, red);
     if (threadIdx.x == 0) {
-        sums[2 * b] = sg;
-        sums[2 * b + 1] = sgh;
+        sums[2 * ((size_t)b * RS + sl)] = sg;
+        sums[2 * ((size_t)b * RS + sl) + 1] = sgh;
     }
 }
 
@@ -1081,7 +1082,7 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
 // registers; k_lnb_gsum adds the slices in a fixed order (no atomics: deterministic)
 __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, const float* __restrict__ dxo,
                                                    const float* __restrict__ gamma, const float* __restrict__ stats,
-                                                   const double* __restrict__ sums, long long n, int B, int act,
+                                                   const double* __restrict__ sums, int rsl, long long n, int B, int act,
                                                    float* __restrict__ dx, int accumulate, float* __restrict__ gpart,
                                                    float* __restrict__ bpart) {
     const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -1119,8 +1120,13 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
             if (stats) {
                 mu = stats[2 * b];
                 rs = stats[2 * b + 1];
-                mg = (float)(sums[2 * b] * inv_n);
-                mgh = (float)(sums[2 * b + 1] * inv_n);
+                double s0 = 0.0, s1 = 0.0;   // the image's slice partials, in slice order
+                for (int k = 0; k < rsl; k++) {
+                    s0 += sums[2 * ((size_t)b * rsl + k)];
+                    s1 += sums[2 * ((size_t)b * rsl + k) + 1];
+                }
+                mg = (float)(s0 * inv_n);
+                mgh = (float)(s1 * inv_n);
             }
             f4 g4;
 #pragma unroll
@@ -1169,12 +1175,18 @@ __global__ __launch_bounds__(256) void k_lnb_gsum(const float* __restrict__ gpar
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
                         float* scratch, hipStream_t st) {
-    if (stats) hipLaunchKernelGGL(k_lnb_reduce, dim3(B), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
+    // slices per image: at least two full passes of the workgroup each (64 images x 8 slices fill the
+    // GPU where one workgroup per image used a quarter of it)
+#ifndef CNF_LNB_RS
+#define CNF_LNB_RS LNB_RS
+#endif
+    const int rsl = (int)std::min<long long>(CNF_LNB_RS, std::max<long long>(1, (n / 4) / (2LL * LNT)));
+    if (stats) hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
     const int S = B < LNB_SLICES ? B : LNB_SLICES;
     float* gpart = scratch;
     float* bpart = scratch + (size_t)LNB_SLICES * n;
     hipLaunchKernelGGL(k_lnb_apply, dim3((unsigned)((n + 1023) / 1024), S), dim3(256), 0, st, x, dxo, gamma, stats,
-                       sums, n, B, act, dx, accumulate, gpart, bpart);
+                       sums, rsl, n, B, act, dx, accumulate, gpart, bpart);
     if (stats)
         hipLaunchKernelGGL(k_lnb_gsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gpart, bpart, S, n, dgamma,
                            dbeta);
