@@ -66,6 +66,8 @@ struct ConvProb {
     uint32_t st_mask_lo, st_mask_hi;       // output channels actually stored (bit per channel < 64)
     int st_compact;                        // 1: stores through st_map (k_pw only)
     const int* st_map;                     // [64][2]: channel -> (offset of pixel 0 inside the image, pixel stride) in floats, offset < 0: not stored
+    int in_mapped;                         // 1: A-operand quads through in_map (k_pw only; in_cs = floats per pixel of an image)
+    const int* in_map;                     // [quad][2]: input channel quad -> (offset of pixel 0 inside the image, pixel stride)
 };
 
 struct ConvArgs {
@@ -184,6 +186,7 @@ struct GcBranch {
     int band_off, BW, BH, S;                      // LDS band: byte offset, width, height, pixel stride
     int w_off, q_off, b_off;                      // LDS byte offsets: packed weights, quad offsets, bias
     int pcs;                                      // pixel stride of the input window (floats)
+    int opcs;                                     // pixel stride of the output slice (out_off: floats from the image start to pixel 0's slice)
     uint32_t cpq_mag, bw_mag;                     // x / (cinp/4) == umulhi(x, cpq_mag) (cinp > 4), x / BW likewise
 };
 struct GcShape {
@@ -200,6 +203,7 @@ struct GcShape {
     int ps, nbk, tpp;
     int nw;                      // waves per workgroup of the shape-specialised instantiation (16, or 4 for
                                  // small bands: four workgroups per CU hide each other's per-image latency)
+    int pd;                      // images whose band quads are in flight (registers) ahead of the one computed
 };
 constexpr int GCSHAPE_WORDS = (int)(sizeof(GcShape) / 4);
 struct GcArgs {
@@ -248,7 +252,7 @@ struct PwShape {
     int in_cs, in_off, cin, out_cs, out_off, cout, lds_w_off, part_stride;
     int umask, uW, uD, udc, uimg, udil, uoff;   // tap mode (0 otherwise)
     uint32_t st_mask_lo, st_mask_hi;
-    int st_compact;
+    int st_compact, in_mapped;
 };
 constexpr int PWSHAPE_WORDS = (int)(sizeof(PwShape) / 4);
 // the shape of a k_pw launch; false when its problems differ in a shape field
@@ -258,12 +262,13 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvA
                 q.cin, q.out_cs, q.out_off, q.cout, q.lds_w_off, q.part_stride,
                 tap ? a.umask : 0, tap ? a.uW : 0, tap ? a.uD : 0, tap ? a.udc : 0, tap ? a.uimg : 0,
                 tap ? a.udil : 0, tap ? a.uoff : 0,
-                q.st_mask_lo, q.st_mask_hi, q.st_compact};
+                q.st_mask_lo, q.st_mask_hi, q.st_compact, q.in_mapped};
     for (int i = 1; i < a.nprob; i++) {
         const ConvProb& r = a.p[i];
         if (r.in_cs != q.in_cs || r.in_off != q.in_off || r.cin != q.cin || r.out_cs != q.out_cs ||
             r.out_off != q.out_off || r.cout != q.cout || r.lds_w_off != q.lds_w_off || r.part_stride != q.part_stride ||
-            r.st_mask_lo != q.st_mask_lo || r.st_mask_hi != q.st_mask_hi || r.st_compact != q.st_compact)
+            r.st_mask_lo != q.st_mask_lo || r.st_mask_hi != q.st_mask_hi || r.st_compact != q.st_compact ||
+            r.in_mapped != q.in_mapped)
             return false;
     }
     return true;

@@ -425,6 +425,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         g.cinp = (b.cin + 3) / 4 * 4;
                         g.cout = b.cout;
                         g.out_off = b.out_off;
+                        g.opcs = c.gc;
                         g.dil = dil_eff > 0 ? dil_eff : b.dil;
                         g.G = (9 * (g.cinp / 4) + 3) / 4;
                         g.BW = TW + 2 * g.dil;
@@ -562,6 +563,9 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     }
                     if (!ok) continue;
                     g.ps = d;
+                    // little work per image: the next image's band load is a whole memory round trip
+                    // per image unless several are in flight (4 images: 32 VGPRs at 2 quads per thread)
+                    g.pd = g.nw == 4 ? 4 : 1;
                     g.nbk = nbk;
                     g.tpp = tpp;
                     g.tiles_x = 1;
@@ -662,6 +666,82 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     for (size_t k = 0; k < g.br.size(); k++) {
                         g.gcb[k].cin_off = c.t1_off[g.br[k]];
                         g.gcb[k].pcs = c.t1_pcs[g.br[k]];
+                    }
+            }
+        }
+
+        // t2 split into its producers' sub-tensors when there are several (cfg4 / cfg5: k_gc groups of one
+        // branch each); CNF_T2_MAP=0 is the A/B knob
+        {
+            bool allow_t2 = true;
+            if (const char* e = std::getenv("CNF_PW")) allow_t2 = allow_t2 && std::atoi(e) != 0;
+            if (const char* e = std::getenv("CNF_T2_MAP")) allow_t2 = allow_t2 && std::atoi(e) != 0;
+            int tap_dmin2 = 4;
+            if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin2 = std::atoi(e);
+            for (auto& c : p.couplings) {
+                c.t2_mapped = false;
+                c.t2_cs = c.gc;
+                c.t2_off.clear();
+                c.t2_pcs.clear();
+                c.t2_qmap.clear();
+                c.t2_bmap.clear();
+                for (const Branch& b : c.br) {
+                    c.t2_off.push_back(b.out_off);
+                    c.t2_pcs.push_back(c.gc);
+                }
+                if (c.use_lds || c.R == 0 || c.br.empty() || !allow_t2 || c.gc % 4 != 0 || c.gc > 128) continue;
+                std::vector<std::vector<int>> units;
+                for (const auto& g : c.gcg) units.push_back(g.br);
+                bool ok = true;
+                for (size_t bi = 0; bi < c.br.size(); bi++) {
+                    const Branch& b = c.br[bi];
+                    ok = ok && b.out_off % 4 == 0 && b.cout % 4 == 0;
+                    if (c.in_gc((int)bi)) continue;
+                    ok = ok && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin2;
+                    units.push_back({(int)bi});
+                }
+                if (!ok || units.size() < 2) continue;
+                const int hw = c.hc * c.wc;
+                std::vector<int> ust, ucs;
+                int total = 0;
+                for (const auto& u : units) {
+                    int lo = 1 << 30, hi = 0, sum = 0;
+                    for (int bi : u) {
+                        lo = std::min(lo, c.br[bi].out_off);
+                        hi = std::max(hi, c.br[bi].out_off + c.br[bi].cout);
+                        sum += c.br[bi].cout;
+                    }
+                    ok = ok && sum == hi - lo;   // the unit's slices are one channel range
+                    ust.push_back(lo);
+                    ucs.push_back(hi - lo);
+                    total += hi - lo;
+                }
+                if (!ok || total != c.gc) continue;
+                c.t2_mapped = true;
+                c.t2_cs = total;
+                c.t2_qmap.assign((size_t)2 * (c.gc / 4), -1);
+                c.t2_bmap.assign(c.br.size(), std::vector<int>(128, -1));
+                int base = 0;
+                for (size_t u = 0; u < units.size(); u++) {
+                    for (int ch = ust[u]; ch < ust[u] + ucs[u]; ch += 4) {
+                        c.t2_qmap[2 * (ch / 4)] = base + (ch - ust[u]);
+                        c.t2_qmap[2 * (ch / 4) + 1] = ucs[u];
+                    }
+                    for (int bi : units[u]) {
+                        const Branch& b = c.br[bi];
+                        c.t2_off[bi] = base + (b.out_off - ust[u]);
+                        c.t2_pcs[bi] = ucs[u];
+                        for (int j = 0; j < b.cout; j++) {
+                            c.t2_bmap[bi][2 * j] = c.t2_off[bi] + j;
+                            c.t2_bmap[bi][2 * j + 1] = ucs[u];
+                        }
+                    }
+                    base += hw * ucs[u];
+                }
+                for (auto& g : c.gcg)
+                    for (size_t k = 0; k < g.br.size(); k++) {
+                        g.gcb[k].out_off = c.t2_off[g.br[k]];
+                        g.gcb[k].opcs = c.t2_pcs[g.br[k]];
                     }
             }
         }
@@ -806,6 +886,20 @@ Plan* build_plan(const cnf_flow_desc* d) {
                             p.n_aux += (int64_t)at.size();
                         }
                     }
+                    if (c.t2_mapped && ln) {   // LN3 gamma/beta in t2's layout
+                        const int64_t hw = (int64_t)c.hc * c.wc;
+                        std::vector<int64_t> at((size_t)hw * c.t2_cs, -1);
+                        for (int ch = 0; ch < c.gc; ch++) {
+                            const int o = c.t2_qmap[2 * (ch / 4)] + ch % 4, st = c.t2_qmap[2 * (ch / 4) + 1];
+                            for (int64_t px = 0; px < hw; px++) at[o + px * st] = px * c.gc + ch;
+                        }
+                        for (int which = 0; which < 2; which++) {
+                            const int64_t src = which == 0 ? rb.ln3g : rb.ln3b;
+                            (which == 0 ? rb.ln3c_g : rb.ln3c_b) = p.n_aux;
+                            for (int64_t v : at) p.aux_map.push_back(v >= 0 ? src + v : -1);
+                            p.n_aux += (int64_t)at.size();
+                        }
+                    }
                     pack(rb.cb, PK_1X1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
                          [=](int n) { return bb + n; });
                     dense_img(rb.cb, 1, c.gc, nk, [=](int ci2, int j) { return bk + (int64_t)ci2 * nk + j; },
@@ -919,6 +1013,15 @@ Plan* build_plan(const cnf_flow_desc* d) {
             if (c.t1_compact) {
                 c.dev_t1_map = (int)p.host_table.size();
                 p.host_table.insert(p.host_table.end(), c.t1_map.begin(), c.t1_map.end());
+            }
+            c.dev_t2_bmap.assign(c.br.size(), -1);
+            if (c.t2_mapped) {
+                c.dev_t2_qmap = (int)p.host_table.size();
+                p.host_table.insert(p.host_table.end(), c.t2_qmap.begin(), c.t2_qmap.end());
+                for (size_t bi = 0; bi < c.br.size(); bi++) {
+                    c.dev_t2_bmap[bi] = (int)p.host_table.size();
+                    p.host_table.insert(p.host_table.end(), c.t2_bmap[bi].begin(), c.t2_bmap[bi].end());
+                }
             }
         }
         p.dev_final_orig = (int)p.host_table.size();

@@ -48,6 +48,7 @@ struct RBParams {
     std::vector<PackedConv> gc;                // grouped branches as dense 3x3 convs (PK_KN)
     std::vector<PackedConv> gpw;               // streamed, k_gc not fused: branch as a 1x1 over its 9*cin im2col row (size 0: none)
     int64_t ln2c_g = -1, ln2c_b = -1;          // aux: LN2 gamma/beta gathered to the compact t1 layout (t1_compact)
+    int64_t ln3c_g = -1, ln3c_b = -1;          // aux: LN3 gamma/beta in the mapped t2 layout (t2_mapped)
 };
 
 struct NetParams {
@@ -96,6 +97,7 @@ struct Coupling {
         int TP = 0;                       // tile pixels the plan aimed at (TH = min(H, TP / TW))
         int ps = 1, nbk = 1, tpp = 1;     // polyphase tiles (GcShape): phase stride, grids per tile, slices per grid
         int nw = GC_NW_SPEC;              // waves per workgroup (GcShape::nw)
+        int pd = 1;                       // band prefetch depth in images (GcShape::pd)
     };
     std::vector<GcGroup> gcg;
     bool gc_fused = false;                // gcg non-empty
@@ -110,6 +112,17 @@ struct Coupling {
     bool t1_compact = false;
     std::vector<int> t1_off, t1_pcs, t1_map;
     int dev_t1_map = -1;   // offset of t1_map in the device table
+    // ... and t2 (the grouped stage's concat, conv_b's input) likewise when several launches produce it:
+    // one dense sub-tensor per producer, so a k_gc group of a few output channels stores whole lines
+    // instead of 16-32 bytes of every (124-channel) pixel. t2_cs = floats per pixel of an image,
+    // t2_off[bi] / t2_pcs[bi] = branch bi's output slice (offset of pixel 0, pixel stride), t2_qmap =
+    // (offset, stride) per input quad of conv_b, t2_bmap[bi] = branch bi's per-output-channel store map
+    bool t2_mapped = false;
+    int t2_cs = 0;
+    std::vector<int> t2_off, t2_pcs, t2_qmap;
+    std::vector<std::vector<int>> t2_bmap;
+    int dev_t2_qmap = -1;
+    std::vector<int> dev_t2_bmap;
     bool in_gc(int bi) const {
         for (const GcGroup& g : gcg)
             for (int b : g.br)

@@ -268,7 +268,8 @@ struct TapSrc {
 
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
 static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
-                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, const int* st_map = nullptr) {
+                       uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, const int* st_map = nullptr,
+                       const int* in_map = nullptr) {
     const bool st_compact = st_map != nullptr;
     if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
@@ -321,6 +322,10 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         q.st_mask_hi = (uint32_t)(store_mask >> 32);
         q.st_compact = st_compact ? 1 : 0;
         q.st_map = st_map;
+        q.in_mapped = in_map != nullptr ? 1 : 0;
+        q.in_map = in_map;
+        if (in_map != nullptr && (ks != 1 || tap != nullptr || s.in_off != 0 || s.cin % 4 != 0))
+            throw std::logic_error("mapped input: plain k_pw over whole quads only");
         if (st_compact && (s.res != nullptr || s.cout > 64)) throw std::logic_error("mapped stores: no residual, <= 64 outputs");
         if (s.cout > 64) throw std::invalid_argument("conv with more than 64 output channels");
         const int K = ks * ks * s.cin;
@@ -384,7 +389,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         fits32 = fits32 && (double)h * w * std::max(s.in_cs, s.out_cs) * 4.0 < 2147483648.0 &&
                  (tap == nullptr || (double)tap->img * 4.0 < 2147483648.0);
     const bool pw_ok = ks == 1 && vec && pw_gm > 0 && ln_uniform && fits32 && E.p.use_pw;
-    if (st_compact && !pw_ok) throw std::logic_error("compact stores need the k_pw path");
+    if ((st_compact || in_map != nullptr) && !pw_ok) throw std::logic_error("mapped loads / stores need the k_pw path");
     if (ks == 3) {
         const int grid_x = E.B * g.tiles;
         const int mr = g.MR;
@@ -705,6 +710,12 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // LN2 gamma/beta in t1's layout: the aux copies gathered to the compact layout, or the parameters
     auto ln2g = [&](const RBParams& rb) { return c.t1_compact ? X + rb.ln2c_g : P + rb.ln2g; };
     auto ln2b = [&](const RBParams& rb) { return c.t1_compact ? X + rb.ln2c_b : P + rb.ln2b; };
+    auto ln3g = [&](const RBParams& rb) { return c.t2_mapped ? X + rb.ln3c_g : P + rb.ln3g; };
+    auto ln3b = [&](const RBParams& rb) { return c.t2_mapped ? X + rb.ln3c_b : P + rb.ln3b; };
+    // device-table maps of the mapped layouts (fake, never dereferenced, in dry runs)
+    auto dmap = [&](int off) -> const int* {
+        return E.p.dry ? reinterpret_cast<const int*>(uintptr_t(1) << 40) : E.p.dev_table + off;
+    };
 
     // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
     if (cin_tap) {
@@ -773,7 +784,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.s.H = c.hc;
             ga.s.W = c.wc;
             ga.s.in_cs = c.t1_cs;
-            ga.s.out_cs = c.gc;
+            ga.s.out_cs = c.t2_cs;
             ga.B = B;
             ga.s.TH = gg.TH;
             ga.s.TW = gg.TW;
@@ -783,6 +794,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.s.nbk = gg.nbk;
             ga.s.tpp = gg.tpp;
             ga.s.nw = gg.nw;
+            ga.s.pd = gg.pd;
             ga.in_nparts = sl[0][1].nparts;
             ga.part_stride = L.st_parts;
             // images per workgroup: one workgroup per CU, looping over its images with the next
@@ -824,13 +836,14 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int n = 0; n < 2; n++) {
                     const RBParams& rb = c.net[n].rb[r];
                     pt.push_back(ProbSpec{t1[n], 9 * b.cin, 0, 9 * b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
-                                          ln ? ln2b(rb) : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.gc,
+                                          ln ? ln2b(rb) : none, 1, X + rb.gpw[bi].w, X + rb.gpw[bi].b, t2[n], c.t2_cs,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base, 1});
                 }
+                const int* bmap = c.t2_mapped ? dmap(c.dev_t2_bmap[bi]) : nullptr;
                 TapSrc ts{-1, c.wc, c.t1_pcs[bi], b.cin, c.hc * c.wc * c.t1_cs};
                 ts.dil = b.dil;
                 ts.off = c.t1_off[bi];
-                base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts);
+                base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts, bmap);
                 done[bi] = 1;
             }
             int nrest = 0;
@@ -840,7 +853,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (int bi = 0; bi < nbr; bi++) {
                     const Branch& b = c.br[bi];
                     if (done[bi]) continue;
-                    if (c.t1_compact) throw std::logic_error("k_conv<3> branch on a mapped t1 layout");
+                    if (c.t1_compact || c.t2_mapped) throw std::logic_error("k_conv<3> branch on a mapped t1 / t2 layout");
                     pr.push_back(ProbSpec{t1[n], c.nk, b.cin_off, b.cin, in_slab(n, 1), ln ? ln2g(rb) : none,
                                           ln ? ln2b(rb) : none, 1, X + rb.gc[bi].w, X + rb.gc[bi].b, t2[n], c.gc,
                                           b.out_off, b.cout, none, out_slab(n, 2, 0), base + k * nt3 * 4, b.dil});
@@ -857,11 +870,12 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
-                pr.push_back(ProbSpec{t2[n], c.gc, 0, c.gc, in_slab(n, 2), ln ? P + rb.ln3g : none,
-                                      ln ? P + rb.ln3b : none, 1, X + rb.cb.w, X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n],
+                pr.push_back(ProbSpec{t2[n], c.t2_cs, 0, c.gc, in_slab(n, 2), ln ? ln3g(rb) : none,
+                                      ln ? ln3b(rb) : none, 1, X + rb.cb.w, X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n],
                                       out_slab(n, 0, 4 * nt1), 0, 1});
             }
-            set_parts(0, conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr));
+            set_parts(0, conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr, ~0ull, nullptr, nullptr,
+                                     c.t2_mapped ? dmap(c.dev_t2_qmap) : nullptr));
         }
     }
     // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b); > 64 outputs in 64-channel chunks
@@ -1563,7 +1577,7 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
         s.H = c.hc;
         s.W = c.wc;
         s.in_cs = c.t1_cs;   // as run_coupling launches it
-        s.out_cs = c.gc;
+        s.out_cs = c.t2_cs;
         s.TH = gg.TH;
         s.TW = gg.TW;
         s.tiles_x = gg.tiles_x;
@@ -1572,6 +1586,7 @@ int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) 
         s.nbk = gg.nbk;
         s.tpp = gg.tpp;
         s.nw = gg.nw;
+        s.pd = gg.pd;
         s.band_bytes = gg.band_bytes;
         s.lnst = p.desc.layer_norm ? 3 : 0;   // the forward's k_gc: LN2 on load and LN3 partials iff LayerNorm
         std::memcpy(words + n, &s, sizeof(s));

@@ -90,6 +90,15 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     const int pa = tile * (16 * NW) + wave * 16 + i16;
     const bool pav = full_px || pa < HW;
     const uint32_t aoff = ((uint32_t)pa * PP(in_cs) + PP(in_off) + 4 * kq) * 4u;
+    // mapped input (conv_b over a t2 split into its producers' sub-tensors): quad 4g + kq of the
+    // lane's pixel at in_map's (offset, pixel stride)
+    uint32_t amap[GM];
+#pragma unroll
+    for (int g = 0; g < GM; g++)
+        amap[g] = PP(in_mapped) && 16 * g + 4 * kq < cin
+                      ? (uint32_t)(P.in_map[2 * (4 * g + kq)] + pa * P.in_map[2 * (4 * g + kq) + 1]) * 4u
+                      : 0u;
+    auto aoffg = [&](int g) -> uint32_t { return PP(in_mapped) ? amap[g] : aoff + 64u * g; };
     auto gok = [&](int g) { return pav && g < G && (cin % 16 == 0 || 16 * g + 4 * kq < cin); };
     // output: acc[n][r] = out[pixel po0 + r][channel 16n + i16]
     const int po0 = tile * (16 * NW) + wave * 16 + kq * 4;
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             }
         } else {
 #pragma unroll
-            for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoff + 64u * g : BUF_OOB);
+            for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoffg(g) : BUF_OOB);
         }
         if (RES) {
             const auto rres = img_rsrc(RES ? P.res : P.out, img0 + ii, out_img);
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
                     }
                 }
             } else {
-                const uint32_t o = gok(g) ? aoff + 64u * g : BUF_OOB;   // 0 where masked: the normalised value is then exactly 0
+                const uint32_t o = gok(g) ? aoffg(g) : BUF_OOB;   // 0 where masked: the normalised value is then exactly 0
                 gm[g] = buf_load4(rg, o);
                 bt[g] = buf_load4(rb, o);
             }
@@ -431,7 +440,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
 #pragma unroll
         for (int r = 0; r < 4; r++) bz[n][r] = r < nq[n] ? bias[c0 + r] : 0.f;
     }
-    const bool vq = ((GS(out_cs) | br.out_off) & 3) == 0;
+    const bool vq = ((br.opcs | br.out_off) & 3) == 0;
     const int nsub = (npx + 15) >> 4;
     // two subtiles per wave and pass (s0, s0 + NW) share every B read: two independent MFMA
     // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
@@ -495,10 +504,14 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             if (h == 1 && !v1) break;
             const int po = (h ? s1 : s0) * 16 + i16;
             const bool pv = po < npx;
-            float* orow = outp + (size_t)gc_out_pixel<SID>(a, pv ? po : 0, px0, r0, ph0) * GS(out_cs) + br.out_off + 4 * kq;
+            float* orow = outp + (size_t)gc_out_pixel<SID>(a, pv ? po : 0, px0, r0, ph0) * br.opcs + br.out_off + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NR; n++) {
                 f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
+#ifdef CNF_ABL_GC_NOSTORE_POLY   // ablation (diagnostic builds only): no t2 stores from polyphase tiles
+                if (GS(ps) > 1) {
+                } else
+#endif
                 if (pv && nq[n] == 4 && vq) {
                     *reinterpret_cast<f4*>(orow + n * 16) = v;
                 } else if (pv) {
@@ -518,6 +531,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
 // staged band quads per thread: 2 in the specialised instantiations (the plan keeps a group's bands
 // within 128 quads per wave), GC_STAGE_QUADS over the generic kernel's threads
 #define GC_GQS (SID >= 0 ? 2 : GC_STAGE_QUADS / GC_NTS)
+#define GC_PDS (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].pd : 1)   // band prefetch depth (images)
 
 // the branches of table entry SID, unrolled at compile time
 template <int SID, int BI>
@@ -551,7 +565,7 @@ __device__ long long g_gc_stamps[64];
 // latency hides behind the compute; the tile's LN2 gamma/beta stay in registers for all images.
 template <int SID>
 __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArgs a) {
-    constexpr int GC_NW = GC_NWS, GC_NT = GC_NTS, GC_GQ = GC_GQS;
+    constexpr int GC_NW = GC_NWS, GC_NT = GC_NTS, GC_GQ = GC_GQS, PD = GC_PDS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
     const int tile = blockIdx.x % GS(tiles_per_img);
@@ -625,19 +639,19 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     };
     const uint32_t img_bytes = (uint32_t)HW * GS(in_cs) * 4u;
     // tile LN2 gamma/beta (image-independent) and the first image's raw quads, all in flight together
-    f4 gq[GC_GQ], bq[GC_GQ], xq[GC_GQ];
+    f4 gq[GC_GQ], bq[GC_GQ], xq[PD][GC_GQ];   // xq: a ring of PD images' raw quads
 #pragma unroll
     for (int u = 0; u < GC_GQ; u++) {
         gq[u] = ln ? load_q(buf_rsrc(a.gamma[net], img_bytes), u) : f4{1.f, 1.f, 1.f, 1.f};
         bq[u] = ln ? load_q(buf_rsrc(a.beta[net], img_bytes), u) : f4{0.f, 0.f, 0.f, 0.f};
     }
-    auto load_img = [&](int ii) {
+    auto load_img = [&](int ii, f4 (&xd)[GC_GQ]) {
         const auto r = buf_rsrc(a.in[net] + (size_t)(img0 + ii) * HW * GS(in_cs), img_bytes);
 #pragma unroll
-        for (int u = 0; u < GC_GQ; u++) xq[u] = load_q(r, u);
+        for (int u = 0; u < GC_GQ; u++) xd[u] = load_q(r, u);
     };
     // LN2(LeakyReLU(t1)) of the quads in xq -> band buffer (ii & 1); zero outside the image / window
-    auto store_img = [&](int ii) {
+    auto store_img = [&](int ii, const f4 (&xs)[GC_GQ]) {
         const float rs = ln ? lstat[2 * ii + 1] : 1.f;
         const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
         float* dst = lds_f + (ii & 1) * (GS(band_bytes) / 4);
@@ -648,14 +662,14 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
             if (nv[u] != 0) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const float t = lrelu(xq[u][j]);
+                    const float t = lrelu(xs[u][j]);
                     v[j] = ln ? fmaf(fmaf(t, rs, nmr), gq[u][j], bq[u][j]) : t;
                 }
             }
             *reinterpret_cast<f4*>(dst + loff[u]) = v;
         }
     };
-    load_img(0);
+    load_img(0, xq[0]);
     // this wave's first LN2 image: partial slots fetched in the same memory round trip as the band
     // and weight loads (folded below)
     ConvProb lnP;
@@ -697,13 +711,24 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
         }
     }
     __syncthreads();
-    store_img(0);
+    store_img(0, xq[0]);
     __syncthreads();
     GSTAMP(gs++);
 
-    for (int ii = 0; ii < nimg; ii++) {
+    // the ring's other images (PD > 1)
+#pragma unroll
+    for (int j = 1; j < PD; j++)
+        if (j < nimg) load_img(j, xq[j]);
+    for (int i0 = 0; i0 < nimg; i0 += PD)
+#pragma unroll
+    for (int jj = 0; jj < PD; jj++) {
+        const int ii = i0 + jj;
+        if (ii >= nimg) break;
         const int img = img0 + ii;
-        if (ii + 1 < nimg) load_img(ii + 1);   // lands while this image's MFMAs run
+        // lands while this image's MFMAs run: the next image (PD == 1), or image ii + PD into the
+        // ring slot image ii (already staged) leaves
+        if (PD == 1 && ii + 1 < nimg) load_img(ii + 1, xq[0]);
+        if (PD > 1 && ii + PD < nimg) load_img(ii + PD, xq[jj]);
         LnAcc st;
         st.reset();
         bool first = true;
@@ -725,7 +750,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
             }
         }
         if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * LNP);
-        if (ii + 1 < nimg) store_img(ii + 1);   // the other buffer: nobody reads it this iteration
+        if (ii + 1 < nimg) store_img(ii + 1, xq[(jj + 1) % PD]);   // the other buffer: nobody reads it this iteration
         __syncthreads();
         GSTAMP(gs++);
     }

@@ -31,7 +31,7 @@ OUT_GC = HERE / 'cnf_gc_shapes.inc'
 OUT_PW = HERE / 'cnf_pw_shapes.inc'
 PW_BATCH = 64                 # the benchmark batch (k_pw shapes do not depend on it: ipw and B stay runtime)
 PW_MASK_WORDS = 2             # PwShape ends with the two uint32 stored-channel masks and st_compact
-GC_BRANCH_WORDS = 17          # GcBranch: 15 ints, then the two uint32 division magics
+GC_BRANCH_WORDS = 18          # GcBranch: 16 ints, then the two uint32 division magics
 GC_MAXBR = 8
 CNF_LAYER_COUPLING = 0
 CAP = 2048
@@ -121,9 +121,9 @@ def render_pw(sh):
         if w is None:
             lines.append('    {},')
             continue
-        k = len(w) - PW_MASK_WORDS - 1
-        lines.append('    {' + ', '.join([str(x) for x in w[:k]] + [f'{x & 0xffffffff}u' for x in w[k:-1]] +
-                                       [str(w[-1])]) + '},')
+        k = len(w) - PW_MASK_WORDS - 2   # ..., st_mask_lo, st_mask_hi, st_compact, in_mapped
+        lines.append('    {' + ', '.join([str(x) for x in w[:k]] + [f'{x & 0xffffffff}u' for x in w[k:k + 2]] +
+                                       [str(x) for x in w[k + 2:]]) + '},')
     lines.append('};')
     return '\n'.join(lines) + '\n'
 

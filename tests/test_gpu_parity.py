@@ -172,7 +172,7 @@ def test_layerwise_equals_fused(gpu, name, B):
 
 @pytest.mark.parametrize('name,B', [('cfg2', 3), ('cfg4', 2), ('cfg5', 1)])
 def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
-    """The streamed layers' t1 sub-tensor layout (CNF_T1_COMPACT) changes where t1's values live, never
+    """The streamed layers' t1 / t2 sub-tensor layouts (CNF_T1_COMPACT, CNF_T2_MAP) change where values live, never
     the arithmetic: with the generic k_gc / k_pw in both runs (the plain layout has no specialised
     instantiation, and those partition the LN statistics over their own wave counts) zy, the per-image
     log-det and the inverse are equal bit for bit. The polyphase tiles of large dilations (CNF_GC_POLY,
@@ -181,7 +181,7 @@ def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
     import os
     flow, ora, P, xy = _setup(name, B)
     x = torch.from_numpy(xy).to(gpu)
-    for knob in ('CNF_T1_COMPACT', 'CNF_GC_POLY'):
+    for knob in ('CNF_T1_COMPACT', 'CNF_T2_MAP', 'CNF_GC_POLY'):
         os.environ[knob] = '0'
         try:
             f2, _, _, _ = _setup(name, B)
@@ -198,7 +198,7 @@ def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
         finally:
             os.environ.pop('CNF_GC_GENERIC', None)
             os.environ.pop('CNF_PW_GENERIC', None)
-        if knob == 'CNF_T1_COMPACT':
+        if knob != 'CNF_GC_POLY':
             assert torch.equal(zy, zy0) and torch.equal(ld, ld0) and torch.equal(xi, xi0), knob
         else:
             # two fp32 summation orders of every LN3 statistic: a few ulp per layer, well inside the
