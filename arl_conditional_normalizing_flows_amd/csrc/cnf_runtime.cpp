@@ -1598,6 +1598,26 @@ int cnf_debug_gc_words() { return GCSHAPE_WORDS; }
 
 // t1 layout of a coupling (Coupling::t1_map): [compact, floats per pixel of the image, then per branch
 // (window offset of pixel 0, pixel stride, cin_off, cin), then 128 words of t1_map (compact only)]
+// t2 layout of a coupling (Coupling::t2_*): [mapped, floats per pixel of the image, gc, then per branch
+// (slice offset of pixel 0, pixel stride, out_off, cout), then conv_b's quad map (gc / 4 pairs, mapped only)]
+int cnf_debug_t2_layout(const cnf_plan* plan, int coupling, int* words, int cap) {
+    if (!plan || !words) return -1;
+    const Plan& p = *plan->p;
+    if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
+    const Coupling& c = p.couplings[coupling];
+    std::vector<int> w = {c.t2_mapped ? 1 : 0, c.t2_cs, c.gc};
+    for (size_t bi = 0; bi < c.br.size(); bi++) {
+        w.push_back(bi < c.t2_off.size() ? c.t2_off[bi] : -1);
+        w.push_back(bi < c.t2_pcs.size() ? c.t2_pcs[bi] : -1);
+        w.push_back(c.br[bi].out_off);
+        w.push_back(c.br[bi].cout);
+    }
+    w.insert(w.end(), c.t2_qmap.begin(), c.t2_qmap.end());
+    if ((int)w.size() > cap) return -1;
+    std::memcpy(words, w.data(), w.size() * sizeof(int));
+    return (int)w.size();
+}
+
 int cnf_debug_t1_layout(const cnf_plan* plan, int coupling, int* words, int cap) {
     if (!plan || !words) return -1;
     const Plan& p = *plan->p;

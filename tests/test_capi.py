@@ -297,3 +297,49 @@ def test_t1_layout_is_dense_per_consumer(lib, name):
         lib.cnf_plan_destroy(p)
     if name in ('cfg2', 'cfg5'):
         assert compact_seen > 0
+
+
+@pytest.mark.parametrize('name', ['cfg2', 'cfg4', 'cfg5', 'small'])
+def test_t2_layout_is_dense_per_producer(lib, name):
+    """When several launches produce t2 (cfg4 / cfg5), it holds one dense sub-tensor per producer
+    (Coupling::t2_*): each branch's output slice has its own pixel stride, conv_b's quad map agrees
+    with the slices, and every (pixel, channel) of the image has its own float among its t2_cs floats
+    per pixel. cfg2's single k_gc group keeps the plain layout."""
+    kw = PRESETS[name].kwargs()
+    kw.pop('group_mode')
+    rc, p, keep = _plan(lib, kw)
+    assert rc == 0
+    lib.cnf_debug_t2_layout.restype = C.c_int
+    lib.cnf_debug_t2_layout.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int]
+    o = OracleCFlow(**kw)
+    mapped = 0
+    try:
+        for c in o.coupling_specs:
+            buf = (C.c_int * 512)()
+            n = lib.cnf_debug_t2_layout(p, c.index, buf, 512)
+            assert n >= 3
+            w = list(buf[:n])
+            m, cs, gc = w[:3]
+            nb = len(c.branches)
+            br = [w[3 + 4 * i:7 + 4 * i] for i in range(nb)]
+            if not m:
+                assert cs == gc and all(b[0] == b[2] and b[1] == gc for b in br)
+                continue
+            mapped += 1
+            assert cs == gc
+            q = np.array(w[3 + 4 * nb:3 + 4 * nb + 2 * (gc // 4)]).reshape(-1, 2)
+            hw = c.hc * c.wc
+            where = {}
+            for off, pcs, out_off, cout in br:
+                assert off % 4 == 0 and pcs % 4 == 0 and cout <= pcs
+                for j in range(cout):
+                    where[out_off + j] = (off + j, pcs)
+            assert sorted(where) == list(range(gc))
+            for qi in range(gc // 4):
+                assert tuple(q[qi]) == where[4 * qi]
+                assert all(where[4 * qi + k] == (where[4 * qi][0] + k, where[4 * qi][1]) for k in range(4))
+            idx = np.concatenate([o_ + np.arange(hw) * s_ for o_, s_ in where.values()])
+            assert idx.min() >= 0 and idx.max() < hw * cs and np.unique(idx).size == idx.size
+    finally:
+        lib.cnf_plan_destroy(p)
+    assert (mapped > 0) == (name in ('cfg4', 'cfg5'))
