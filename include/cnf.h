@@ -96,8 +96,10 @@ int cnf_plan_num_param_tensors(const cnf_plan* plan);
 int cnf_plan_param_tensor(const cnf_plan* plan, int index, char* name, int name_cap,
                           int64_t* offset, int* ndim, int shape[4]);
 
-/* Device-side auxiliary parameter image (dense grouped-conv weights built from
- * the per-group Conv2D kernels). Size in floats; filled by cnf_pack_params,
+/* Device-side auxiliary parameter image (every conv's weights in its kernel's
+ * staging layout, the grouped convs as dense images built from the per-group
+ * Conv2D kernels, and the streamed layers' LN2 / LN3 gamma/beta gathered into
+ * their t1 / t2 sub-tensor layouts). Size in floats; filled by cnf_pack_params,
  * which must run again whenever the canonical params change. */
 int64_t cnf_plan_aux_floats(const cnf_plan* plan);
 int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* stream);
