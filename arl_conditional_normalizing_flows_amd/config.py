@@ -55,4 +55,7 @@ PRESETS = {
     # small architectures for tests
     'tiny': FlowConfig((8, 8, 2), 1, (0, 1), (1, 1), (8, 8), (2, 2), batch=2, name='tiny'),
     'small': FlowConfig((16, 16, 4), 3, (0, 1, 0), (2, 1, 1), (16, 16, 8), (4, 4, 2), batch=3, name='small'),
+    # squeezes down to 2x2 blocks: checkerboard couplings 2 and 1 pixels wide (a shape the reference
+    # accepts; the training path's narrow-width weight-gradient fallback)
+    'narrow': FlowConfig((8, 8, 4), 3, (1, 1, 0), (1, 1, 1), (8, 8, 8), (2, 2, 2), batch=2, name='narrow'),
 }

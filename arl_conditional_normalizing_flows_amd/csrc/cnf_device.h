@@ -35,6 +35,12 @@ __device__ __forceinline__ float cpl_tanh(float x) {
     return copysignf(t, x);
 }
 __device__ __forceinline__ float cpl_exp(float s) { return __expf(s); }
+// the affine law on one transformed element (k_coupling, and the deferred law in k_net_lds / k_map2:
+// one expression, so the fused schedules equal the layer-by-layer API bit for bit)
+// dir > 0: v2 = exp(s) u2 + t (:1215-1233); dir < 0: u2 = reciprocal(exp(s)) (v2 - t) (:1235-1253)
+__device__ __forceinline__ float cpl_law(float s, float x, float t, int dir) {
+    return dir > 0 ? fmaf(cpl_exp(s), x, t) : (1.0f / cpl_exp(s)) * (x - t);
+}
 
 // compressed index (p * dc2 + c) in layer k's transformed half of element pos of u_k, or -1 when pos
 // lies in its conditioning half: the inverse of mask_pos_ for the complement mask q.mask_c

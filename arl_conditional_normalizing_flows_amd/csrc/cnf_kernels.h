@@ -130,6 +130,10 @@ struct CoupPend {
     // k's conditioning half, mask / dc1) from u_k — no pass over v_k at the end of the kernel
     int comp = 0, mask = 0, dc1 = 0;
     int W = 0, D = 0;   // u_k's width and depth (k_map2 applies a pending coupling of the last layer of a block)
+    // +1: the forward law v2 = exp(s) u2 + t (ld_part collects layer k's sum of s); -1: the inverse
+    // law u2 = (1 / exp(s)) (v2 - t) of cnf_flow_inverse (ld_part null). In the inverse schedule
+    // "layer k" is the layer just run and "k+1" the one before it in index order, run next.
+    int dir = 1;
 };
 
 struct NetLdsArgs {
@@ -297,6 +301,7 @@ struct MapOp {
     const int* sidx = nullptr;
     const int* didx = nullptr;
     int n = 0, ss = 0, ds = 0;
+    int pend = 0;   // k_map2: read the source through the launch's pending coupling (src is then unused)
 };
 struct LdReduce {
     const double* part = nullptr;   // null: no reduction
@@ -364,6 +369,9 @@ constexpr int WGRAD_MAX_CHUNKS = 256;
 int wgrad_band_chunks(int B, int H, int W, int taps, int CI, int CO);
 size_t wgrad_band_lds(int H, int W, int taps, int dil, int CI, int CO);
 bool train_valu_kernels();   // CNF_TRAIN_VALU=1: the register-blocked VALU convolutions (A/B)
+// k_wgrad_band handles this conv (taps 1 / 9, width >= 4, staged band within 160 KiB); otherwise the
+// weight gradient runs on the VALU k_wgrad (WGradArgs::chunk_px > 0) with a separate bias scatter
+bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO);
 // dparams[map[i]] += sum_c part[c][i] for i < n (map[i] >= 0)
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st);
 void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st);

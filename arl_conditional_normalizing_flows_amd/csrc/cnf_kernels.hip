@@ -503,15 +503,8 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
                 t = tb[e];
             }
             const float s = w * cpl_tanh(sp);
-            const float x = ub[q];
-            float y;
-            if (a.dir > 0) {
-                y = fmaf(cpl_exp(s), x, t);   // (k_net_lds applies a deferred coupling with the same expression)
-                lsum += s;
-            } else {
-                y = (1.0f / cpl_exp(s)) * (x - t);
-            }
-            vb[q] = y;
+            vb[q] = cpl_law(s, ub[q], t, a.dir);   // (k_net_lds / k_map2 apply a deferred coupling with the same expression)
+            if (a.dir > 0) lsum += s;
         } else {
             const int e1 = e - n2;
             const int p = e1 / a.dc1, c = e1 - p * a.dc1;
@@ -621,8 +614,9 @@ __global__ __launch_bounds__(256) void k_map_scatter(const float* __restrict__ s
     }
 }
 
-// blocks [0, ga): map a; [ga, ga + gb): map b; block ga + gb (when r.part or pend.on): the log-det
-// work of image blockIdx.y by wave 0 — layer k's sum of s for a pending coupling, and / or the
+// blocks [0, ga): map a; [ga, ga + gb): map b (each reading its source through the pending coupling
+// when MapOp::pend); block ga + gb (when r.part, or a pending forward coupling): the log-det work of
+// image blockIdx.y by wave 0 — layer k's sum of s for a pending forward coupling, and / or the
 // reduction of the partial slots (as k_ld_reduce)
 __global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, LdReduce r, CoupPend q, int B) {
     const int img = blockIdx.y;
@@ -631,7 +625,7 @@ __global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, 
     if (bx < ga + gb) {
         const MapOp& m = bx < ga ? a : b;
         const int g0 = bx < ga ? 0 : ga, gn = bx < ga ? ga : gb;
-        if (q.on) {
+        if (q.on && m.pend) {
             const float* ub = q.u + (size_t)img * n_img;
             const size_t sb = (size_t)img * q.hc * q.wc * q.dc2;
             const float w = *q.tanh_w;
@@ -640,7 +634,7 @@ __global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, 
                 const int d = m.didx ? m.didx[i] : i;
                 const int ci = pend_index(q, s, q.W, q.D);
                 float v = ub[s];
-                if (ci >= 0) v = fmaf(cpl_exp(w * cpl_tanh(q.s_pre[sb + ci])), v, q.t[sb + ci]);   // k_coupling's expression
+                if (ci >= 0) v = cpl_law(w * cpl_tanh(q.s_pre[sb + ci]), v, q.t[sb + ci], q.dir);   // k_coupling's expression
                 m.dst[(size_t)img * m.ds + d] = v;
             }
         } else {
@@ -655,7 +649,7 @@ __global__ __launch_bounds__(256) void k_map2(MapOp a, MapOp b, int ga, int gb, 
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
     double acc = 0.0;
-    if (q.on) {
+    if (q.on && q.ld_part != nullptr) {
         const int n2 = q.hc * q.wc * q.dc2;
         const float* sp = q.s_pre + (size_t)img * n2;
         const float w = *q.tanh_w;
@@ -902,7 +896,7 @@ void launch_map_scatter(const float* src, float* dst, const int* sidx, const int
 void launch_map2(const MapOp& a, const MapOp& b, const LdReduce& r, const CoupPend& pend, int B, hipStream_t st) {
     auto gx = [](int n) { return n <= 0 ? 0 : (n + 255) / 256 > 64 ? 64 : (n + 255) / 256; };
     const int ga = gx(a.n), gb = gx(b.n);
-    const int g = ga + gb + (r.part || pend.on ? 1 : 0);
+    const int g = ga + gb + (r.part || (pend.on && pend.ld_part) ? 1 : 0);
     if (g == 0) return;
     if (pend.on && pend.np > 64) throw std::invalid_argument("k_map2: more than 64 log-det slots");
     CNF_LAUNCH(k_map2, dim3(g, B), dim3(256), 0, st, a, b, ga, gb, r, pend, B);

@@ -936,7 +936,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             const int p = e / SA(dc1), c = e - p * SA(dc1);
             const int pos = mask_pos_(a.mask, p, c, W, SA(W), SA(D));
             const float s = w * cpl_tanh(q.s_pre[sb + e]);
-            const float val = fmaf(cpl_exp(s), ub[pos], q.t[sb + e]);   // k_coupling's expression, bit for bit
+            const float val = cpl_law(s, ub[pos], q.t[sb + e], q.dir);   // k_coupling's expression, bit for bit
             T2[p * SU + c] = val;
             if (net == 0) {
                 vb[pos] = val;
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             const float x = ub[pos];
             if (ci < 0) return x;
             s = w * cpl_tanh(q.s_pre[sb + ci]);
-            return fmaf(cpl_exp(s), x, q.t[sb + ci]);   // k_coupling's expression, bit for bit
+            return cpl_law(s, x, q.t[sb + ci], q.dir);   // k_coupling's expression, bit for bit
         };
         const int n = HW * SA(dc1);
         for (int e = threadIdx.x; e < n; e += NT) {
@@ -986,7 +986,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         wpf_store(pf, WL, ci_src);
         lst_reset(st);
         lds_barrier();
-        if (a.pend.comp != 0 && net == 0 && threadIdx.x == 0) {   // layer k's log-det partial slots
+        if (a.pend.comp != 0 && net == 0 && threadIdx.x == 0 && a.pend.ld_part != nullptr) {   // layer k's log-det partial slots
             const double* ws = reinterpret_cast<const double*>(smem + NW * 16);
             double t = 0.0;
             for (int i = 0; i < NW; i++) t += ws[i];
@@ -1203,7 +1203,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             const float x = ub[pos];
             if (ci < 0) return x;
             s = w * cpl_tanh(q.s_pre[sb + ci]);
-            return fmaf(cpl_exp(s), x, q.t[sb + ci]);
+            return cpl_law(s, x, q.t[sb + ci], q.dir);
         };
         const bool split = q.np >= 2;
         const int e0 = split && net == 1 ? n_img / 2 : 0, e1 = split && net == 0 ? n_img / 2 : n_img;
@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const double ws = wave_sum((double)lsum);
         if ((threadIdx.x & 63) == 0) lsl[threadIdx.x >> 6] = ws;
         lds_barrier();
-        if (threadIdx.x == 0 && (split || net == 0)) {
+        if (threadIdx.x == 0 && (split || net == 0) && q.ld_part != nullptr) {   // (the inverse has none)
             double t = 0.0;
             for (int i = 0; i < NW; i++) t += lsl[i];
             double* dst = q.ld_part + (size_t)img * q.np;

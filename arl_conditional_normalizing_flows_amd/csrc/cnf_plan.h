@@ -8,6 +8,8 @@
 #include <cstdint>
 #include <functional>
 #include <string>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/cnf.h"
@@ -237,6 +239,12 @@ struct Plan {
     hipStream_t wside[2] = {nullptr, nullptr};
     std::vector<hipEvent_t> tev;
     size_t tev_next = 0;
+    // cnf_nll's completion counters: NLL_SLOTS ints past the device table, one per stream that has
+    // called cnf_nll on this plan (host-side assignment, so concurrent calls on different streams
+    // never share a counter and a call inside graph capture needs no allocation)
+    static constexpr int NLL_SLOTS = 64;
+    std::vector<void*> nll_streams;
+    std::shared_ptr<std::mutex> nll_mu = std::make_shared<std::mutex>();
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;
 };

@@ -629,8 +629,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     const bool alt = c.use_lds && (c.index & 1) != 0;
     float* so0 = E.at<float>(alt ? L.so_alt[0] : L.so[0]);
     float* so1 = E.at<float>(alt ? L.so_alt[1] : L.so[1]);
-    if ((pend != nullptr || defer) && (!c.use_lds || dir <= 0))
-        throw std::logic_error("deferred couplings are only fused into forward k_net_lds layers");
+    if ((pend != nullptr || defer) && !c.use_lds)
+        throw std::logic_error("deferred couplings are only fused into k_net_lds layers");
+    if (pend != nullptr && pend->dir != dir) throw std::logic_error("deferred coupling of the other direction");
     const float* tap_c[2] = {nullptr, nullptr};   // streamed tap-GEMM conv_out (finished in k_coupling)
     const float* tap_b[2] = {nullptr, nullptr};
     NetLdsArgs na;
@@ -935,6 +936,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         q.dc1 = c.dc1;
         q.W = c.W;
         q.D = c.D;
+        q.dir = dir;
         return;
     }
     {
@@ -974,8 +976,8 @@ static void ensure_tables(Plan& p) {
     // uploading is not capturable: the first call on a device must run eagerly
     if (hipStreamIsCapturing(nullptr, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
         throw std::runtime_error("plan tables not uploaded yet (call cnf_pack_params before graph capture)");
-    // one int past the table: cnf_nll's completion counter (zero between launches)
-    size_t nb = (p.host_table.size() + 1) * sizeof(int);
+    // NLL_SLOTS ints past the table: cnf_nll's completion counters (zero between launches)
+    size_t nb = (p.host_table.size() + Plan::NLL_SLOTS) * sizeof(int);
     hip_check(hipMalloc(&p.dev_table, nb), "hipMalloc(table)");
     hip_check(hipMemset(p.dev_table, 0, nb), "hipMemset(table)");
     if (!p.host_table.empty())
@@ -1182,6 +1184,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             mk.src = src, mk.dst = nxt, mk.sidx = ks, mk.n = nnext, mk.ss = ncur, mk.ds = nnext;
             mf.src = src, mf.dst = zy, mf.sidx = fs, mf.didx = fo, mf.n = nfac, mf.ss = ncur, mf.ds = nuv;
             const CoupPend q = have_pend ? pend : CoupPend{};
+            mk.pend = mf.pend = q.on;
             if (!p.dry && q.on && (nxt == q.u || zy == q.u)) throw std::logic_error("k_map2 would overwrite the u_k it reads");
             have_pend = false;
             E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
@@ -1198,6 +1201,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
         LdReduce r;
         r.part = ld, r.out = logdet_per_image, r.nl = (int)p.couplings.size(), r.np = L.ld_parts, r.accumulate = 0;
         const CoupPend q = have_pend ? pend : CoupPend{};
+        mf.pend = q.on;
         if (have_pend) r.nl -= 1;   // the pending layer is the last one: its log-det sum goes straight into the total
         E.record("k_map2", 0, 8.0 * B * p.last_n, [=](void* st) { launch_map2(mf, MapOp{}, r, q, B, (hipStream_t)st); });
     }
@@ -1284,7 +1288,7 @@ int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, cons
     if (xy == zy) return fail(CNF_E_INVALID, "zy and xy must not alias (out-of-place only)");
     CNF_TRY
     Plan& p = *plan->p;
-    ensure_tables(p);
+    if (!p.dry) ensure_tables(p);
     p.recorded.clear();
     Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
     const WsLayout& L = E.L;
@@ -1299,45 +1303,72 @@ int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, cons
         E.record("k_map_gather", 0, 8.0 * B * n,
                  [=](void* st) { launch_map_gather(zy, dst, T + off, n, nuv, n, B, (hipStream_t)st); });
     }
-    float* cur = buf[which];
+    const float* cur = buf[which];
     which ^= 1;
+    // the first layer that launches anything (squeezes are folded into the boundary maps): the layer
+    // the inverse ends with writes xy itself
+    int first = 0;
+    while (first < (int)p.layers.size() && p.layers[first].kind == CNF_LAYER_SQUEEZE) first++;
+    // deferred inverse law (as the forward's, CoupPend::dir = -1): an LDS layer whose successor in
+    // the inverse order (the previous layer by index) launches k_net_lds or the boundary maps leaves
+    // its law to that kernel — no k_coupling launch for it
+    static const bool fuse = [] {   // A/B knob (shared with the forward)
+        const char* e = std::getenv("CNF_FUSE_COUPLING");
+        return !(e && std::atoi(e) == 0);
+    }();
+    CoupPend pend;
+    bool have_pend = false;
     int bi = (int)p.boundaries.size() - 1;
     for (int li = (int)p.layers.size() - 1; li >= 0; li--) {
         const Layer& ly = p.layers[li];
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
-            float* nxt = buf[which];
-            run_coupling(E, c, cur, nxt, nullptr, -1);
+            int nx = li - 1;
+            while (nx >= 0 && p.layers[nx].kind == CNF_LAYER_SQUEEZE) nx--;
+            const bool next_lds = nx >= 0 && p.layers[nx].kind == CNF_LAYER_COUPLING &&
+                                  p.couplings[p.layers[nx].ci].use_lds;
+            const bool next_maps = nx >= 0 && p.layers[nx].kind == CNF_LAYER_FACTOR;
+            const bool defer = fuse && c.use_lds && (next_lds || next_maps);
+            float* nxt = li == first ? xy : buf[which];
+            CoupPend next;
+            run_coupling(E, c, cur, nxt, nullptr, -1, have_pend ? &pend : nullptr, defer, &next);
+            pend = next;
+            have_pend = defer;
             cur = nxt;
             which ^= 1;
         } else if (ly.kind == CNF_LAYER_FACTOR) {
             // factor.backward (:294-329) + squeeze.backward (:191-217): rebuild the previous block
-            // layout from the kept part (cur) and the factored part (read from zy at xy positions).
+            // layout from the kept part (cur) and the factored part (read from zy at xy positions), one
+            // k_map2 launch. With a pending coupling the kept part is read through it from u_k (the
+            // other buffer), and v_k's own buffer (cur, never written) takes the result.
             const Boundary& b = p.boundaries[bi--];
-            float* prev = buf[which];
-            const float* src = cur;
+            const bool last = li == first;
+            float* prev = last ? xy : have_pend ? const_cast<float*>(cur) : buf[which];
+            const bool flip = !have_pend;
             const int ncur = b.n_cur, nnext = b.n_next, nfac = b.n_fac;
-            const int* ks = T + b.dev_keep_src;
-            const int* fs = T + b.dev_fac_src;
-            const int* fo = T + b.dev_fac_orig;
-            E.record("k_map_scatter", 0, 8.0 * B * nnext, [=](void* st) {
-                launch_map_scatter(src, prev, nullptr, ks, nnext, nnext, ncur, B, (hipStream_t)st);
-            });
-            E.record("k_map_scatter", 0, 8.0 * B * nfac, [=](void* st) {
-                launch_map_scatter(zy, prev, fo, fs, nfac, nuv, ncur, B, (hipStream_t)st);
-            });
+            MapOp mk, mf;
+            mk.src = cur, mk.dst = prev, mk.didx = T + b.dev_keep_src, mk.n = nnext, mk.ss = nnext, mk.ds = ncur;
+            mf.src = zy, mf.dst = prev, mf.sidx = T + b.dev_fac_orig, mf.didx = T + b.dev_fac_src, mf.n = nfac;
+            mf.ss = nuv, mf.ds = ncur;
+            const CoupPend q = have_pend ? pend : CoupPend{};
+            mk.pend = q.on;
+            if (!p.dry && q.on && prev == q.u) throw std::logic_error("k_map2 would overwrite the u_k it reads");
+            have_pend = false;
+            E.record("k_map2", 0, 8.0 * B * (nnext + nfac),
+                     [=](void* st) { launch_map2(mk, mf, LdReduce{}, q, B, (hipStream_t)st); });
             cur = prev;
-            which ^= 1;
+            if (flip) which ^= 1;
         }
     }
-    {
+    if (have_pend) throw std::logic_error("inverse: a deferred coupling was left pending");
+    if (cur != xy) {   // (a schedule ending in a layout layer the maps did not cover)
         const float* src = cur;
         const size_t bytes = (size_t)B * nuv * 4;
         E.record("copy", 0, 2.0 * bytes, [=](void* st) {
             (void)hipMemcpyAsync(xy, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)st);
         });
     }
-    check_launch();
+    if (!p.dry) check_launch();
     return CNF_OK;
     CNF_CATCH
 }
@@ -1413,7 +1444,19 @@ int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float*
     Plan& p = *plan->p;
     ensure_tables(p);
     const cnf_flow_desc& d = p.desc;
-    unsigned* done = reinterpret_cast<unsigned*>(p.dev_table + p.host_table.size());
+    int slot = -1;
+    {
+        std::lock_guard<std::mutex> lk(*p.nll_mu);
+        for (size_t i = 0; i < p.nll_streams.size(); i++)
+            if (p.nll_streams[i] == stream) slot = (int)i;
+        if (slot < 0) {
+            if ((int)p.nll_streams.size() == Plan::NLL_SLOTS)
+                throw std::runtime_error("cnf_nll: more than 64 streams on one plan");
+            p.nll_streams.push_back(stream);
+            slot = (int)p.nll_streams.size() - 1;
+        }
+    }
+    unsigned* done = reinterpret_cast<unsigned*>(p.dev_table + p.host_table.size()) + slot;
     launch_nll(xy, zy, logdet_per_image, per_image, sums, done, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y,
                (hipStream_t)stream);
     check_launch();

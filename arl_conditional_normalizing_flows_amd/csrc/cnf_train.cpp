@@ -254,7 +254,7 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
     a.B = E.B;
     const int64_t* map = E.p.dev_bw_map;
     const long long nw = (long long)pc.taps * cin * cout;
-    if (train_valu_kernels()) {
+    if (train_valu_kernels() || !wgrad_band_ok(h, w, pc.taps, dil, cin, cout)) {
         a.chunks = wgrad_chunks(E.B, h * w);
         const long long total = (long long)E.B * h * w;
         a.chunk_px = (int)(((total + a.chunks - 1) / a.chunks + 15) / 16 * 16);
@@ -290,6 +290,10 @@ void ensure_side(Plan& p) {
         (void)hipStreamDestroy(p.side);
         for (hipStream_t& s : p.wside) (void)hipStreamDestroy(s);
         p.side = nullptr;
+        // the pooled events belong to the old device too: recording them on the new device's streams fails
+        for (hipEvent_t e : p.tev) (void)hipEventDestroy(e);
+        p.tev.clear();
+        p.tev_next = 0;
     }
     hchk(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking), "hipStreamCreate");
     hchk(hipEventCreateWithFlags(&p.ev_fork, hipEventDisableTiming), "hipEventCreate");
@@ -315,7 +319,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     const float* P = E.params;
     ensure_side(E.p);
     E.p.tev_next = 0;   // every event of the previous coupling has been waited for (the join below)
-    static const bool wstreams = [] {   // A/B knob: weight gradients on the chain streams
+    const bool wstreams = [] {   // A/B knob: weight gradients on the chain streams (read per call: tests switch it)
         const char* e = std::getenv("CNF_TRAIN_WSTREAM");
         return !(e && std::atoi(e) == 0);
     }();

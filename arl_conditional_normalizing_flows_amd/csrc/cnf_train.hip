@@ -379,12 +379,9 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
     }
 }
 
-static bool train_valu() {
-    static const bool v = [] {   // A/B knob: the register-blocked VALU kernels
-        const char* e = std::getenv("CNF_TRAIN_VALU");
-        return e && std::atoi(e) != 0;
-    }();
-    return v;
+static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (read per call: tests switch it)
+    const char* e = std::getenv("CNF_TRAIN_VALU");
+    return e && std::atoi(e) != 0;
 }
 bool train_valu_kernels() { return train_valu(); }
 
@@ -526,93 +523,6 @@ __global__ __launch_bounds__(256) void k_wgrad(WGradArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_wgrad_mfma: the same weight gradient on v_mfma_f32_16x16x4_f32, a (ci, co) = 64 x 64 tile per
-// workgroup, K = the chunk's pixels. Each 32-pixel step stages X (LN-on-load, shifted by the tap)
-// and dY into LDS (the next step's values are loaded into registers behind this step's MFMAs);
-// wave w owns ci rows 16w.. of the tile: lane (i16, kq) feeds X[px 4s+kq][ci 16w+i16] and
-// dY[px 4s+kq][co 16m+i16], so acc[m][r] = dW[ci 16w+4kq+r][co 16m+i16].
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_wgrad_mfma(WGradArgs a) {
-    constexpr int SP = 32, XS = 80, NE = SP * 64 / 256;   // row stride 80: conflict-free half-wave reads
-    __shared__ __attribute__((aligned(16))) float Xs[SP * XS];
-    __shared__ __attribute__((aligned(16))) float Ds[SP * XS];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i16 = lane & 15, kq = lane >> 4;
-    const int npx = a.H * a.W;
-    const long long total = (long long)a.B * npx;
-    const int tap = blockIdx.y;
-    const int nco = (a.CO + 63) / 64;
-    const int ci0 = (blockIdx.z / nco) * 64, co0 = (blockIdx.z % nco) * 64;
-    const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
-    const long long g0 = (long long)blockIdx.x * a.chunk_px;
-    const long long g1 = g0 + a.chunk_px < total ? g0 + a.chunk_px : total;
-    const bool do_bias = a.bpart != nullptr && tap == 0 && ci0 == 0;
-    f4 acc[4];
-#pragma unroll
-    for (int m = 0; m < 4; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
-    float bacc = 0.f;
-    float xv[NE], dv[NE];
-    auto load = [&](long long gs) {
-#pragma unroll
-        for (int u = 0; u < NE; u++) {
-            const int e = t + 256 * u;
-            const int c = e & 63, px = e >> 6;
-            const long long g = gs + px;
-            float x = 0.f, d = 0.f;
-            if (g < g1) {
-                const int b = (int)(g / npx), p = (int)(g - (long long)b * npx);
-                if (co0 + c < a.CO) d = a.dy[((size_t)b * npx + p) * a.dy_cs + a.dy_off + co0 + c];
-                if (ci0 + c < a.CI) {
-                    const int r = p / a.W + a.dil * dr, cc = p % a.W + a.dil * dc;
-                    if (r >= 0 && r < a.H && cc >= 0 && cc < a.W) {
-                        const size_t q = (size_t)r * a.W + cc;
-                        const size_t gi = q * a.x_cs + a.x_off + ci0 + c;
-                        x = act_load(a.x[(size_t)b * npx * a.x_cs + gi], a.act, a.stats, a.gamma, a.beta, b, gi);
-                    }
-                }
-            }
-            xv[u] = x;
-            dv[u] = d;
-        }
-    };
-    load(g0);
-    for (long long gs = g0; gs < g1; gs += SP) {
-        __syncthreads();   // the previous step's LDS reads are done
-#pragma unroll
-        for (int u = 0; u < NE; u++) {
-            const int e = t + 256 * u;
-            Xs[(e >> 6) * XS + (e & 63)] = xv[u];
-            Ds[(e >> 6) * XS + (e & 63)] = dv[u];
-        }
-        __syncthreads();
-        if (gs + SP < g1) load(gs + SP);   // in flight during this step's MFMAs
-#pragma unroll
-        for (int s = 0; s < SP / 4; s++) {
-            const int px = 4 * s + kq;
-            const float av = Xs[px * XS + 16 * wave + i16];
-#pragma unroll
-            for (int m = 0; m < 4; m++)
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Ds[px * XS + 16 * m + i16], acc[m], 0, 0, 0);
-        }
-        if (do_bias && t < 64) {
-#pragma unroll
-            for (int px = 0; px < SP; px++) bacc += Ds[px * XS + t];
-        }
-    }
-    float* part = a.part + (size_t)blockIdx.x * a.taps * a.CI * a.CO;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int ci = ci0 + 16 * wave + 4 * kq + r;
-        if (ci >= a.CI) continue;
-#pragma unroll
-        for (int m = 0; m < 4; m++) {
-            const int co = co0 + 16 * m + i16;
-            if (co < a.CO) part[((size_t)tap * a.CI + ci) * a.CO + co] = acc[m][r];
-        }
-    }
-    if (do_bias && t < 64 && co0 + t < a.CO) a.bpart[(size_t)blockIdx.x * a.CO + co0 + t] = bacc;
-}
-
-// ------------------------------------------------------------------------------------------------
 // k_wgrad_band: weight gradient of a 3x3 (TR = 3) or 1x1 (TR = 1) conv on MFMA with every tap of
 // one kernel row per workgroup. Work units are (image, band of RB rows); a workgroup of grid
 // column `chunk` takes units chunk, chunk + chunks, ... For each unit it stages the X rows its
@@ -656,7 +566,10 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
     float bacc = 0.f;
     const int bands = (H + RB - 1) / RB;
     const bool ln = a.stats != nullptr;
-    const bool qx = (CIB & 3) == 0 && (a.x_cs & 3) == 0 && ((a.x_off + ci0) & 3) == 0;
+    // quad loads of X need the window quad aligned, and (with LN) 16-byte aligned gamma / beta: they are
+    // canonical-parameter pointers (P + offset) with no alignment guarantee of their own
+    const bool qx = (CIB & 3) == 0 && (a.x_cs & 3) == 0 && ((a.x_off + ci0) & 3) == 0 &&
+                    (!ln || ((((uintptr_t)a.gamma) | ((uintptr_t)a.beta)) & 15) == 0);
     const bool qd = (COB & 3) == 0 && (a.dy_cs & 3) == 0 && ((a.dy_off + co0) & 3) == 0;
     for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         const int b = unit / bands, r0 = (unit - b * bands) * RB;
@@ -907,8 +820,12 @@ static int wg_abl() {   // diagnostics: CNF_WG_ABL bit 0 skips the X/dY staging,
     return v;
 }
 
+bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO) {
+    return (taps == 1 || taps == 9) && W >= 4 && wgrad_band_lds(H, W, taps, dil, CI, CO) <= 160 * 1024;
+}
+
 void launch_wgrad(const WGradArgs& a, hipStream_t st) {
-    if (train_valu()) {
+    if (a.chunk_px > 0) {   // k_wgrad, the VALU kernel: the caller chose it (CNF_TRAIN_VALU, or !wgrad_band_ok)
         const dim3 g(a.chunks, a.taps, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
         hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);
         return;

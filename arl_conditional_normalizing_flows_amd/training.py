@@ -200,8 +200,10 @@ def _agree_stop(model, process_group):
 def _agreed_batches(model, data, process_group, what):
     """The epoch's batches; data-parallel, every rank must run the same number of them (each
     train_step / test_step is a collective: a rank with more batches would block forever in its
-    extra all-reduce), so the counts are compared once per epoch (one all-reduce of two ints) and
-    a mismatch raises on every rank instead of hanging."""
+    extra all-reduce). A source with len() is checked once per epoch (one all-reduce of two ints);
+    any other source (a generator making a device tensor per batch) is streamed one batch at a time
+    with a 'have another batch' flag all-reduced before each step, so the epoch is never held in
+    memory at once. Either way a mismatch raises on every rank instead of hanging."""
     batches = _batches(data)
     if process_group is None:
         return batches
@@ -209,18 +211,40 @@ def _agreed_batches(model, data, process_group, what):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return batches
-    batches = list(batches)
     grp = None if process_group is True else process_group
     dev = getattr(model, 'device', None)
     if dist.get_backend(grp) == 'gloo' or dev is None:
         dev = torch.device('cpu')
-    n = torch.tensor([len(batches), -len(batches)], dtype=torch.int64, device=dev)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=grp)
-    hi, lo = int(n[0]), -int(n[1])
-    if hi != lo:
-        raise ValueError(f'data-parallel fit: ranks hold {lo}..{hi} {what} batches this epoch; every shard '
-                         f'must have the same number of batches')
-    return batches
+
+    def agree(k):
+        n = torch.tensor([k, -k], dtype=torch.int64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX, group=grp)
+        return int(n[0]), -int(n[1])
+
+    def mismatch(lo, hi):
+        return ValueError(f'data-parallel fit: ranks hold {lo}..{hi} {what} batches this epoch; every shard '
+                          f'must have the same number of batches')
+
+    if hasattr(batches, '__len__'):
+        hi, lo = agree(len(batches))
+        if hi != lo:
+            raise mismatch(lo, hi)
+        return batches
+
+    def stream():
+        it = iter(batches)
+        done = object()
+        count = 0
+        while True:
+            xy = next(it, done)
+            hi, lo = agree(0 if xy is done else 1)
+            if hi != lo:
+                raise mismatch(count, count + 1)
+            if xy is done:
+                return
+            count += 1
+            yield xy
+    return stream()
 
 
 def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Optional[List[Callback]] = None,

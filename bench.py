@@ -271,6 +271,36 @@ def cpu_baseline(cfg, flow, xy_np, B, budget_s=20.0):
             'bits_per_dim_ref': loss64 / (math.log(2) * H * Wd * cfg.x_d)}
 
 
+def cpu_baseline_inverse(cfg, flow, zy_np, B, budget_s=20.0):
+    """The torch-CPU fp32 restatement's inverse (oracle/cflow_torch_cpu.py TorchCPUFlow.inverse,
+    conv_cINN_make_model.py:1774-1798) on the bench's zy batch and weights, whole batches of B for
+    about budget_s, median per batch (rank 0, N=1 only)."""
+    try:
+        from oracle.cflow_torch_cpu import TorchCPUFlow
+    except Exception as e:  # pragma: no cover
+        return {'value': None, 'unit': 'images/s', 'cores': 0, 'kind': 'port', 'sample': f'unavailable: {e}'}
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    tf = TorchCPUFlow(**cfg.kwargs())
+    P32 = {k: torch.from_numpy(np.ascontiguousarray(v, np.float32)) for k, v in flow.get_weights().items()}
+    zy = torch.from_numpy(np.ascontiguousarray(zy_np, np.float32))
+    times = []
+    with torch.no_grad():
+        tf.inverse(zy, P32)           # warm-up
+        t_all = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            tf.inverse(zy, P32)
+            times.append(time.perf_counter() - t0)
+            if time.perf_counter() - t_all > budget_s and len(times) >= 3:
+                break
+    med = float(np.median(times))
+    return {'value': round(B / med, 3), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{len(times)} batches of {B} images of {cfg.name} inverse (the bench zy and weights), '
+                      f'median {med * 1e3:.1f} ms/batch over {sum(times):.1f}s, torch-CPU fp32 restatement '
+                      f'(oracle/cflow_torch_cpu.py), {threads} threads'}
+
+
 def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
     """images/s of cFlow.train_step (conv_cINN_make_model.py:1850-1880) on the bench batch: every
     step = cnf_flow_forward_train + cnf_nll + the 5-float loss all-reduce + cnf_flow_backward + the
@@ -325,10 +355,12 @@ def main():
     ap.add_argument('--global-batch', type=int, default=0,
                     help='strong scaling: shard this many images over the ranks (default: weak scaling, '
                          'the per-GPU batch on every rank)')
-    ap.add_argument('--mode', choices=['forward', 'train'], default='forward',
+    ap.add_argument('--mode', choices=['forward', 'inverse', 'train'], default='forward',
                     help='train: the NLL training step (cFlow.train_step: forward with saved layer inputs, '
                          'backward, gradient all-reduce when N>1, Keras Adam, weight repack) instead of the '
-                         'fwd+logdet metric step; prints its own JSON line')
+                         'fwd+logdet metric step; prints its own JSON line. inverse: sampling, '
+                         'cFlow.call(zy, -1) (conv_cINN_make_model.py:1774-1798) on the forward\'s zy of the '
+                         'bench batch (no collective: the inverse has no cross-image term)')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -381,8 +413,19 @@ def main():
     ws = flow._workspace(B)
     lib = _lib.load()
 
+    inverse = args.mode == 'inverse'
+    if inverse:
+        # sampling input: the forward's zy of the bench batch (a valid latent of this flow)
+        zy_in, _ = flow(xy, 1)
+        x_out = torch.empty_like(xy)
+        torch.cuda.synchronize()
+
     def local_step():
         st = torch.cuda.current_stream().cuda_stream
+        if inverse:
+            _lib.check(lib.cnf_flow_inverse(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
+                                            zy_in.data_ptr(), x_out.data_ptr(), ws.data_ptr(), B, st), 'inverse')
+            return
         _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(), xy.data_ptr(),
                                         zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
         _lib.check(lib.cnf_nll(flow._plan, xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
@@ -390,8 +433,8 @@ def main():
 
     def exchange():
         # the path's one exchange step, issued eagerly after the (graph-replayed) local work: RCCL
-        # collectives are never captured into the graph
-        if dist is not None:
+        # collectives are never captured into the graph (the inverse has none)
+        if dist is not None and not inverse:
             pack_nll_sums(sums, B, red)
             dist.all_reduce(red)
 
@@ -454,8 +497,9 @@ def main():
     value = total_imgs / el
 
     # results of the timed steps
-    ld_mean = ld.mean().item()
-    loss_mean = (red[0] / red[4]).item() if dist is not None else sums[0].item() / B
+    ld_mean = ld.mean().item() if not inverse else None
+    loss_mean = ((red[0] / red[4]).item() if dist is not None else sums[0].item() / B) if not inverse else None
+    rt_err = ((x_out - xy).abs().max() / xy.abs().max()).item() if inverse else None
     out = None
     if rank == 0:
         # per-step times for the median (BASELINE.md protocol): local work only, rank 0
@@ -490,19 +534,26 @@ def main():
                      'achieved_gbs': round(by_img * B / (step_ms / 1e3) / 1e9, 1)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, flow, xy_np, B)
+            cpu = (cpu_baseline_inverse(cfg, flow, zy_in.cpu().numpy(), B) if inverse
+                   else cpu_baseline(cfg, flow, xy_np, B))
         H, W, _ = cfg.io_shape
-        bpd = float(loss_mean / (np.log(2) * H * W * cfg.x_d))
+        bpd = float(loss_mean / (np.log(2) * H * W * cfg.x_d)) if not inverse else None
+        if inverse:
+            metric = f'images/sec inverse (sampling, zy -> xy), {args.config}'
+        elif args.config == 'cfg2':
+            metric = 'images/sec fwd+logdet, 32x32x3 3-scale flow @1/2/4/8 GPU; bits/dim vs ref'
+        else:
+            metric = f'images/sec fwd+logdet ({args.config})'
         out = {
-            'metric': 'images/sec fwd+logdet, 32x32x3 3-scale flow @1/2/4/8 GPU; bits/dim vs ref'
-            if args.config == 'cfg2' else f'images/sec fwd+logdet ({args.config})',
+            'metric': metric,
             'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 4), 'higher_is_better': True, 'scaling': scaling,
             'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded class-conditional batch, 2% noise), '
                                                         'seeded orthogonal-init weights'
             if cfg.data == 'class' else 'synthetic (seeded SR batch: residual x, down/up y, 2% noise), '
                                         'seeded orthogonal-init weights',
-            'config': {'workload': f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, '
+            'config': {'workload': (f'{cfg.name}: cFlow.call(zy,-1), zy {list(cfg.io_shape)}, ' if inverse else
+                                    f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, ')
                                    + (f'{G} images global over {world} GPUs' if scaling == 'strong'
                                       else f'{B} images per GPU'),
                        'model': f'cFlow {cfg.name}', 'global_batch': G,
@@ -510,8 +561,9 @@ def main():
                                                                           f'1 all-reduce of 5 fp32)',
                        'graph': graph is not None},
             'step_ms_median': round(float(np.median(st_ms)), 4) if st_ms else None,
-            'bits_per_dim': round(bpd, 6),
+            'bits_per_dim': round(bpd, 6) if bpd is not None else None,
             'logdet_mean': ld_mean,
+            'roundtrip_rel_err': rt_err,
             'roofline': roof,
             'step_roofline': step_roof,
             'cpu_baseline': cpu,

@@ -146,8 +146,10 @@ int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out
  * sums[4] = (sum_i loss_i, sum_i -llz_i, sum_i -lly_i, sum_i -logdet_i),
  * loss_i = -(llz_i + lly_i + logdet_i). Dividing sums by the (global) batch
  * gives the reference's (loss, z_loss, y_loss, detJ_loss). One kernel launch;
- * it uses a completion counter owned by the plan, so calls on one plan must not
- * run concurrently on different streams (a plan is single-stream anyway). */
+ * its last workgroup is found through a completion counter the plan keeps per
+ * stream (up to 64 streams per plan), so calls on different streams may run
+ * concurrently. The first call on a plan uploads its tables (not capturable:
+ * cnf_pack_params does the same, call it before graph capture). */
 int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image,
             float* per_image, float* sums, int B, void* stream);
 

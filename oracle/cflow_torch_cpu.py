@@ -181,6 +181,34 @@ class TorchCPUFlow:
                 zy = _d2s(zy) if zy is not None else None
         return vu, ld
 
+    def inverse(self, zy_in, P):
+        """cFlow.call(zy, -1) (conv_cINN_make_model.py:1774-1798): the squeeze / factor layers'
+        forward rebuilds the last block's layout from zy (:1782-1788), then every layer's backward
+        in reverse order (:1793-1796; coupling inverse law :1235-1253, :1333-1394)."""
+        uv, zy = zy_in, None
+        for e in self.sf:
+            if e.kind == 'squeeze':
+                uv = _s2d(uv)
+                zy = _s2d(zy) if zy is not None else None
+            else:
+                split = uv.shape[3] // 2
+                f = uv[..., :split]
+                uv = uv[..., split:]
+                zy = torch.cat([zy, f], 3) if zy is not None else f
+        vu = uv
+        for e in reversed(self.layers):
+            if e.kind == 'coupling':
+                vu, _ = self._coupling(vu, e.coupling, P, -1)
+            elif e.kind == 'squeeze':
+                vu = _d2s(vu)
+                zy = _d2s(zy) if zy is not None else None
+            else:
+                split = zy.shape[3] // (2 ** e.num_prev_factors) if vu is None else vu.shape[3]
+                re = zy[..., zy.shape[3] - split:]
+                zy = zy[..., :zy.shape[3] - split]
+                vu = torch.cat([re, vu], 3)
+        return vu
+
     def log_loss(self, xy, P):
         x_d = self.x_d
         zy, ld = self.forward(xy, P)

@@ -111,7 +111,7 @@ class ToyCINN:
                 P[n] = rng.normal(0.0, bias_std, s)
         return P
 
-    def coupling(self, u, P, j, direction):
+    def coupling(self, u, P, j, direction, with_abs=False):
         t = j % 6
         i1, i2 = MASK_U1[t], MASK_U2[t]
         u1, u2 = u[:, i1], u[:, i2]
@@ -120,19 +120,27 @@ class ToyCINN:
         v = u.copy()
         if direction == -1:
             v[:, i2] = np.exp(A) * u2 + b
+            if with_abs:
+                return v, A.sum(axis=1), np.abs(A).sum(axis=1)
             return v, A.sum(axis=1)
         v[:, i2] = (u2 - b) / np.exp(A)
-        return v, None
+        return (v, None, None) if with_abs else (v, None)
 
-    def call(self, u, P, direction=-1):
-        """(:237-417) returns (v, log_detJ[B]) for direction -1 and (v, None) for +1."""
+    def call(self, u, P, direction=-1, abs_s=False):
+        """(:237-417) returns (v, log_detJ[B]) for direction -1 and (v, None) for +1. abs_s=True
+        (direction -1) also returns the per-sample sum over layers of |A| (the log-det's
+        conditioning scale, the Sum|s| of the north-star bound)."""
         u = np.asarray(u, np.float64)
         P = {k: np.asarray(v, np.float64) for k, v in P.items()}
         ld = np.zeros(u.shape[0])
+        sa = np.zeros(u.shape[0])
         for i in list(range(self.L))[::direction]:
-            u, d = self.coupling(u, P, self.mask_indices[i], direction)
+            u, d, a = self.coupling(u, P, self.mask_indices[i], direction, with_abs=True)
             if d is not None:
                 ld = ld + d
+                sa = sa + a
+        if abs_s:
+            return u, (ld if direction == -1 else None), (sa if direction == -1 else None)
         return u, (ld if direction == -1 else None)
 
     def log_loss(self, xy, P):

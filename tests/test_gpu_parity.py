@@ -20,22 +20,27 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 
+# plan-time knobs of the streamed path's fallback kernels: 'nogc' = no fused k_gc stage (CNF_GC=0: the
+# grouped branches run as k_pw tap-mode launches over their im2col rows); 'conv1' = no k_pw (CNF_PW=0:
+# the per-tile k_conv1 / k_conv<3> kernels, and conv_out as the one-kernel k_convtap, CNF_TAP_PW=0)
+KNOBS = {'nogc': {'CNF_NETLDS': '0', 'CNF_GC': '0'},
+         'conv1': {'CNF_NETLDS': '0', 'CNF_PW': '0', 'CNF_TAP_PW': '0'}}
+
+
 def _setup(name, B, group_mode='reference', seed=0, netlds=True):
-    """netlds: True / False (CNF_NETLDS), or 'nogc' = streamed layers without the fused k_gc stage
-    (CNF_GC=0: the grouped branches run as k_pw tap-mode launches over their im2col rows)"""
+    """netlds: True / False (CNF_NETLDS), or a KNOBS key (streamed layers with fallback kernels)"""
     import os
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
-    os.environ['CNF_NETLDS'] = '0' if netlds is False else '1'
-    if netlds == 'nogc':
-        os.environ['CNF_GC'] = '0'
+    env = KNOBS.get(netlds, {'CNF_NETLDS': '0' if netlds is False else '1'})
+    os.environ.update(env)
     cfg = PRESETS[name]
     kw = cfg.kwargs()
     kw['group_mode'] = group_mode
     try:
         flow = cFlow(**kw)
     finally:
-        os.environ.pop('CNF_NETLDS', None)
-        os.environ.pop('CNF_GC', None)
+        for k in env:
+            os.environ.pop(k, None)
     ora = OracleCFlow(**kw)
     P = ora.init_params(seed)
     flow.set_weights(P)
@@ -87,8 +92,12 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          ('ref_default', 2, 'reference', False),
          # streamed grouped branches as k_pw tap-mode launches (no fused k_gc)
          ('cfg2', 2, 'reference', 'nogc'),
+         # the per-tile fallback kernels (k_conv1, k_conv<3>, k_convtap) instead of k_pw / k_gc
+         ('small', 3, 'reference', 'conv1'), ('cfg2', 2, 'reference', 'conv1'),
          # BASELINE configs[3] / configs[4] architectures (64x64 4-scale, 128x128 5-scale) at a small batch
-         ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True)]
+         ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True),
+         # couplings 2 and 1 pixels wide (squeezed to 2x2 blocks)
+         ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False)]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
@@ -210,38 +219,56 @@ def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
             assert torch.allclose(ld, ld0, rtol=1e-6, atol=1e-5)
 
 
-def test_roundtrip_cfg2_full_batch(gpu):
-    """BASELINE configs[1] at its full batch (64): size-independent round-trip property."""
-    flow, ora, P, xy = _setup('cfg2', 64)
+# the batches the benches and the strong-scaling runs put on one GPU: cfg2 B=64 (headline), cfg4 at the
+# per-GPU shares of its global 256 over 8 / 2 GPUs (32, 128), cfg5 at its 512 over 8 (64)
+BENCH_BATCHES = [('cfg2', 64), ('cfg4', 32), ('cfg4', 128), ('cfg5', 64)]
+
+
+@pytest.mark.parametrize('name,B', BENCH_BATCHES)
+def test_roundtrip_bench_batches(gpu, name, B):
+    """Size-independent round-trip property at the benched per-GPU batches (the oracle cannot finish
+    cfg4/cfg5 at these sizes in seconds): inverse(forward(xy)) == xy within 1e-5 relative, finite
+    per-image log-det."""
+    flow, ora, P, xy = _setup(name, B)
     x = torch.from_numpy(xy).to(gpu)
     zy, ld = flow(x, 1, per_image_logdet=True)
     x2 = flow(zy, -1)
     torch.cuda.synchronize()
     e = (x2 - x).abs().max().item() / x.abs().max().item()
-    print(f'cfg2 B=64 round trip rel err {e:.3e}')
+    print(f'{name} B={B} round trip rel err {e:.3e}')
     assert e < RTOL
-    assert torch.isfinite(ld).all()
+    assert torch.isfinite(ld).all() and torch.isfinite(zy).all()
 
 
-@pytest.mark.parametrize('name,netlds', [('cfg2', True), ('cfg2', False), ('cfg3', True)])
-def test_ragged_large_batch_matches_small_batches(gpu, name, netlds):
+@pytest.mark.parametrize('name,netlds,B', [('cfg2', True, 67), ('cfg2', False, 67), ('cfg3', True, 67),
+                                           ('cfg4', True, 32), ('cfg4', True, 128), ('cfg5', True, 64)])
+def test_ragged_large_batch_matches_small_batches(gpu, name, netlds, B):
     """Every op is per image, so an image's result must not depend on the batch it rides in: a
-    ragged batch of 67 (the image-looping kernels' last workgroups get partial image sets) against
-    the same images in batches of 5, on the LDS and the streamed paths (tolerance: fp32 ordering
-    of the LN partial merges, 1e-6 relative)."""
+    large batch (67: the image-looping kernels' last workgroups get partial image sets; cfg4 / cfg5 at
+    their per-GPU strong-scaling shares, where the k_pw / k_gc workgroups loop over several images and
+    the polyphase band ring has batch-dependent tails) against the same images in batches of 5 (the
+    last one ragged), on the LDS and the streamed paths (tolerance: fp32 ordering of the LN partial
+    merges, 1e-6 relative), plus the inverse of the large batch against the small batches'."""
     flow, ora, P, _ = _setup(name, 2, netlds=netlds)
     cfg = PRESETS[name]
     H, W, _D = cfg.io_shape
-    xy = (synthetic_class_batch(67, H, W, cfg.x_d, seed=5) if cfg.data == 'class'
-          else synthetic_sr_batch(67, H, W, cfg.x_d, cfg.sr_pow, seed=5))
+    xy = (synthetic_class_batch(B, H, W, cfg.x_d, seed=5) if cfg.data == 'class'
+          else synthetic_sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=5))
     x = torch.from_numpy(xy).to(gpu)
     zy, ld = flow(x, 1, per_image_logdet=True)
-    for s in range(0, 67, 5):
+    xi = flow(zy, -1)
+    worst = 0.0
+    for s in range(0, B, 5):
         zs, ls = flow(x[s:s + 5], 1, per_image_logdet=True)
         e = (zs - zy[s:s + 5]).abs().max().item() / zy[s:s + 5].abs().max().item()
         assert e < 1e-6, (s, e)
         assert torch.allclose(ls, ld[s:s + 5], rtol=1e-6, atol=1e-4)
+        xs = flow(zy[s:s + 5], -1)
+        ei = (xs - xi[s:s + 5]).abs().max().item() / xi[s:s + 5].abs().max().item()
+        assert ei < 1e-6, (s, ei)
+        worst = max(worst, e, ei)
     torch.cuda.synchronize()
+    print(f'{name} B={B} lds={netlds}: worst batch-of-5 vs batch-of-{B} rel diff {worst:.2e}')
 
 
 def test_nll_matches_oracle(gpu):

@@ -187,3 +187,35 @@ def test_torch_cpu_float64_is_the_numpy_oracle():
         assert np.allclose(st[0].numpy(), lr, rtol=0, atol=1e-10)
         assert np.allclose(st[1].numpy(), ar, rtol=0, atol=1e-10)
         assert np.all(ar >= np.abs(lr))
+
+
+@pytest.mark.parametrize('B,H,W,x_d,seed', [(3, 8, 8, 1, 0), (5, 32, 32, 3, 7)])
+def test_product_synthetic_batches_equal_the_oracle_generators(B, H, W, x_d, seed):
+    """bench.py draws its inputs from the package's synthetic.py (the product never imports oracle/);
+    the parity tests draw theirs from oracle/cflow_np.py. Same seeds, same bytes: the benched
+    batches are exactly the distribution the parity tests cover."""
+    from arl_conditional_normalizing_flows_amd import synthetic
+    from oracle.cflow_np import synthetic_class_batch, synthetic_sr_batch
+    assert np.array_equal(synthetic.class_batch(B, H, W, x_d, seed=seed), synthetic_class_batch(B, H, W, x_d, seed=seed))
+    for p in (1, 2, 3):
+        assert np.array_equal(synthetic.sr_batch(B, H, W, x_d, p, seed=seed), synthetic_sr_batch(B, H, W, x_d, p, seed=seed))
+
+
+@pytest.mark.parametrize('name', ['tiny', 'small', 'cfg2'])
+def test_torch_cpu_inverse_is_the_numpy_oracle(name):
+    """oracle/cflow_torch_cpu.TorchCPUFlow.inverse (the CPU baseline of bench.py --mode inverse and the
+    full-size inverse oracle) equals OracleCFlow.inverse in float64, and inverts the forward."""
+    import torch
+    from oracle.cflow_torch_cpu import TorchCPUFlow
+    from arl_conditional_normalizing_flows_amd.config import PRESETS
+    cfg = PRESETS[name]
+    kw = cfg.kwargs()
+    o, t = O.OracleCFlow(**kw), TorchCPUFlow(**kw)
+    P = o.init_params(0)
+    H, W, D = cfg.io_shape
+    xy = O.synthetic_class_batch(2, H, W, cfg.x_d, seed=1)
+    zy, _ = o.forward(xy, P)
+    x1 = o.inverse(zy, P)
+    x2 = t.inverse(torch.from_numpy(zy), {k: torch.from_numpy(np.asarray(v, np.float64)) for k, v in P.items()}).numpy()
+    assert np.max(np.abs(x1 - x2)) <= 1e-12
+    assert np.max(np.abs(x1 - xy)) <= 1e-12

@@ -143,12 +143,26 @@ def _gpu_flow(kw, P, gpu):
 
 
 GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'intended'}),
-              ('tiny', 2, {'LAYER_NORM': False}), ('cfg2', 2, {})]
+              ('tiny', 2, {'LAYER_NORM': False}), ('cfg2', 2, {}),
+              # couplings 2 and 1 pixels wide: the weight gradients fall back to the VALU k_wgrad
+              ('narrow', 3, {}),
+              # every training convolution on the VALU kernels (k_tconv, k_wgrad; CNF_TRAIN_VALU=1, read per call)
+              ('small', 3, {'_env': {'CNF_TRAIN_VALU': '1'}}),
+              # the benched training batch (bench.py --mode train): the batch-sliced LN backward (up to 8
+              # workgroups per image), the multi-unit band weight gradients and the four-stream schedule
+              # all see their full-size partitions only here
+              ('cfg2', 64, {})]
+# at the bench batch the float64 spread is sampled more sparsely (each float64 autograd pass of
+# cfg2 B=64 takes ~20 s on the box's 16 host threads)
+PERTURB_LARGE_B = ((1e-6, 4e-6), 1)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('name,B,extra', GRAD_CASES)
 def test_gradients_match_oracle(gpu, name, B, extra):
+    import os
+    extra = dict(extra)
+    env = extra.pop('_env', {})
     cfg = PRESETS[name]
     kw = dict(cfg.kwargs(), **extra)
     ora = OracleCFlow(**kw)
@@ -160,14 +174,20 @@ def test_gradients_match_oracle(gpu, name, B, extra):
     G_spread = {k: np.zeros(np.size(v)) for k, v in G_ref.items()}
     if name in PERTURB_CASES:
         rng = np.random.default_rng(11)
-        for eps in PERTURB:
-            for _ in range(PERTURB_SEEDS):
+        eps_list, seeds = (PERTURB, PERTURB_SEEDS) if B < 32 else PERTURB_LARGE_B
+        for eps in eps_list:
+            for _ in range(seeds):
                 Gp, _ = oracle_grads(kw, P, np.asarray(xy, np.float64) * (1.0 + eps * rng.standard_normal(xy.shape)))
                 for k in G_spread:
                     G_spread[k] = np.maximum(G_spread[k], np.abs(Gp[k].reshape(-1) - G_ref[k].reshape(-1)))
     flow = _gpu_flow(kw, P, gpu)
-    g, terms = flow.gradients(torch.from_numpy(xy).to(gpu))
-    g = g.cpu().numpy().astype(np.float64)
+    os.environ.update(env)
+    try:
+        g, terms = flow.gradients(torch.from_numpy(xy).to(gpu))
+        g = g.cpu().numpy().astype(np.float64)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
     terms = [float(t) for t in terms]
     for r, t in zip(terms_ref, terms):
         assert abs(r - t) <= 1e-5 * max(1.0, abs(r)) * 10, (terms_ref, terms)
@@ -187,6 +207,31 @@ def test_gradients_match_oracle(gpu, name, B, extra):
                        f'fp32 autograd err {np.max(np.abs(g32 - ref)):.3e})')
     print(f'{name} {extra} B={B}: worst gradient error / tolerance {worst[0]:.3f} ({worst[1]}), max|g| {gmax:.3e}')
     assert not bad, '\n'.join(bad)
+
+
+@pytest.mark.gpu
+def test_gradients_bitwise_reproducible_across_runs_and_streams(gpu):
+    """The training backward at the benched batch (cfg2 B=64) is atomic-free and every multi-stream
+    join is event-ordered with the u1 gradients added in a fixed order: two runs give the same
+    gradient bit for bit, and so does the single-stream schedule of the weight gradients
+    (CNF_TRAIN_WSTREAM=0, read per call) — a missing event or a wrong slice count would show here."""
+    import os
+    cfg = PRESETS['cfg2']
+    kw = cfg.kwargs()
+    P = OracleCFlow(**kw).init_params(5)
+    xy = torch.from_numpy(_batch(cfg, 64, 6)).to(gpu)
+    flow = _gpu_flow(kw, P, gpu)
+    g1 = flow.gradients(xy)[0].clone()
+    g2 = flow.gradients(xy)[0].clone()
+    os.environ['CNF_TRAIN_WSTREAM'] = '0'
+    try:
+        g3 = flow.gradients(xy)[0].clone()
+    finally:
+        os.environ.pop('CNF_TRAIN_WSTREAM', None)
+    torch.cuda.synchronize()
+    assert torch.isfinite(g1).all()
+    assert torch.equal(g1, g2)
+    assert torch.equal(g1, g3)
 
 
 @pytest.mark.gpu

@@ -182,7 +182,7 @@ def test_gloo_world2_fit_agrees_on_early_stop(tmp_path):
     assert os.path.exists(tmp_path / 'w0.e04.npz') and not any(p.name.startswith('w1') for p in tmp_path.iterdir())
 
 
-def _mismatch_worker(rank, world, port, out_dir):
+def _mismatch_worker(rank, world, port, out_dir, gen=False):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
@@ -190,8 +190,11 @@ def _mismatch_worker(rank, world, port, out_dir):
     try:
         stub = _DPStub([1.0] * 3)
         msg = ''
+        data = [0, 0, 0] if rank == 0 else [0, 0]
+        if gen:   # a generator source (no len): streamed, the epoch never materialised
+            data = (lambda d=data: (b for b in d))
         try:
-            T.fit(stub, [0, 0, 0] if rank == 0 else [0, 0], epochs=1, process_group=True)
+            T.fit(stub, data, epochs=1, process_group=True)
         except ValueError as e:
             msg = str(e)
         with open(os.path.join(out_dir, f'm{rank}.txt'), 'w') as f:
@@ -213,6 +216,22 @@ def test_gloo_world2_fit_rejects_unequal_shards(tmp_path):
     for r in (0, 1):
         steps, msg = (tmp_path / f'm{r}.txt').read_text().split('|', 1)
         assert steps == '0' and 'same number of batches' in msg
+
+
+def test_gloo_world2_fit_streams_generator_batches_and_rejects_unequal(tmp_path):
+    """A generator source (anneal_and_fit's noisy copies, pretrain_on_noise's renewed noise) is not
+    turned into a list: a 'have another batch' flag is agreed before each step, so ranks with 3 and 2
+    batches both run the 2 common steps and then both raise (never one blocked in an all-reduce)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_mismatch_worker, args=(2, port, str(tmp_path), True), nprocs=2, join=True)
+    for r in (0, 1):
+        steps, msg = (tmp_path / f'm{r}.txt').read_text().split('|', 1)
+        assert steps == '2' and 'same number of batches' in msg
 
 
 @pytest.mark.gpu
