@@ -9,7 +9,8 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / 'csrc'
-LIB = PKG / 'lib' / 'libcnf_hip.so'
+# CNF_BUILD_LIB: write a diagnostic build elsewhere (e.g. the host-sanitizer build, tools/host_sanitize.sh)
+LIB = Path(os.environ['CNF_BUILD_LIB']) if os.environ.get('CNF_BUILD_LIB') else PKG / 'lib' / 'libcnf_hip.so'
 SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
            'cnf_plan.cpp', 'cnf_train.cpp', 'cnf_comm.cpp']
 HEADERS = ["cnf_kernels.h", "cnf_device.h", "cnf_plan.h", "cnf_netlds_shapes.inc", "cnf_gc_shapes.inc", "cnf_pw_shapes.inc"]
@@ -85,7 +86,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         for f in [ex.submit(_compile, src, obj, verbose) for src, obj in jobs]:
             f.result()
     tmp = LIB.with_suffix('.so.tmp')
-    cmd = [_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(tmp)] + [str(o) for o in objs] + ['-ldl']
+    cmd = ([_hipcc(), f'--offload-arch={ARCH}', '-shared', '-fPIC', '-o', str(tmp)] + [str(o) for o in objs] + ['-ldl']
+           + os.environ.get('CNF_EXTRA_LDFLAGS', '').split())
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed ({r.returncode}):\n{r.stdout}\n{r.stderr}')

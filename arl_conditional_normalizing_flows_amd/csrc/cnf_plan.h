@@ -224,6 +224,7 @@ struct Plan {
     bool dry = false;         // host-only dry run: record launches without issuing them (shape dumps)
     std::vector<PwShape> pw_shapes;   // k_pw launch shapes seen by a dry run
     std::vector<GcShape> gc_launch;   // dry runs: the k_gc launch shapes (GcArgs::s) as run_coupling issues them
+    std::vector<std::string> dry_launches;   // dry runs: the launch names in issue order (cnf_debug_schedule)
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
     std::vector<Recorded> recorded;
@@ -247,6 +248,11 @@ struct Plan {
     std::shared_ptr<std::mutex> nll_mu = std::make_shared<std::mutex>();
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;
+    // device-table address of entry `off`; host-only dry runs carry no device tables, so they get a
+    // placeholder base (the address is recorded, never dereferenced, and never null + offset)
+    const int* dtab(int64_t off) const {
+        return (dry ? reinterpret_cast<const int*>(uintptr_t(1) << 40) : dev_table) + off;
+    }
 };
 
 // cnf_train.cpp: dL/dparams of the NLL (loss scaled by inv_batch = 1 / global batch) into dparams,

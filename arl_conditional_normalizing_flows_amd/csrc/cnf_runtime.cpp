@@ -186,7 +186,10 @@ struct Exec {
     }
 
     void record(const std::string& name, double flops, double bytes, std::function<void(void*)> fn) {
-        if (p.dry) return;
+        if (p.dry) {
+            p.dry_launches.push_back(name);
+            return;
+        }
         const size_t k = p.recorded.size();
         const bool timed = p.timing && p.record && name.rfind("k_", 0) == 0;   // kernels only (not copies)
         if (timed) {
@@ -643,7 +646,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.so[1] = so1;
         na.params = P;
         na.aux = X;
-        na.offs = E.p.dev_table + c.dev_lds_offs;
+        na.offs = E.p.dtab(c.dev_lds_offs);
         for (int n = 0; n < 2; n++) na.ci_off[n] = E.p.host_table[(size_t)c.dev_lds_offs + (size_t)n * na.offs_per_net];
         na.zero_bias = X + E.p.aux_zero;
         if (pend != nullptr) {
@@ -715,7 +718,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     auto ln3b = [&](const RBParams& rb) { return c.t2_mapped ? X + rb.ln3c_b : P + rb.ln3b; };
     // device-table maps of the mapped layouts (fake, never dereferenced, in dry runs)
     auto dmap = [&](int off) -> const int* {
-        return E.p.dry ? reinterpret_cast<const int*>(uintptr_t(1) << 40) : E.p.dev_table + off;
+        return E.p.dtab(off);
     };
 
     // conv_in (:1114-1119 / :1159-1164): u1c -> y, both nets in one launch
@@ -749,9 +752,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             }
             // only the channels the branches read are stored (into their consumers' sub-tensors when
             // t1_compact); the LN2 statistics still cover all nk channels
-            const int* t1map = c.t1_compact ? (E.p.dry ? reinterpret_cast<const int*>(uintptr_t(1) << 40)
-                                                       : E.p.dev_table + c.dev_t1_map)
-                                            : nullptr;
+            const int* t1map = c.t1_compact ? E.p.dtab(c.dev_t1_map) : nullptr;
             set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map));
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]. The k_gc
@@ -1172,7 +1173,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             // own buffer (cur, never written) takes the kept half
             float* nxt = have_pend ? const_cast<float*>(cur) : buf[which];
             const bool flip = !have_pend;
-            const int* T = p.dev_table;
+            const int* T = p.dtab(0);
             const float* src = cur;
             const int ncur = b.n_cur, nnext = b.n_next, nfac = b.n_fac;
             const int* ks = T + b.dev_keep_src;
@@ -1196,7 +1197,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     {
         // final scatter (restore to xy's layout) and the per-image log-det reduction: one launch
         MapOp mf;
-        mf.src = cur, mf.dst = zy, mf.didx = p.dev_table + p.dev_final_orig, mf.n = p.last_n, mf.ss = p.last_n;
+        mf.src = cur, mf.dst = zy, mf.didx = p.dtab(p.dev_final_orig), mf.n = p.last_n, mf.ss = p.last_n;
         mf.ds = nuv;
         LdReduce r;
         r.part = ld, r.out = logdet_per_image, r.nl = (int)p.couplings.size(), r.np = L.ld_parts, r.accumulate = 0;
@@ -1281,20 +1282,32 @@ int cnf_adam_step(float* params, const float* grads, float* m, float* v, int64_t
     CNF_CATCH
 }
 
+static void flow_inverse(Plan& p, const float* params, const float* aux, const float* zy, float* xy, void* workspace,
+                         int B, hipStream_t stream);
+
 int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, const float* zy, float* xy,
                      void* workspace, int B, void* stream) {
     if (!plan || !params || !aux || !xy || !zy || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy) return fail(CNF_E_INVALID, "zy and xy must not alias (out-of-place only)");
     CNF_TRY
-    Plan& p = *plan->p;
+    flow_inverse(*plan->p, params, aux, zy, xy, workspace, B, (hipStream_t)stream);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+}  // extern "C"
+
+// cFlow.call(zy, -1) (:1774-1798) as a launch schedule
+static void flow_inverse(Plan& p, const float* params, const float* aux, const float* zy, float* xy, void* workspace,
+                         int B, hipStream_t stream) {
     if (!p.dry) ensure_tables(p);
     p.recorded.clear();
-    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, (hipStream_t)stream};
+    Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
     const WsLayout& L = E.L;
     float* buf[2] = {E.at<float>(L.uv[0]), E.at<float>(L.uv[1])};
     const int nuv = (int)L.n_uv;
-    const int* T = p.dev_table;
+    const int* T = p.dtab(0);
     // squeeze/factor forward on zy (:1784-1788) == gather of the last block layout from xy positions
     int which = 0;
     {
@@ -1369,9 +1382,9 @@ int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, cons
         });
     }
     if (!p.dry) check_launch();
-    return CNF_OK;
-    CNF_CATCH
 }
+
+extern "C" {
 
 int cnf_coupling_forward(cnf_plan* plan, int layer, const float* params, const float* aux, const float* u, float* v,
                          float* logdet_accum, void* workspace, int B, void* stream) {
@@ -1573,6 +1586,36 @@ int cnf_debug_gc_launch_shapes(cnf_plan* plan, int B, int* words, int cap) {
     if ((int64_t)g.size() * GCSHAPE_WORDS > cap) return -1;
     for (size_t i = 0; i < g.size(); i++) std::memcpy(words + i * GCSHAPE_WORDS, &g[i], sizeof(GcShape));
     return (int)g.size() * GCSHAPE_WORDS;
+}
+
+// launch names of a B-image forward (direction +1) or inverse (-1) from a host-only dry run, one per
+// line into out (cap bytes, NUL-terminated); returns the number of launches, -1 on error
+int cnf_debug_schedule(cnf_plan* plan, int B, int direction, char* out, int cap) {
+    if (!plan || !out || cap <= 0 || B <= 0 || (direction != 1 && direction != -1)) return -1;
+    Plan& p = *plan->p;
+    CNF_TRY
+    p.dry = true;
+    p.dry_launches.clear();
+    char* fake = reinterpret_cast<char*>(uintptr_t(1) << 40);   // never dereferenced
+    const float* f = reinterpret_cast<const float*>(fake);
+    float* g = reinterpret_cast<float*>(fake + (1 << 20));        // a distinct output address
+    try {
+        if (direction > 0)
+            flow_forward(p, f, f, f, g, g, fake, B, nullptr, false);
+        else
+            flow_inverse(p, f, f, f, g, fake, B, nullptr);
+    } catch (...) {
+        p.dry = false;
+        throw;
+    }
+    p.dry = false;
+    p.recorded.clear();
+    std::string s;
+    for (const std::string& n : p.dry_launches) s += n + "\n";
+    if ((int)s.size() + 1 > cap) return -1;
+    std::memcpy(out, s.c_str(), s.size() + 1);
+    return (int)p.dry_launches.size();
+    CNF_CATCH
 }
 
 int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap) {

@@ -343,3 +343,67 @@ def test_t2_layout_is_dense_per_producer(lib, name):
     finally:
         lib.cnf_plan_destroy(p)
     assert (mapped > 0) == (name in ('cfg4', 'cfg5'))
+
+
+def _schedule(lib, name, B, direction):
+    lib.cnf_debug_schedule.restype = C.c_int
+    lib.cnf_debug_schedule.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_int]
+    kw = PRESETS[name].kwargs()
+    lists = [(C.c_int * len(kw[k]))(*kw[k]) for k in ('squeeze_factor_block_list', 'ResNeXt_block_list',
+                                                        'num_kernels_list', 'cardinality_list')]
+    d = _lib.cnf_flow_desc(*kw['io_shape'], kw['x_d'], len(lists[0]), *lists, 100.0, 3, 1, 1, 0)
+    p = C.c_void_p()
+    assert lib.cnf_plan_create(C.byref(d), C.byref(p)) == 0
+    try:
+        buf = C.create_string_buffer(1 << 16)
+        n = lib.cnf_debug_schedule(p, B, direction, buf, 1 << 16)
+        assert n > 0, lib.cnf_last_error()
+        names = buf.value.decode().split('\n')[:-1]
+        assert len(names) == n
+        return names
+    finally:
+        lib.cnf_plan_destroy(p)
+
+
+@pytest.mark.parametrize('name', ['tiny', 'small', 'cfg2', 'cfg3', 'ref_default', 'cfg4', 'cfg5', 'narrow'])
+def test_inverse_schedule_defers_like_the_forward(lib, name):
+    """Host-only dry runs of the fused forward and inverse schedules (cnf_flow_forward / _inverse,
+    conv_cINN_make_model.py:1723-1798): the inverse applies the deferred coupling law as the forward
+    does (an LDS layer followed by an LDS layer or a block boundary launches no k_coupling), rebuilds
+    each block boundary in one k_map2, and its last layer writes xy (no copy)."""
+    from arl_conditional_normalizing_flows_amd.config import PRESETS as PR
+    fwd = _schedule(lib, name, 3, 1)
+    inv = _schedule(lib, name, 3, -1)
+    assert 'copy' not in inv and 'k_map_scatter' not in inv
+    nb = sum(PR[name].squeeze_factor_block_list)
+    assert inv.count('k_map2') == nb and inv.count('k_map_gather') == 1
+    assert fwd.count('k_map2') == nb + 1
+    assert inv.count('k_net_lds') == fwd.count('k_net_lds')
+    # expected k_coupling launches from the layer kinds (kind 0 coupling, 2 factor; fused_net = LDS layer):
+    # a layer defers when it is an LDS layer whose successor (forward: next index; inverse: previous
+    # index) is an LDS coupling or a block boundary; the forward's last layer may defer into the tail
+    kw = PR[name].kwargs()
+    kw.pop('group_mode')
+    rc, p, keep = _plan(lib, kw)
+    assert rc == 0
+    info = _lib.cnf_layer_info()
+    kinds = []
+    try:
+        for li in range(lib.cnf_plan_num_layers(p)):
+            assert lib.cnf_plan_layer_info(p, li, C.byref(info)) == 0
+            if info.kind != 1:   # squeezes are folded into the boundary maps
+                kinds.append((info.kind, info.fused_net))
+    finally:
+        lib.cnf_plan_destroy(p)
+
+    def launches(seq, tail_defers):
+        n = 0
+        for i, (k, lds) in enumerate(seq):
+            if k != 0:
+                continue
+            nxt = seq[i + 1] if i + 1 < len(seq) else None
+            defer = lds and ((nxt is None and tail_defers) or (nxt is not None and (nxt[0] == 2 or (nxt[0] == 0 and nxt[1]))))
+            n += 0 if defer else 1
+        return n
+    assert fwd.count('k_coupling') == launches(kinds, True)
+    assert inv.count('k_coupling') == launches(kinds[::-1], False)
