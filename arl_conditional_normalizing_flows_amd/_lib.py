@@ -41,6 +41,9 @@ class cnf_toy_desc(C.Structure):
                 ('lambda_y', C.c_float)]
 
 
+# per-layer completion callback of cnf_flow_backward_ex (void (*)(void* user, int coupling_index))
+LAYER_DONE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int)
+
 # (name, restype, argtypes)
 _P = C.c_void_p
 _F = C.c_void_p   # device float* as integer address
@@ -67,6 +70,7 @@ _SIGS = [
     ('cnf_plan_train_workspace_bytes', C.c_size_t, [_P, C.c_int]),
     ('cnf_flow_forward_train', C.c_int, [_P, _F, _F, _F, _F, _F, _P, C.c_int, _P]),
     ('cnf_flow_backward', C.c_int, [_P, _F, _F, _F, _P, C.c_int, C.c_float, _F, _P]),
+    ('cnf_flow_backward_ex', C.c_int, [_P, _F, _F, _F, _P, C.c_int, _F, _F, LAYER_DONE_FN, _P, _P]),
     ('cnf_coupling_backward', C.c_int, [_P, C.c_int, _F, _F, _F, _F, C.c_float, _P, C.c_int, _F, _P]),
     ('cnf_adam_step', C.c_int, [_F, _F, _F, _F, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int,
                                 _P]),

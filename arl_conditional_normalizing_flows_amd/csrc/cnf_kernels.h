@@ -395,6 +395,7 @@ struct CoupBwArgs {
     float* dt;                // dL/dt
     double* dw_part;          // [B][gridDim.x]
     float g_ld;               // dL/d(per-image log-det)
+    const float* count;       // non-null: g_ld = -1 / *count (the global image count, on device)
     int H, W, D, mask, mask_c, hc, wc, dc1, dc2;
 };
 void launch_coupling_backward(const CoupBwArgs& a, int B, int nparts, hipStream_t st);
@@ -402,8 +403,10 @@ void launch_scatter_add_u1c(const float* du1c, float* du, int B, int H, int W, i
                             hipStream_t st);
 void launch_dsum(const double* part, long long n, float* out, hipStream_t st);
 // dL/dzy of the NLL (conv_cINN_make_model.py:1800-1848): z / Bg, lambda_y * sign(y - y') / Bg
+// count (device, may be null): the global image count; when given, inv_batch = 1 / *count (computed in
+// fp64 and rounded once, as the host does), so the scale needs no host read of the all-reduced count
 void launch_nll_grad(const float* xy, const float* zy, float* dzy, int B, int HW, int D, int x_d, float lambda_y,
-                     float inv_batch, hipStream_t st);
+                     float inv_batch, const float* count, hipStream_t st);
 void launch_adam(float* params, const float* grads, float* m, float* v, long long n, float alpha, float b1, float b2,
                  float eps, hipStream_t st);
 }  // namespace cnf

@@ -257,8 +257,10 @@ struct Plan {
 
 // cnf_train.cpp: dL/dparams of the NLL (loss scaled by inv_batch = 1 / global batch) into dparams,
 // from the coupling inputs saved by the training forward in `workspace`
+typedef void (*LayerDoneFn)(void* user, int coupling_index);
 void flow_backward(Plan& p, const float* params, const float* xy, const float* zy, void* workspace, int B,
-                   float inv_batch, float* dparams, hipStream_t st);
+                   float inv_batch, float* dparams, hipStream_t st, const float* count = nullptr,
+                   LayerDoneFn done = nullptr, void* user = nullptr);
 // one coupling layer's backward: du, dparams (zeroed first) for dL/dv = dv and dL/d logdet_b = g_ld
 void coupling_layer_backward(Plan& p, int ci, const float* params, const float* u, const float* dv, float* du,
                              float g_ld, void* workspace, int B, float* dparams, hipStream_t st);

@@ -1254,6 +1254,20 @@ int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, cons
     CNF_CATCH
 }
 
+int cnf_flow_backward_ex(cnf_plan* plan, const float* params, const float* xy, const float* zy, void* train_workspace,
+                         int B, const float* global_count, float* dparams, cnf_layer_done_fn layer_done, void* user,
+                         void* stream) {
+    if (!plan || !params || !xy || !zy || !train_workspace || !dparams || !global_count || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    CNF_TRY
+    Plan& p = *plan->p;
+    ensure_tables(p);
+    flow_backward(p, params, xy, zy, train_workspace, B, 0.f, dparams, (hipStream_t)stream, global_count, layer_done,
+                  user);
+    return CNF_OK;
+    CNF_CATCH
+}
+
 int cnf_coupling_backward(cnf_plan* plan, int layer, const float* params, const float* u, const float* dv, float* du,
                           float dlogdet, void* train_workspace, int B, float* dparams, void* stream) {
     if (!plan || !params || !u || !dv || !du || !train_workspace || !dparams || B <= 0)

@@ -128,6 +128,7 @@ struct TExec {
     int B;
     hipStream_t st;
     float inv_batch_ = 0.f;
+    const float* count = nullptr;   // device global image count (overrides inv_batch_)
     int net = 0;   // which per-net scratch set (and stream) this executor's launches use
     hipStream_t wst = nullptr;   // weight-gradient stream (null: on st)
     const float* bw() const { return reinterpret_cast<const float*>(ws + T.bw); }
@@ -385,6 +386,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         a.dt = E.at<float>(E.T.dso[1]);
         a.dw_part = E.at<double>(E.T.dwpart);
         a.g_ld = -E.inv_batch_;
+        a.count = E.count;
         a.H = c.H;
         a.W = c.W;
         a.D = c.D;
@@ -457,9 +459,10 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
 }  // namespace
 
 void flow_backward(Plan& p, const float* params, const float* xy, const float* zy, void* workspace, int B,
-                   float inv_batch, float* dparams, hipStream_t st) {
+                   float inv_batch, float* dparams, hipStream_t st, const float* count, LayerDoneFn done, void* user) {
     TExec E{p, params, dparams, (char*)workspace, p.layout(B), p.train_layout(B), B, st};
     E.inv_batch_ = inv_batch;
+    E.count = count;
     const WsLayout& L = E.L;
     const int* T = p.dev_table;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
@@ -467,7 +470,7 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     const int nuv = (int)L.n_uv;
     const cnf_flow_desc& d = p.desc;
     float* dzy = E.at<float>(E.T.dzy);
-    launch_nll_grad(xy, zy, dzy, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y, inv_batch, st);
+    launch_nll_grad(xy, zy, dzy, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y, inv_batch, count, st);
     float* buf[2] = {E.at<float>(E.T.duv[0]), E.at<float>(E.T.duv[1])};
     int which = 0;
     launch_map_gather(dzy, buf[which], T + p.dev_final_orig, p.last_n, nuv, p.last_n, B, st);
@@ -480,6 +483,9 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
             const Coupling& c = p.couplings[ly.ci];
             float* nxt = buf[which];
             coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
+            // every launch writing this layer's parameter gradients is ordered before anything enqueued
+            // on st from here (its side streams joined st): the caller may reduce them now
+            if (done != nullptr) done(user, c.index);
             cur = nxt;
             which ^= 1;
         } else if (ly.kind == CNF_LAYER_FACTOR) {

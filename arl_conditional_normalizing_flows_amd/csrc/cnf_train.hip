@@ -1124,6 +1124,7 @@ __global__ __launch_bounds__(256) void k_coup_bw(CoupBwArgs a) {
     float* dsb = a.ds_pre + (size_t)img * npx * a.dc2;
     float* dtb = a.dt + (size_t)img * npx * a.dc2;
     const float w = *a.tanh_w;
+    const float g_ld = a.count != nullptr ? -(float)(1.0 / (double)*a.count) : a.g_ld;
     double dw = 0.0;
     for (int p = blockIdx.x * 256 + threadIdx.x; p < npx; p += gridDim.x * 256) {
         for (int c = 0; c < a.dc1; c++) {
@@ -1137,7 +1138,7 @@ __global__ __launch_bounds__(256) void k_coup_bw(CoupBwArgs a) {
             const float ex = cpl_exp(w * th);
             const float g = dvb[e];
             dub[e] = g * ex;
-            const float ds = g * ex * ub[e] + a.g_ld;
+            const float ds = g * ex * ub[e] + g_ld;
             dsb[q] = ds * w * (1.f - th * th);
             dtb[q] = g;
             dw += (double)ds * th;
@@ -1185,7 +1186,8 @@ void launch_dsum(const double* part, long long n, float* out, hipStream_t st) {
 // loss = -(mean_b(llz + lly) + mean_b(logdet)) over the global batch (inv_batch = 1 / global B)
 __global__ __launch_bounds__(256) void k_nll_grad(const float* __restrict__ xy, const float* __restrict__ zy,
                                                   float* __restrict__ dzy, long long total, int D, int x_d,
-                                                  float lambda_y, float inv_batch) {
+                                                  float lambda_y, float inv_batch_h, const float* __restrict__ count) {
+    const float inv_batch = count != nullptr ? (float)(1.0 / (double)*count) : inv_batch_h;
     for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
         const int c = (int)(e % D);
         const float z = zy[e];
@@ -1201,12 +1203,12 @@ __global__ __launch_bounds__(256) void k_nll_grad(const float* __restrict__ xy, 
 }
 
 void launch_nll_grad(const float* xy, const float* zy, float* dzy, int B, int HW, int D, int x_d, float lambda_y,
-                     float inv_batch, hipStream_t st) {
+                     float inv_batch, const float* count, hipStream_t st) {
     const long long total = (long long)B * HW * D;
     long long gx = (total + 255) / 256;
     if (gx > 8192) gx = 8192;
     hipLaunchKernelGGL(k_nll_grad, dim3((unsigned)gx), dim3(256), 0, st, xy, zy, dzy, total, D, x_d, lambda_y,
-                       inv_batch);
+                       inv_batch, count);
 }
 
 // Keras Adam (optimizer.Adam: m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2);

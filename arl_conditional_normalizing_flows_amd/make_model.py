@@ -524,11 +524,31 @@ class cFlow:
             self._ws[key] = ws
         return ws
 
+    def _coupling_param_ranges(self):
+        """{coupling index: (lo, hi)} of its parameters (names 'c<i>.*') in the flat canonical vector."""
+        r = getattr(self, '_cranges', None)
+        if r is None:
+            r = {}
+            for n, o, s in self.param_specs:
+                ci = int(n.split('.', 1)[0][1:])
+                size = int(np.prod(s)) if s else 1
+                lo, hi = r.get(ci, (o, o))
+                if o != hi:
+                    raise RuntimeError(f'parameters of coupling {ci} are not contiguous')
+                r[ci] = (lo, o + size)
+            self._cranges = r
+        return r
+
     def gradients(self, xy, process_group=None):
         """tape.gradient(loss, trainable_variables) of train_step (:1863-1869) as one flat
-        vector in the canonical parameter order, plus the 4 loss terms (batch means). With
-        process_group (True = default group) the loss sums and the gradient are all-reduced, so
-        both are those of the global batch."""
+        vector in the canonical parameter order, plus the 4 loss terms (batch means, device
+        scalars). With process_group (True = default group) the loss sums and the gradient are
+        all-reduced, so both are those of the global batch: the 5-float loss all-reduce runs
+        between forward and backward with no host read of its result (the backward takes the
+        global image count from the device buffer), and each coupling layer's gradient range is
+        all-reduced asynchronously as soon as that layer's backward is enqueued, overlapping the
+        backward of the layers before it (CNF_GRAD_OVERLAP=0: one all-reduce after the backward)."""
+        import os
         from .distributed import allreduce_grads, pack_nll_sums
         xy = _as_input(xy, 'xy')
         if tuple(xy.shape[1:]) != tuple(self.io_shape):
@@ -543,16 +563,32 @@ class cFlow:
         sums, _ = self.nll_sums(xy, zy, ld)
         buf = pack_nll_sums(sums, B)
         grp = None if process_group is True else process_group
+        dist = None
         if process_group is not None:
-            import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized():
-                dist.all_reduce(buf, group=grp)
-        n_global = float(buf[4].item())
+            import torch.distributed as tdist
+            if tdist.is_available() and tdist.is_initialized():
+                dist = tdist
+        if dist is not None:
+            dist.all_reduce(buf, group=grp)
         if getattr(self, '_grads', None) is None or self._grads.numel() != self.num_params:
             self._grads = torch.empty(self.num_params, device=self.device, dtype=torch.float32)
-        check(lib.cnf_flow_backward(self._plan, ptr(self.params), ptr(xy), ptr(zy), ptr(ws), B, 1.0 / n_global,
-                                    ptr(self._grads), _stream()), 'cnf_flow_backward')
-        if process_group is not None:
+        overlap = dist is not None and os.environ.get('CNF_GRAD_OVERLAP', '1') != '0'
+        works = []
+        if overlap:
+            ranges = self._coupling_param_ranges()
+            grads = self._grads
+
+            def done(_user, ci):
+                lo, hi = ranges[ci]
+                works.append(dist.all_reduce(grads[lo:hi], group=grp, async_op=True))
+            cb = _lib.LAYER_DONE_FN(done)
+        else:
+            cb = _lib.LAYER_DONE_FN()
+        check(lib.cnf_flow_backward_ex(self._plan, ptr(self.params), ptr(xy), ptr(zy), ptr(ws), B, ptr(buf) + 16,
+                                       ptr(self._grads), cb, None, _stream()), 'cnf_flow_backward_ex')
+        for w in works:
+            w.wait()
+        if dist is not None and not overlap:
             allreduce_grads(self._grads, group=grp)
         m = buf[:4] / buf[4]
         return self._grads, (m[0], m[1], m[2], m[3])

@@ -175,6 +175,23 @@ int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux
 int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, const float* zy,
                       void* train_workspace, int B, float inv_batch, float* dparams, void* stream);
 
+/* cnf_flow_backward for data-parallel training with the gradient reduction
+ * overlapped (conv_cINN_make_model.py:1863-1870):
+ *  - global_count (device, 1 float) is the global image count, e.g. red5[4] of
+ *    cnf_nll_allreduce: inv_batch = 1 / *global_count is taken on the device, so
+ *    no host read of the all-reduced count sits between forward and backward;
+ *  - layer_done (may be NULL) is called on the calling host thread as soon as the
+ *    launches producing coupling layer `coupling_index`'s parameter gradients
+ *    (names "c<index>.*", one contiguous range of dparams) are enqueued on
+ *    `stream` (the backward's side streams have joined it). Work the callback
+ *    enqueues behind that point on `stream` (or on a stream waiting for it), e.g.
+ *    cnf_allreduce_sum_f32 of that range, overlaps the backward of the layers
+ *    before it. Layers complete in reverse index order. */
+typedef void (*cnf_layer_done_fn)(void* user, int coupling_index);
+int cnf_flow_backward_ex(cnf_plan* plan, const float* params, const float* xy, const float* zy,
+                         void* train_workspace, int B, const float* global_count, float* dparams,
+                         cnf_layer_done_fn layer_done, void* user, void* stream);
+
 /* Backward of one coupling layer (layer index into layers_list) at input u:
  * du = dL/du and dparams = dL/dparams (zeroed first; only this layer's entries
  * are non-zero) for upstream dv = dL/dv and dlogdet = dL/d(per-image log-det). */

@@ -116,3 +116,55 @@ def test_capi_comm_rejects_bad_arguments(gpu):
     comm = C.c_void_p()
     assert lib.cnf_comm_init(0, 0, b'\0' * 128, C.byref(comm)) == -1
     assert lib.cnf_allreduce_sum_f32(None, None, 4, None) == -1
+
+
+def _grad_worker(rank, world, port, G, out_dir, overlap):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['CNF_GRAD_OVERLAP'] = '1' if overlap else '0'
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from arl_conditional_normalizing_flows_amd.make_model import cFlow
+        dev = torch.device('cuda', 0)
+        cfg = PRESETS['small']
+        kw = cfg.kwargs()
+        flow = cFlow(**kw, device=dev)
+        flow.set_weights(OracleCFlow(**kw).init_params(3))
+        H, W, _ = cfg.io_shape
+        xy = synthetic_class_batch(G, H, W, cfg.x_d, seed=9)
+        lo, hi = shard_range(G, rank, world)
+        g, terms = flow.gradients(torch.from_numpy(xy[lo:hi]).to(dev), process_group=True)
+        torch.cuda.synchronize()
+        np.save(os.path.join(out_dir, f'g{rank}_{int(overlap)}.npy'), g.cpu().numpy())
+        np.save(os.path.join(out_dir, f't{rank}_{int(overlap)}.npy'), torch.stack(terms).cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('G', [6, 7])
+def test_gloo_world2_overlapped_gradient_allreduce(gpu, tmp_path, G):
+    """cFlow.gradients(process_group=...): each coupling layer's gradient range all-reduced
+    asynchronously as its backward is enqueued (cnf_flow_backward_ex layer callbacks), the global image
+    count read on the device (no host sync) — bitwise the non-overlapped path (one all-reduce after
+    the backward, CNF_GRAD_OVERLAP=0), the same on every rank, and equal (to fp32 summation order) to
+    one process's gradient of the whole global batch."""
+    world = 2
+    for overlap in (True, False):
+        mp.spawn(_grad_worker, args=(world, _free_port(), G, str(tmp_path), overlap), nprocs=world, join=True)
+    g = {(r, o): np.load(tmp_path / f'g{r}_{o}.npy') for r in (0, 1) for o in (0, 1)}
+    t = {(r, o): np.load(tmp_path / f't{r}_{o}.npy') for r in (0, 1) for o in (0, 1)}
+    assert np.array_equal(g[0, 1], g[0, 0]) and np.array_equal(g[1, 1], g[1, 0])
+    assert np.array_equal(g[0, 1], g[1, 1]) and np.array_equal(t[0, 1], t[1, 1])
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    cfg = PRESETS['small']
+    kw = cfg.kwargs()
+    flow = cFlow(**kw, device=gpu)
+    flow.set_weights(OracleCFlow(**kw).init_params(3))
+    H, W, _ = cfg.io_shape
+    xy = synthetic_class_batch(G, H, W, cfg.x_d, seed=9)
+    g1, t1 = flow.gradients(torch.from_numpy(xy).to(gpu))
+    g1 = g1.cpu().numpy()
+    err = np.max(np.abs(g[0, 1] - g1))
+    print(f'G={G}: sharded vs whole-batch gradient max abs diff {err:.2e} (max |g| {np.max(np.abs(g1)):.2e})')
+    assert err <= 1e-5 * np.max(np.abs(g1))
+    assert np.allclose(t[0, 1], torch.stack(t1).cpu().numpy(), rtol=1e-5, atol=1e-4)
