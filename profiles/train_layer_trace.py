@@ -42,13 +42,14 @@ def fold(out):
         with open(f) as fh:
             rows += list(csv.DictReader(fh))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    # the last rep: after the last gap > 10 ms
-    starts = [int(r['Start_Timestamp']) for r in rows]
-    cut = 0
-    for i in range(1, len(rows)):
-        if starts[i] - int(rows[i - 1]['End_Timestamp']) > 10_000_000:
-            cut = i
-    rows = rows[cut:]
+    # reps are separated by torch's GPU sleep kernel (at::cuda::...): keep the last rep
+    reps = [[]]
+    for r in rows:
+        if 'at::' in r['Kernel_Name']:
+            reps.append([])
+        else:
+            reps[-1].append(r)
+    rows = [x for x in reps if x][-1]
     t0 = int(rows[0]['Start_Timestamp'])
     tend = max(int(r['End_Timestamp']) for r in rows)
     busy = {}
