@@ -11,7 +11,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / 'csrc'
 # CNF_BUILD_LIB: write a diagnostic build elsewhere (e.g. the host-sanitizer build, tools/host_sanitize.sh)
 LIB = Path(os.environ['CNF_BUILD_LIB']) if os.environ.get('CNF_BUILD_LIB') else PKG / 'lib' / 'libcnf_hip.so'
-SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
+SOURCES = ['cnf_kernels.hip', 'cnf_stream.hip', 'cnf_netlds.hip', 'cnf_toy.hip', 'cnf_train.hip', 'cnf_ldsbwd.hip', 'cnf_transforms.hip', 'cnf_runtime.cpp',
            'cnf_plan.cpp', 'cnf_train.cpp', 'cnf_comm.cpp']
 HEADERS = ["cnf_kernels.h", "cnf_device.h", "cnf_plan.h", "cnf_netlds_shapes.inc", "cnf_gc_shapes.inc", "cnf_pw_shapes.inc"]
 ARCH = os.environ.get('CNF_OFFLOAD_ARCH', 'gfx950')

@@ -157,6 +157,28 @@ struct NetLdsArgs {
     CoupPend pend;                               // previous layer's deferred coupling (pend.on)
     int ci_off[2];                               // conv_in image offset in aux per net (offs[net][0]): its
                                                  // prefetch starts before the offset table is staged
+    // training forward (cnf_flow_forward_train): the raw activations and LN statistics the fused
+    // backward (k_lds_bwd) reads, one LdsSave block of save_img floats per (net, image), [net][B]
+    // (null: inference)
+    float* save;
+    int save_img, save_t1, save_t2, save_st;
+};
+
+// Block of one (net, image) in a k_net_lds layer's training save area (all float offsets):
+//   y_r  [HW][nk] at r * HW * nk                 (r = 0..R: conv_in's output, then each block's output)
+//   t1_r [HW][nk] at t1 + r * HW * nk            (conv_a's raw output)
+//   t2_r [HW][gc] at t2 + r * HW * gc            (the grouped stage's raw concat)
+//   (mean, rstd) at st: LN1_r at 2r, LN2_r at 2(R + r), LN3_r at 2(2R + r), LN_out at 6R
+struct LdsSave {
+    int img = 0, t1 = 0, t2 = 0, st = 0;
+    static LdsSave of(int HW, int nk, int gc, int R) {
+        LdsSave s;
+        s.t1 = (R + 1) * HW * nk;
+        s.t2 = s.t1 + R * HW * nk;
+        s.st = s.t2 + R * HW * gc;
+        s.img = (s.st + 2 * (3 * R + 1) + 3) / 4 * 4;
+        return s;
+    }
 };
 // The launch-independent "shape" of a k_net_lds launch as int words: [offs_per_net, zero_bias) and
 // [off_y, stamp_off) of NetLdsArgs (the mask word inside is not part of it). Shape-specialised
@@ -385,6 +407,43 @@ constexpr int LNB_RS = 8;
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
                         float* scratch, hipStream_t st);
+// Fused training backward of a k_net_lds layer (cnf_ldsbwd.hip): grid (B, 2 nets), one workgroup per
+// (image, net). Offsets table per net (int32, `offs_per_net` entries): canonical parameter offsets
+// (LN gamma / beta, the net's first parameter, tanh scale or -1) and dense backward-image offsets
+// (conv weights _DW, biases _DB), laid out as the LDSBWD_* indices below (per residual block r at
+// LDSBWD_RB0 + r * (10 + 2 * nbr), branch bi's (dw, db) at LDSBWD_BR + 2 bi of it).
+enum {
+    LDSBWD_LO = 0, LDSBWD_CI_DW, LDSBWD_CI_DB, LDSBWD_LNO_G, LDSBWD_LNO_B, LDSBWD_CO_DW, LDSBWD_CO_DB, LDSBWD_TANH,
+    LDSBWD_RB0
+};
+enum {
+    LDSBWD_LN1G = 0, LDSBWD_LN1B, LDSBWD_CA_DW, LDSBWD_CA_DB, LDSBWD_LN2G, LDSBWD_LN2B, LDSBWD_LN3G, LDSBWD_LN3B,
+    LDSBWD_CB_DW, LDSBWD_CB_DB, LDSBWD_BR
+};
+struct LdsBwdArgs {
+    const float* save;        // the training forward's save area of the layer [net][B][save_img] (LdsSave)
+    int save_img, save_t1, save_t2, save_st;
+    const float* dso[2];      // dL/d(raw conv_out) per net [B][hc][wc][dc2] (k_coup_bw)
+    const float* u;           // the layer input [B][H][W][D] (conv_in reads its mask-compressed half)
+    float* du1c[2];           // out: dL/du1c per net [B][hc][wc][dc1]
+    const float* params;      // canonical parameters (LN gamma / beta)
+    const float* bw;          // dense backward weight image (launch_pack)
+    const int64_t* bw_map;    // dense -> canonical parameter index
+    const int* offs;          // [2][offs_per_net]
+    int offs_per_net;
+    float* part;              // out: per (net, image) gradient rows [2][B][row], the net's canonical range
+    int row;
+    int H, W, D, mask, hc, wc, dc1, dc2, nk, gc, R, nbr, ln, taps;
+    int br_cin_off[NETLDS_MAXBR], br_cin[NETLDS_MAXBR], br_cout[NETLDS_MAXBR], br_out_off[NETLDS_MAXBR],
+        br_dil[NETLDS_MAXBR];
+    int sy, st, sa, ac_chunk;                                   // LDS pixel strides (floats); conv_b staging chunk
+    int off_gt, off_ac, off_w, off_kt, off_red, off_ot, lds_bytes;   // LDS byte offsets (GY at 0)
+};
+void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st);
+// dparams[lo_n + i] += sum_b part[n][b][i] (i < len_n, n = 0, 1; row floats per (net, image) row)
+void launch_grad_rows(const float* part, int B, int row, int64_t lo0, int64_t lo1, int len0, int len1, float* dparams,
+                      hipStream_t st);
+
 struct CoupBwArgs {
     const float* u;           // layer input [B][H][W][D]
     const float* dv;          // dL/dv

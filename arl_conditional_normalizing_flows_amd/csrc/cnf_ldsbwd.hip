@@ -1,0 +1,453 @@
+// cnf_ldsbwd.hip — fused training backward of a k_net_lds layer's s,t networks
+// (conv_cINN_make_model.py:1076-1213 under the tf.GradientTape of train_step, :1850-1870).
+//
+// One workgroup per (image, net) walks the network in reverse with every gradient resident in LDS:
+// conv_out, LN_out, then per residual block (last first) conv_b, LN3, the grouped dilated branches,
+// LN2, conv_a, LN1 (the residual adds the identity path), and conv_in. The forward activations it
+// needs are the raw tensors and LN statistics the training forward's k_net_lds saved (LdsSave), so
+// nothing is recomputed; LN is LayerNormalization over H*W*C per image of LeakyReLU(x)
+// (conv_cINN_base_functions.py:330-362). Data gradients are implicit GEMMs on
+// v_mfma_f32_16x16x4_f32 over the transposed weights (3x3 taps mirrored through a k-table); weight
+// gradients contract over the image's pixels on MFMA. Every parameter gradient of the image goes to
+// its (net, image) row of the partial buffer in the net's canonical parameter order (convs through
+// the dense backward map), and k_grad_rows sums the rows over the batch in image order: the result is
+// bitwise reproducible. This replaces the ~230 launches per layer of the multi-kernel backward
+// (cnf_train.cpp) — one launch per layer plus the row sum.
+//
+// LDS (floats): GY [HW][sy] dL/dy (the residual stream's gradient) | GT [HW][st] dL/dt2, dL/dt1,
+// dL/d(so) | AC [HW][sa] staged activations / the next gradient | W [kp][np] transposed weights |
+// KT k-table ints | RED fp64 reduction scratch.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "cnf_device.h"
+#include "cnf_kernels.h"
+
+namespace cnf {
+
+namespace {
+
+constexpr int BWN = 8;          // waves per workgroup
+constexpr int BWT = BWN * 64;   // threads
+
+__device__ __forceinline__ float lrelu_b(float x) { return fmaxf(x, LRELU_ALPHA * x); }
+__device__ __forceinline__ float lrelu_d(float x) { return x > 0.f ? 1.f : LRELU_ALPHA; }
+
+// k-table entry of a flat reduction index k = tap * cpt + c: (dr + 64) | (dc + 64) << 7 | c << 14,
+// dr / dc the pixel offset of the tap (sgn = +1: x[p + d*off], the forward taps; sgn = -1: the
+// transposed conv's mirrored taps); -1 beyond K
+__device__ __forceinline__ void build_kt(int* kt, int K, int Kp, int cpt, int taps, int d, int sgn) {
+    for (int k = threadIdx.x; k < Kp; k += BWT) {
+        int t = -1;
+        if (k < K) {
+            const int tap = k / cpt, c = k - tap * cpt;
+            const int dr = taps == 9 ? sgn * d * (tap / 3 - 1) : 0, dc = taps == 9 ? sgn * d * (tap % 3 - 1) : 0;
+            t = (dr + 64) | ((dc + 64) << 7) | (c << 14);
+        }
+        kt[k] = t;
+    }
+}
+
+// A(p, k) of a k-table entry t for pixel (pr, pc): a[(p + shift) * sa + a_off + c], 0 outside the image
+__device__ __forceinline__ float kt_load(const float* a, int sa, int a_off, int t, int pr, int pc, int H, int W) {
+    if (t < 0) return 0.f;
+    const int y = pr + (t & 127) - 64, x = pc + ((t >> 7) & 127) - 64;
+    if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0.f;
+    return a[(y * W + x) * sa + a_off + (t >> 14)];
+}
+
+// out[p][o_off + n] (= or +=) sum_k A(p, k) * Wl[k][n] for n < N: units of one 16-pixel subtile x
+// NR 16-column blocks, dealt round-robin over the waves (acc[m][r] = out[p0 + 4kq + r][n0 + 16m + i16])
+template <int NR>
+__device__ void gemm_px(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np, float* out,
+                        int so, int o_off, int N, int H, int W, bool accum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int HW = H * W, nsub = (HW + 15) >> 4, ngrp = (np / 16 + NR - 1) / NR;
+    for (int unit = wave; unit < nsub * ngrp; unit += BWN) {
+        const int s = unit % nsub, n0 = (unit / nsub) * 16 * NR;
+        const int p = s * 16 + i16;
+        const bool pv = p < HW;
+        const int pr = pv ? p / W : -4096, pc = pv ? p - (p / W) * W : -4096;
+        f4 acc[NR];
+#pragma unroll
+        for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < Kp; k0 += 4) {
+            const float av = kt_load(a, sa, a_off, kt[k0 + kq], pr, pc, H, W);
+            const float* brow = wl + (size_t)(k0 + kq) * np + n0 + i16;
+#pragma unroll
+            for (int m = 0; m < NR; m++)
+                if (n0 + 16 * m < np) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, brow[16 * m], acc[m], 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int q = s * 16 + 4 * kq + r;
+            if (q >= HW) continue;
+#pragma unroll
+            for (int m = 0; m < NR; m++) {
+                const int n = n0 + 16 * m + i16;
+                if (n >= N) continue;
+                float* o = out + q * so + o_off + n;
+                *o = accum ? *o + acc[m][r] : acc[m][r];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void gemm_any(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np,
+                                         float* out, int so, int o_off, int N, int H, int W, bool accum) {
+    if (np <= 16)
+        gemm_px<1>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+    else if (np <= 32)
+        gemm_px<2>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+    else
+        gemm_px<4>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+}
+
+// dW[k][n] = sum_p A(p, k) * G[p][g_off + n] (k < K = taps * cin flat, n < N) for this image, stored to
+// row[bw_map[dw + k * N + n] - lo]; the bias gradient sum_p G[p][n] to row[bw_map[db + n] - lo].
+// Units: (16-row k block, 16-column n block); the pixel loop alternates two accumulators.
+__device__ void wgrad_px(const float* a, int sa, int a_off, const int* kt, int K, const float* g, int sg, int g_off,
+                         int N, int H, int W, const int64_t* __restrict__ bw_map, int64_t dw, int64_t db, int64_t lo,
+                         float* __restrict__ row) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int HW = H * W, nkb = (K + 15) >> 4, nnb = (N + 15) >> 4;
+    for (int unit = wave; unit < nkb * nnb; unit += BWN) {
+        const int k0 = (unit % nkb) * 16, n0 = (unit / nkb) * 16;
+        const int t = k0 + i16 < K ? kt[k0 + i16] : -1;
+        const int n = n0 + i16;
+        const bool nv = n < N;
+        f4 acc0 = f4{0.f, 0.f, 0.f, 0.f}, acc1 = f4{0.f, 0.f, 0.f, 0.f};
+        int pr = 0, pc = kq;   // pixel p = p0 + kq, tracked incrementally
+        while (pc >= W) {
+            pc -= W;
+            pr++;
+        }
+        for (int p0 = 0; p0 < HW; p0 += 8) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int p = p0 + 4 * h + kq;
+                const bool pv = p < HW;
+                const float av = pv ? kt_load(a, sa, a_off, t, pr, pc, H, W) : 0.f;
+                const float bv = (pv && nv) ? g[p * sg + g_off + n] : 0.f;
+                if (h == 0)
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
+                else
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
+                pc += 4;
+                while (pc >= W) {
+                    pc -= W;
+                    pr++;
+                }
+            }
+        }
+        // acc[r] = dW[k0 + 4kq + r][n]
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int k = k0 + 4 * kq + r;
+            if (k < K && nv) {
+                const int64_t dst = bw_map[dw + (int64_t)k * N + n];
+                if (dst >= 0) row[dst - lo] = acc0[r] + acc1[r];
+            }
+        }
+    }
+    if (db < 0) return;   // (a later row chunk of the same conv: its bias went with the first)
+    for (int j = threadIdx.x; j < N; j += BWT) {
+        float s = 0.f;
+        for (int p = 0; p < HW; p++) s += g[p * sg + g_off + j];
+        const int64_t dst = bw_map[db + j];
+        if (dst >= 0) row[dst - lo] = s;
+    }
+}
+
+// Wl[k][n] = W[tap][n][o] for k = tap * cout + o (the transposed conv's B operand: dgrad of a conv
+// with dense weights W[taps][cin][cout]); n < cin, zero padding to kp rows x np columns
+__device__ __forceinline__ void stage_wt(const float* __restrict__ w, int taps, int cin, int cout, int kp, int np,
+                                         float* wl) {
+    const int K = taps * cout;
+    for (int e = threadIdx.x; e < kp * np; e += BWT) {
+        const int k = e / np, n = e - k * np;
+        float v = 0.f;
+        if (k < K && n < cin) {
+            const int tap = k / cout, o = k - tap * cout;
+            v = w[((size_t)tap * cin + n) * cout + o];
+        }
+        wl[e] = v;
+    }
+}
+
+// fixed-order workgroup sum of two doubles (every thread gets the totals)
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * (threadIdx.x >> 6)] = a;
+        red[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    double s = 0.0, t = 0.0;
+#pragma unroll
+    for (int w = 0; w < BWN; w++) {
+        s += red[2 * w];
+        t += red[2 * w + 1];
+    }
+    __syncthreads();   // (red reusable)
+    a = s;
+    b = t;
+}
+
+// LayerNorm(LeakyReLU) backward of one image (as k_lnb_reduce / k_lnb_apply): d = dL/d(LN output) in
+// LDS ([HW][sd] at d_off, C channels), x the raw input (global, dense [HW][C]), gamma the per-element
+// scale; dx = dL/dx to out ([HW][so] at o_off, stored or added), and the image's dgamma = d * xhat,
+// dbeta = d to its row. ln == false: LeakyReLU only.
+__device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const float* __restrict__ gam, const float* d,
+                       int sd, int d_off, float* out, int so, int o_off, bool accum, int HW, int C, bool ln,
+                       float* __restrict__ rg, float* __restrict__ rb, double* red) {
+    const int n = HW * C;
+    if (!ln) {
+        for (int e = threadIdx.x; e < n; e += BWT) {
+            const int p = e / C, c = e - p * C;
+            const float v = d[p * sd + d_off + c] * lrelu_d(x[e]);
+            float* o = out + p * so + o_off + c;
+            *o = accum ? *o + v : v;
+        }
+        __syncthreads();
+        return;
+    }
+    double sg = 0.0, sgh = 0.0;
+    for (int e = threadIdx.x; e < n; e += BWT) {
+        const int p = e / C, c = e - p * C;
+        const float xh = (lrelu_b(x[e]) - mu) * rs;
+        const float g = d[p * sd + d_off + c] * gam[e];
+        sg += g;
+        sgh += (double)g * xh;
+    }
+    block_sum2(sg, sgh, red);
+    const float inv_n = 1.f / (float)n;
+    const float mg = (float)(sg * inv_n), mgh = (float)(sgh * inv_n);
+    for (int e = threadIdx.x; e < n; e += BWT) {
+        const int p = e / C, c = e - p * C;
+        const float xv = x[e];
+        const float xh = (lrelu_b(xv) - mu) * rs;
+        const float dv = d[p * sd + d_off + c];
+        rg[e] = dv * xh;
+        rb[e] = dv;
+        const float v = rs * (dv * gam[e] - mg - xh * mgh) * lrelu_d(xv);
+        float* o = out + p * so + o_off + c;
+        *o = accum ? *o + v : v;
+    }
+    __syncthreads();
+}
+
+// stage LN(LeakyReLU(x)) (or LeakyReLU(x) when !ln) of channels [c0, c0 + nc) of a C-channel raw tensor
+// x (global, dense) into dst [HW][sd] from channel 0
+__device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, int HW, float mu, float rs,
+                          const float* __restrict__ gam, const float* __restrict__ bet, bool ln, float* dst, int sd) {
+    const int n = HW * nc;
+    for (int e = threadIdx.x; e < n; e += BWT) {
+        const int p = e / nc, c = e - p * nc;
+        const size_t gi = (size_t)p * C + c0 + c;
+        const float h = lrelu_b(x[gi]);
+        dst[p * sd + c] = ln ? (h - mu) * rs * gam[gi] + bet[gi] : h;
+    }
+}
+
+// position in u of element (pixel p, channel c) of the mask-compressed u1c (mask compress, :720-759)
+__device__ __forceinline__ int mask_pos_b(int m, int p, int c, int wc, int W, int D) {
+    const int pr = p / wc, pc = p - pr * wc;
+    if (m < 2) {
+        const int half = c >= D ? 1 : 0;
+        const int ch = c - half * D;
+        const int dcol = (m == 0) ? half : 1 - half;
+        return ((2 * pr + half) * W + (2 * pc + dcol)) * D + ch;
+    }
+    return (pr * W + pc) * D + ((m == 2) ? 2 * c : 2 * c + 1);
+}
+
+}  // namespace
+
+// offsets table per net (LdsBwdArgs::offs): see LDSBWD_* in cnf_kernels.h
+__global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int img = blockIdx.x, net = blockIdx.y, B = gridDim.x;
+    const int H = a.hc, W = a.wc, HW = H * W, nk = a.nk, gc = a.gc, R = a.R;
+    const bool ln = a.ln != 0;
+    float* GY = reinterpret_cast<float*>(smem);
+    float* GT = reinterpret_cast<float*>(smem + a.off_gt);
+    float* AC = reinterpret_cast<float*>(smem + a.off_ac);
+    float* WL = reinterpret_cast<float*>(smem + a.off_w);
+    int* KT = reinterpret_cast<int*>(smem + a.off_kt);
+    double* RED = reinterpret_cast<double*>(smem + a.off_red);
+    int* OT = reinterpret_cast<int*>(smem + a.off_ot);
+    const int SY = a.sy, ST = a.st, SA = a.sa;
+    for (int i = threadIdx.x; i < a.offs_per_net; i += BWT) OT[i] = a.offs[net * a.offs_per_net + i];
+    __syncthreads();
+    const int64_t lo = OT[LDSBWD_LO];
+    const float* sv = a.save + ((size_t)net * B + img) * a.save_img;
+    const float* st = sv + a.save_st;
+    const float* P = a.params;
+    const float* BWI = a.bw;
+    float* row = a.part + ((size_t)net * B + img) * a.row;
+    auto rbo = [&](int r) { return OT + LDSBWD_RB0 + r * (10 + 2 * a.nbr); };
+    auto kp4 = [](int K) { return (K + 3) & ~3; };
+    auto np16 = [](int N) { return (N + 15) & ~15; };
+    const int taps = a.taps;
+    if (OT[LDSBWD_TANH] >= 0 && threadIdx.x == 0) row[OT[LDSBWD_TANH] - lo] = 0.f;   // (k_dsum adds it)
+
+    // ---- conv_out: G = dL/d so (dc2 ch) -> GT; A = LN_out(y_R) -> AC; wgrad; dgrad -> GY
+    {
+        const float* ds = a.dso[net] + (size_t)img * HW * a.dc2;
+        for (int e = threadIdx.x; e < HW * a.dc2; e += BWT) {
+            const int p = e / a.dc2, c = e - p * a.dc2;
+            GT[p * ST + c] = ds[e];
+        }
+        const float* yR = sv + (size_t)R * HW * nk;
+        const float mu = st[6 * R], rs = st[6 * R + 1];
+        stage_act(yR, nk, 0, nk, HW, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, ln ? P + OT[LDSBWD_LNO_B] : nullptr,
+                  ln, AC, SA);
+        build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
+        __syncthreads();
+        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row);
+        __syncthreads();
+        stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, kp4(taps * a.dc2), np16(nk), WL);
+        build_kt(KT, taps * a.dc2, kp4(taps * a.dc2), a.dc2, taps, 1, -1);
+        __syncthreads();
+        gemm_any(GT, ST, 0, KT, kp4(taps * a.dc2), WL, np16(nk), GY, SY, 0, nk, H, W, false);
+        __syncthreads();
+        // LN_out backward in place on GY
+        ln_bwd(yR, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, GY, SY, 0, GY, SY, 0, false, HW, nk, ln,
+               ln ? row + (OT[LDSBWD_LNO_G] - lo) : nullptr, ln ? row + (OT[LDSBWD_LNO_B] - lo) : nullptr, RED);
+    }
+    for (int r = R - 1; r >= 0; r--) {
+        const int* o = rbo(r);
+        const float* yr = sv + (size_t)r * HW * nk;
+        const float* t1r = sv + a.save_t1 + (size_t)r * HW * nk;
+        const float* t2r = sv + a.save_t2 + (size_t)r * HW * gc;
+        const float mu1 = st[2 * r], rs1 = st[2 * r + 1];
+        const float mu2 = st[2 * (R + r)], rs2 = st[2 * (R + r) + 1];
+        const float mu3 = st[2 * (2 * R + r)], rs3 = st[2 * (2 * R + r) + 1];
+        // ---- conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r))): wgrad in channel chunks of the staged LN3(t2),
+        // dgrad dL/d LN3-out -> GT
+        for (int c0 = 0; c0 < gc; c0 += a.ac_chunk) {
+            const int nc = gc - c0 < a.ac_chunk ? gc - c0 : a.ac_chunk;
+            stage_act(t2r, gc, c0, nc, HW, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, ln ? P + o[LDSBWD_LN3B] : nullptr,
+                      ln, AC, SA);
+            build_kt(KT, nc, kp4(nc), nc, 1, 1, 1);
+            __syncthreads();
+            // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
+            // gradient once, with the first chunk)
+            wgrad_px(AC, SA, 0, KT, nc, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
+                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row);
+            __syncthreads();
+        }
+        stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, kp4(nk), np16(gc), WL);
+        build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
+        __syncthreads();
+        gemm_any(GY, SY, 0, KT, kp4(nk), WL, np16(gc), GT, ST, 0, gc, H, W, false);
+        __syncthreads();
+        // ---- LN3 backward in place on GT -> dL/dt2
+        ln_bwd(t2r, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, GT, ST, 0, GT, ST, 0, false, HW, gc, ln,
+               ln ? row + (o[LDSBWD_LN3G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN3B] - lo) : nullptr, RED);
+        // ---- grouped branches: every wgrad (A = LN2(t1) window -> AC), then every dgrad into AC (zeroed)
+        for (int bi = 0; bi < a.nbr; bi++) {
+            const int cin = a.br_cin[bi], cout = a.br_cout[bi];
+            stage_act(t1r, nk, a.br_cin_off[bi], cin, HW, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr,
+                      ln ? P + o[LDSBWD_LN2B] : nullptr, ln, AC, SA);
+            build_kt(KT, taps * cin, kp4(taps * cin), cin, taps, a.br_dil[bi], 1);
+            __syncthreads();
+            wgrad_px(AC, SA, 0, KT, taps * cin, GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
+                     o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row);
+            __syncthreads();
+        }
+        for (int e = threadIdx.x; e < HW * nk; e += BWT) {
+            const int p = e / nk, c = e - p * nk;
+            AC[p * SA + c] = 0.f;
+        }
+        for (int bi = 0; bi < a.nbr; bi++) {
+            const int cin = a.br_cin[bi], cout = a.br_cout[bi];
+            stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, kp4(taps * cout), np16(cin), WL);
+            build_kt(KT, taps * cout, kp4(taps * cout), cout, taps, a.br_dil[bi], -1);
+            __syncthreads();
+            gemm_any(GT, ST, a.br_out_off[bi], KT, kp4(taps * cout), WL, np16(cin), AC, SA, a.br_cin_off[bi], cin, H, W,
+                     true);
+            __syncthreads();
+        }
+        // ---- LN2 backward: AC (dL/d LN2-out, zero outside the windows) -> dL/dt1 in GT
+        ln_bwd(t1r, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr, AC, SA, 0, GT, ST, 0, false, HW, nk, ln,
+               ln ? row + (o[LDSBWD_LN2G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN2B] - lo) : nullptr, RED);
+        // ---- conv_a: A = LN1(y_r) -> AC; wgrad with GT; dgrad -> AC
+        stage_act(yr, nk, 0, nk, HW, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, ln ? P + o[LDSBWD_LN1B] : nullptr, ln,
+                  AC, SA);
+        build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
+        __syncthreads();
+        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row);
+        __syncthreads();
+        stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, kp4(nk), np16(nk), WL);
+        build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
+        __syncthreads();
+        gemm_any(GT, ST, 0, KT, kp4(nk), WL, np16(nk), AC, SA, 0, nk, H, W, false);
+        __syncthreads();
+        // ---- LN1 backward: GY += dL/dy_r through conv_a (the identity path keeps GY)
+        ln_bwd(yr, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, AC, SA, 0, GY, SY, 0, true, HW, nk, ln,
+               ln ? row + (o[LDSBWD_LN1G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN1B] - lo) : nullptr, RED);
+    }
+    // ---- conv_in: A = u1c (gathered from the layer input) -> AC; wgrad with GY; dgrad -> GT -> du1c
+    {
+        const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
+        for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
+            const int p = e / a.dc1, c = e - p * a.dc1;
+            AC[p * SA + c] = ub[mask_pos_b(a.mask, p, c, W, a.W, a.D)];
+        }
+        build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
+        __syncthreads();
+        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row);
+        __syncthreads();
+        stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, kp4(taps * nk), np16(a.dc1), WL);
+        build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, -1);
+        __syncthreads();
+        gemm_any(GY, SY, 0, KT, kp4(taps * nk), WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false);
+        __syncthreads();
+        float* du = a.du1c[net] + (size_t)img * HW * a.dc1;
+        for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
+            const int p = e / a.dc1, c = e - p * a.dc1;
+            du[e] = GT[p * ST + c];
+        }
+    }
+}
+
+void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_lds_bwd, dim3(B, 2), dim3(BWT), a.lds_bytes, st, a);
+}
+
+// dst[net][i] += sum over images b (in order) of part[net][b][i], i < row; lo[net]: the net's first
+// canonical parameter (deterministic: one thread per element, fp64 sum in image order)
+__global__ __launch_bounds__(256) void k_grad_rows(const float* __restrict__ part, int B, int row, int64_t lo0,
+                                                   int64_t lo1, int len0, int len1, float* __restrict__ dparams) {
+    const int net = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int len = net == 0 ? len0 : len1;
+    if (i >= len) return;
+    const float* pr = part + (size_t)net * B * row + i;
+    double s = 0.0;
+    int b = 0;
+    for (; b + 4 <= B; b += 4) {
+        const float v0 = pr[(size_t)b * row], v1 = pr[(size_t)(b + 1) * row], v2 = pr[(size_t)(b + 2) * row],
+                    v3 = pr[(size_t)(b + 3) * row];
+        s += v0;
+        s += v1;
+        s += v2;
+        s += v3;
+    }
+    for (; b < B; b++) s += pr[(size_t)b * row];
+    float* d = dparams + (net == 0 ? lo0 : lo1) + i;
+    *d += (float)s;
+}
+
+void launch_grad_rows(const float* part, int B, int row, int64_t lo0, int64_t lo1, int len0, int len1, float* dparams,
+                      hipStream_t st) {
+    const int n = len0 > len1 ? len0 : len1;
+    hipLaunchKernelGGL(k_grad_rows, dim3((n + 255) / 256, 2), dim3(256), 0, st, part, B, row, lo0, lo1, len0, len1,
+                       dparams);
+}
+
+}  // namespace cnf

@@ -198,6 +198,23 @@ __device__ __forceinline__ void ln_apply(const float* src, int sstride, float* d
     }
 }
 
+// training forward: a raw LDS tensor [HW][sstride] (C channels) to its dense [HW][C] save slot
+__device__ __forceinline__ void save_tensor(const float* src, int sstride, int HW, int C, float* __restrict__ dst) {
+    if (((C | sstride) & 3) == 0) {
+        const int C4 = C >> 2, n4 = HW * C4;
+        for (int i = threadIdx.x; i < n4; i += NT) {
+            const int p = i / C4, c = (i - p * C4) << 2;
+            *reinterpret_cast<f4*>(dst + p * C + c) = *reinterpret_cast<const f4*>(src + p * sstride + c);
+        }
+        return;
+    }
+    const int n = HW * C;
+    for (int e = threadIdx.x; e < n; e += NT) {
+        const int p = e / C, c = e - p * C;
+        dst[e] = src[p * sstride + c];
+    }
+}
+
 // Register prefetch of the next full-width LayerNorm's gamma/beta quads i = u*NT + tid (u < GPF),
 // issued before the conv that produces the tensor and consumed by ln_full after it; quads beyond
 // the window are loaded on demand.
@@ -876,6 +893,8 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     float* ksb = KSP ? reinterpret_cast<float*>(smem + SA(off_ks)) : nullptr;
     const KSplit ks0{ksb, 0};
     float mu = 0.f, rstd = 1.f;
+    // training forward: this (net, image)'s save block (LdsSave), null in inference
+    float* const sv = a.save != nullptr ? a.save + ((size_t)net * gridDim.x + img) * a.save_img : nullptr;
     const int RB0 = 2;   // offs: [ci_w, ci_b, per rb: 10 + 2*nbr, ln_out_g, ln_out_b, co_w, co_b]
     const int per_rb = 10 + 2 * SA(nbr);
     auto rbo = [&](int r) { return off + RB0 + r * per_rb; };
@@ -1009,6 +1028,13 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         const int* o = rbo(r);
         // LN1(LReLU(y)) -> T2, conv_a (1x1 nk->nk) -> T1 (+ LN2 stats)
         if (ln) lst_final(slots, mu, rstd);
+        if (sv != nullptr) {   // y_r and LN1_r (Y is not written again before conv_b's barriers)
+            save_tensor(Y, SY, HW, nk, sv + (size_t)r * HW * nk);
+            if (threadIdx.x == 0) {
+                sv[a.save_st + 2 * r] = mu;
+                sv[a.save_st + 2 * r + 1] = rstd;
+            }
+        }
         STAMP(sti++);
         if (yq)
             ln_full(Y, SY, T2, S2, HW, nk, mu, rstd, lp, P + o[0], P + o[1]);
@@ -1031,6 +1057,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         // LN2(LReLU(t1)) in place on the channel windows the grouped branches read
         if (ln) lst_final(slots, mu, rstd);
+        if (sv != nullptr) {   // raw t1_r and LN2_r, before LN2 is applied in place
+            save_tensor(T1, S1, HW, nk, sv + a.save_t1 + (size_t)r * HW * nk);
+            if (threadIdx.x == 0) {
+                sv[a.save_st + 2 * (SA(R) + r)] = mu;
+                sv[a.save_st + 2 * (SA(R) + r) + 1] = rstd;
+            }
+            lds_barrier();
+        }
         STAMP(sti++);
         if (yq)
             ln_full(T1, S1, T1, S1, HW, nk, mu, rstd, lp, P + o[4], P + o[5]);
@@ -1085,6 +1119,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         STAMP(sti++);
         // LN3(LReLU(t2)) in place, conv_b (1x1 gc->nk) + shortcut -> Y (+ LN stats of Y)
         if (ln) lst_final(slots, mu, rstd);
+        if (sv != nullptr) {   // raw t2_r and LN3_r, before LN3 is applied in place
+            save_tensor(T2, S2, HW, gc, sv + a.save_t2 + (size_t)r * HW * gc);
+            if (threadIdx.x == 0) {
+                sv[a.save_st + 2 * (2 * SA(R) + r)] = mu;
+                sv[a.save_st + 2 * (2 * SA(R) + r) + 1] = rstd;
+            }
+            lds_barrier();
+        }
         STAMP(sti++);
         if (tq)
             ln_full(T2, S2, T2, S2, HW, gc, mu, rstd, lp, P + o[6], P + o[7]);
@@ -1113,6 +1155,14 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
     {
         const int* o = oend;
         if (ln) lst_final(slots, mu, rstd);
+        if (sv != nullptr) {   // y_R and LN_out, before LN_out is applied in place
+            save_tensor(Y, SY, HW, nk, sv + (size_t)SA(R) * HW * nk);
+            if (threadIdx.x == 0) {
+                sv[a.save_st + 6 * SA(R)] = mu;
+                sv[a.save_st + 6 * SA(R) + 1] = rstd;
+            }
+            lds_barrier();
+        }
         if (yq)
             ln_full(Y, SY, Y, SY, HW, nk, mu, rstd, lp, P + o[0], P + o[1]);
         else

@@ -313,6 +313,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
             for (int net = 0; net < 2; net++) {
                 NetParams& np = c.net[net];
                 std::string pre = "c" + std::to_string(c.index) + (net == 0 ? ".A" : ".b");
+                np.lo = p.n_params;
                 np.conv_in_k = add(pre + ".conv_in.kernel", {ks, ks, c.dc1, c.nk});
                 np.conv_in_b = add(pre + ".conv_in.bias", {c.nk});
                 const int nhw = c.hc * c.wc;
@@ -354,6 +355,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 np.conv_out_k = add(pre + ".conv_out.kernel", {ks, ks, c.nk, c.dc2});
                 np.conv_out_b = add(pre + ".conv_out.bias", {c.dc2});
                 if (net == 0) np.tanh_w = add(pre + ".tanh_scale.w", {});
+                np.hi = p.n_params;
             }
         }
 
@@ -957,6 +959,28 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.lds_offs.insert(c.lds_offs.end(), o.begin(), o.end());
             }
         }
+        // fused LDS-layer backward offset table (LDSBWD_* layout: canonical LN / range offsets, dense
+        // backward-image conv offsets)
+        require(p.n_bw < (1ll << 31), "dense backward image exceeds 2^31 floats");
+        for (auto& c : p.couplings) {
+            if (!c.use_lds) continue;
+            for (int net = 0; net < 2; net++) {
+                const NetParams& np = c.net[net];
+                std::vector<int> o = {(int)np.lo, (int)np.ci.dw, (int)np.ci.db, (int)np.ln_out_g, (int)np.ln_out_b,
+                                      (int)np.co.dw, (int)np.co.db, (int)np.tanh_w};
+                for (const auto& rb : np.rb) {
+                    for (int64_t v : {rb.ln1g, rb.ln1b, rb.ca.dw, rb.ca.db, rb.ln2g, rb.ln2b, rb.ln3g, rb.ln3b, rb.cb.dw,
+                                      rb.cb.db})
+                        o.push_back((int)v);
+                    for (const auto& g : rb.gc) {
+                        o.push_back((int)g.dw);
+                        o.push_back((int)g.db);
+                    }
+                }
+                c.bwd_offs_per_net = (int)o.size();
+                c.bwd_offs.insert(c.bwd_offs.end(), o.begin(), o.end());
+            }
+        }
 
         // squeeze/factor boundary maps. orig[i] = position in the xy layout of element i of
         // the current block layout: the forward's final restoration (:1762-1770) is the exact
@@ -1010,6 +1034,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
         for (auto& c : p.couplings) {
             c.dev_lds_offs = (int)p.host_table.size();
             p.host_table.insert(p.host_table.end(), c.lds_offs.begin(), c.lds_offs.end());
+            if (!c.bwd_offs.empty()) {
+                c.dev_bwd_offs = (int)p.host_table.size();
+                p.host_table.insert(p.host_table.end(), c.bwd_offs.begin(), c.bwd_offs.end());
+            }
             if (c.t1_compact) {
                 c.dev_t1_map = (int)p.host_table.size();
                 p.host_table.insert(p.host_table.end(), c.t1_map.begin(), c.t1_map.end());

@@ -58,6 +58,7 @@ struct NetParams {
     std::vector<RBParams> rb;
     int64_t ln_out_g = -1, ln_out_b = -1, conv_out_k = -1, conv_out_b = -1, tanh_w = -1;
     PackedConv ci, co;                         // conv_in (PK_KN), conv_out (PK_TAP or PK_KN)
+    int64_t lo = -1, hi = -1;                  // the net's canonical parameter range [lo, hi)
     PackedConv ci_pw;                          // streamed conv_in as a 1x1 over its 9*dc1 im2col row (PK_1X1; size 0: none)
     std::vector<PackedConv> co_chunks;         // streamed conv_out with > 64 outputs: 64-column PK_KN chunks
 };
@@ -86,6 +87,13 @@ struct Coupling {
     int ci_fmt = PK_KN, co_fmt = PK_KN;   // packed formats of conv_in / conv_out
     std::vector<int> gc_fmt;              // per grouped branch
     NetLdsGeom lds;                       // valid when use_lds
+    // training: the fused backward of a k_net_lds layer (cnf_ldsbwd.hip) when its LDS image fits
+    // (CNF_LDS_BWD=0 at plan creation: the multi-kernel backward); the training forward then saves the
+    // layer's raw activations (LdsSave) and s/t outputs for it
+    bool lds_bwd = false;
+    std::vector<int> bwd_offs;            // [net][bwd_offs_per_net] (LDSBWD_* layout)
+    int bwd_offs_per_net = 0;
+    int dev_bwd_offs = -1;
     // streamed layer: the grouped stage as k_gc launches (PK_Q4, padded cin), each over a group of
     // branches that fits one workgroup's LDS; branches in none run as k_pw tap-mode launches (k_conv<3>
     // when their im2col row is too long)
@@ -193,6 +201,11 @@ struct TrainLayout {
     size_t dy[2] = {}, dln[2] = {}, dbuf[2] = {}, dt1[2] = {}, dc[2] = {}, dt2[2] = {}, du1c[2] = {};
     size_t u1c = 0, duv[2] = {}, dzy = 0;
     size_t lnsum[2] = {}, wpart[2] = {}, bpart[2] = {}, lnpart[2] = {}, dwpart = 0;
+    // fused LDS-layer backward: per coupling index the forward's save area [2][B][LdsSave::img] and s/t
+    // outputs [2][B][hc][wc][dc2] (0: none), and the per-(net, image) gradient rows [2][B][row_max]
+    std::vector<size_t> act_save, so_save;
+    size_t rows = 0;
+    int row_max = 0;
 };
 
 struct Plan {
@@ -257,6 +270,9 @@ struct Plan {
 
 // cnf_train.cpp: dL/dparams of the NLL (loss scaled by inv_batch = 1 / global batch) into dparams,
 // from the coupling inputs saved by the training forward in `workspace`
+// fused LDS-layer backward geometry of coupling c (LDS layout, strides, shape fields of a); returns the
+// LDS bytes, 0 when it does not fit (cnf_train.cpp)
+size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a);
 typedef void (*LayerDoneFn)(void* user, int coupling_index);
 void flow_backward(Plan& p, const float* params, const float* xy, const float* zy, void* workspace, int B,
                    float inv_batch, float* dparams, hipStream_t st, const float* count = nullptr,

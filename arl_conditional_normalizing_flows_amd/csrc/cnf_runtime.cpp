@@ -617,8 +617,11 @@ static double net_flops(const Coupling& c) {
 // layers only). defer: leave this layer's own coupling pending (no k_coupling launch) and describe it
 // in *out_pend for the next layer's k_net_lds (the caller allows it only when that layer is an LDS
 // layer of the same forward).
+// save / so_save (training forward of a layer with the fused LDS backward): k_net_lds also writes the
+// raw activations and LN statistics to save (LdsSave blocks) and its s / t outputs to so_save[2]
 static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir,
-                         const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr) {
+                         const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr,
+                         float* save = nullptr, float* const* so_save = nullptr) {
     const int B = E.B;
     const WsLayout& L = E.L;
     const float* P = E.params;
@@ -630,8 +633,10 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // k_net_lds layers alternate between two s/t sets by coupling index, so a layer applying its
     // predecessor's deferred coupling never writes the set it reads
     const bool alt = c.use_lds && (c.index & 1) != 0;
-    float* so0 = E.at<float>(alt ? L.so_alt[0] : L.so[0]);
-    float* so1 = E.at<float>(alt ? L.so_alt[1] : L.so[1]);
+    float* so0 = so_save ? so_save[0] : E.at<float>(alt ? L.so_alt[0] : L.so[0]);
+    float* so1 = so_save ? so_save[1] : E.at<float>(alt ? L.so_alt[1] : L.so[1]);
+    if (save != nullptr && (!c.use_lds || so_save == nullptr || defer))
+        throw std::logic_error("training save: k_net_lds layers without a deferred law only");
     if ((pend != nullptr || defer) && !c.use_lds)
         throw std::logic_error("deferred couplings are only fused into k_net_lds layers");
     if (pend != nullptr && pend->dir != dir) throw std::logic_error("deferred coupling of the other direction");
@@ -649,6 +654,14 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         na.offs = E.p.dtab(c.dev_lds_offs);
         for (int n = 0; n < 2; n++) na.ci_off[n] = E.p.host_table[(size_t)c.dev_lds_offs + (size_t)n * na.offs_per_net];
         na.zero_bias = X + E.p.aux_zero;
+        if (save != nullptr) {
+            const LdsSave s = LdsSave::of(c.hc * c.wc, c.nk, c.gc, c.R);
+            na.save = save;
+            na.save_img = s.img;
+            na.save_t1 = s.t1;
+            na.save_t2 = s.t2;
+            na.save_st = s.st;
+        }
         if (pend != nullptr) {
             // buffer discipline of the deferred law (dry runs carry no real pointers): this layer's
             // input is the pending layer's output v_k, which must not be the u_k it is computed
@@ -1020,6 +1033,13 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     if (const char* e = std::getenv("CNF_TAP_PW")) p->tap_pw = std::atoi(e) != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
+    // training: k_net_lds layers whose fused backward fits LDS use it (CNF_LDS_BWD=0: none, A/B knob)
+    bool lds_bwd = true;
+    if (const char* e = std::getenv("CNF_LDS_BWD")) lds_bwd = std::atoi(e) != 0;
+    for (auto& c : p->couplings) {
+        LdsBwdArgs a;
+        c.lds_bwd = lds_bwd && c.use_lds && ldsbwd_setup(*p, c, a) > 0;
+    }
     *out = new cnf_plan{p};
     return CNF_OK;
     CNF_CATCH
@@ -1159,8 +1179,15 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
                 });
             }
             CoupPend next;
+            float* save = nullptr;
+            float* so_save[2] = {nullptr, nullptr};
+            if (save_inputs && c.lds_bwd) {   // the fused LDS backward's activations
+                save = E.at<float>(TL.act_save[c.index]);
+                so_save[0] = E.at<float>(TL.so_save[c.index]);
+                so_save[1] = so_save[0] + (size_t)B * c.hc * c.wc * c.dc2;
+            }
             run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1, have_pend ? &pend : nullptr,
-                         defer, &next);
+                         defer, &next, save, save ? so_save : nullptr);
             pend = next;
             have_pend = defer;
             cur = nxt;

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -46,6 +47,86 @@ int wgrad_chunks(int B, int npx) {
 }
 
 }  // namespace
+
+// LDS pixel stride for C channels: a multiple of 4 floats (16-byte quads), odd in quads
+static int bwd_stride(int C) {
+    int s = (C + 3) / 4 * 4;
+    if (s % 8 == 0) s += 4;
+    return s;
+}
+
+size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
+    std::memset(&a, 0, sizeof(a));
+    if (!c.use_lds || (int)c.br.size() > NETLDS_MAXBR || c.bwd_offs_per_net == 0) return 0;
+    const int ks = p.desc.ksize, taps = ks * ks;
+    if (taps != 1 && taps != 9) return 0;
+    for (const Branch& b : c.br)
+        if (b.dil > 32) return 0;
+    a.H = c.H;
+    a.W = c.W;
+    a.D = c.D;
+    a.mask = c.mask;
+    a.hc = c.hc;
+    a.wc = c.wc;
+    a.dc1 = c.dc1;
+    a.dc2 = c.dc2;
+    a.nk = c.nk;
+    a.gc = c.gc;
+    a.R = c.R;
+    a.nbr = (int)c.br.size();
+    a.ln = p.desc.layer_norm;
+    a.taps = taps;
+    for (int i = 0; i < a.nbr; i++) {
+        a.br_cin_off[i] = c.br[i].cin_off;
+        a.br_cin[i] = c.br[i].cin;
+        a.br_cout[i] = c.br[i].cout;
+        a.br_out_off[i] = c.br[i].out_off;
+        a.br_dil[i] = c.br[i].dil;
+    }
+    const int HW = c.hc * c.wc;
+    const int ac = std::max(std::max(c.nk, c.dc1), 4);
+    a.sy = bwd_stride(c.nk);
+    a.st = bwd_stride(std::max(std::max(c.gc, c.nk), std::max(c.dc2, c.dc1)));
+    a.sa = bwd_stride(ac);
+    a.ac_chunk = std::min(c.gc, ac / 4 * 4);
+    auto kp4 = [](int K) { return (K + 3) / 4 * 4; };
+    auto np16 = [](int N) { return (N + 15) / 16 * 16; };
+    // transposed-weight images of the data gradients, and the k-table lengths of every conv
+    size_t wmax = (size_t)kp4(taps * c.dc2) * np16(c.nk);
+    wmax = std::max(wmax, (size_t)kp4(c.nk) * np16(c.gc));
+    wmax = std::max(wmax, (size_t)kp4(c.nk) * np16(c.nk));
+    wmax = std::max(wmax, (size_t)kp4(taps * c.nk) * np16(c.dc1));
+    int ktmax = std::max(kp4(taps * c.nk), std::max(kp4(taps * c.dc2), kp4(taps * c.dc1)));
+    ktmax = std::max(ktmax, std::max(kp4(c.nk), kp4(a.ac_chunk)));
+    for (const Branch& b : c.br) {
+        wmax = std::max(wmax, (size_t)kp4(taps * b.cout) * np16(b.cin));
+        ktmax = std::max(ktmax, std::max(kp4(taps * b.cout), kp4(taps * b.cin)));
+    }
+    auto al = [](size_t v) { return (v + 15) / 16 * 16; };
+    size_t off = al((size_t)HW * a.sy * 4);
+    a.off_gt = (int)off;
+    off = al(off + (size_t)HW * a.st * 4);
+    a.off_ac = (int)off;
+    off = al(off + (size_t)HW * a.sa * 4);
+    a.off_w = (int)off;
+    off = al(off + wmax * 4);
+    a.off_kt = (int)off;
+    off = al(off + (size_t)ktmax * 4);
+    a.off_red = (int)off;
+    off = al(off + 16 * 8);
+    a.off_ot = (int)off;
+    off = al(off + (size_t)c.bwd_offs_per_net * 4);
+    if (off > 160 * 1024) return 0;
+    a.lds_bytes = (int)off;
+    a.offs_per_net = c.bwd_offs_per_net;
+    const LdsSave s = LdsSave::of(HW, c.nk, c.gc, c.R);
+    a.save_img = s.img;
+    a.save_t1 = s.t1;
+    a.save_t2 = s.t2;
+    a.save_st = s.st;
+    a.row = (int)std::max(c.net[0].hi - c.net[0].lo, c.net[1].hi - c.net[1].lo);
+    return off;
+}
 
 TrainLayout Plan::train_layout(int B) const {
     TrainLayout T;
@@ -112,6 +193,17 @@ TrainLayout Plan::train_layout(int B) const {
         T.bpart[n] = take((size_t)chunks * m_co * 4);
     }
     T.dwpart = take(Bz * std::max(1, L.ld_parts) * 8);
+    T.act_save.assign(couplings.size(), 0);
+    T.so_save.assign(couplings.size(), 0);
+    for (const Coupling& c : couplings) {
+        if (!c.lds_bwd) continue;
+        const int HW = c.hc * c.wc;
+        const LdsSave s = LdsSave::of(HW, c.nk, c.gc, c.R);
+        T.act_save[c.index] = take(2 * Bz * s.img * 4);
+        T.so_save[c.index] = take(2 * Bz * HW * c.dc2 * 4);
+        T.row_max = std::max<int>(T.row_max, (int)std::max(c.net[0].hi - c.net[0].lo, c.net[1].hi - c.net[1].lo));
+    }
+    if (T.row_max > 0) T.rows = take(2 * Bz * T.row_max * 4);
     T.total = off;
     return T;
 }
@@ -313,6 +405,61 @@ void stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
 // nets are independent until the coupling law joins them, so net b's recompute and backward chain run
 // on the plan's side stream (its own scratch set) while net A's run on the caller's stream: the many
 // small, latency-bound launches of the two chains overlap.
+// the fused backward of a k_net_lds layer (cnf_ldsbwd.hip) from the activations the training forward
+// saved: coupling law backward, one k_lds_bwd launch for both nets, the batch sum of the gradient rows
+void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
+    const int B = E.B;
+    const float* P = E.params;
+    const float* so0 = E.at<float>(E.T.so_save[c.index]);
+    const size_t so_n = (size_t)B * c.hc * c.wc * c.dc2;
+    {
+        CoupBwArgs a{};
+        a.u = u;
+        a.dv = dv;
+        a.s_pre = so0;
+        a.tanh_w = P + c.net[0].tanh_w;
+        a.du = du;
+        a.ds_pre = E.at<float>(E.T.dso[0]);
+        a.dt = E.at<float>(E.T.dso[1]);
+        a.dw_part = E.at<double>(E.T.dwpart);
+        a.g_ld = -E.inv_batch_;
+        a.count = E.count;
+        a.H = c.H;
+        a.W = c.W;
+        a.D = c.D;
+        a.mask = c.mask;
+        a.mask_c = c.mask_c;
+        a.hc = c.hc;
+        a.wc = c.wc;
+        a.dc1 = c.dc1;
+        a.dc2 = c.dc2;
+        const int np = std::max(1, E.L.ld_parts);
+        launch_coupling_backward(a, B, np, E.st);
+        launch_dsum(a.dw_part, (long long)B * np, E.dparams + c.net[0].tanh_w, E.st);
+    }
+    (void)so_n;
+    LdsBwdArgs a;
+    if (ldsbwd_setup(E.p, c, a) == 0) throw std::logic_error("fused LDS backward planned for a layer it does not fit");
+    a.save = E.at<float>(E.T.act_save[c.index]);
+    a.dso[0] = E.at<float>(E.T.dso[0]);
+    a.dso[1] = E.at<float>(E.T.dso[1]);
+    a.u = u;
+    a.du1c[0] = E.at<float>(E.T.du1c[0]);
+    a.du1c[1] = E.at<float>(E.T.du1c[1]);
+    a.params = P;
+    a.bw = E.bw();
+    a.bw_map = E.p.dev_bw_map;
+    a.offs = E.p.dev_table + c.dev_bwd_offs;
+    a.part = E.at<float>(E.T.rows);
+    a.row = E.T.row_max;
+    launch_lds_bwd(a, B, E.st);
+    const NetParams& n0 = c.net[0];
+    const NetParams& n1 = c.net[1];
+    launch_grad_rows(a.part, B, a.row, n0.lo, n1.lo, (int)(n0.hi - n0.lo), (int)(n1.hi - n1.lo), E.dparams, E.st);
+    launch_scatter_add_u1c(a.du1c[0], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
+    launch_scatter_add_u1c(a.du1c[1], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
+}
+
 void coupling_backward(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
     const int B = E.B, h = c.hc, w = c.wc, nk = c.nk, gc = c.gc, R = c.R;
     const int64_t npx = (int64_t)h * w;
@@ -482,7 +629,10 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
             float* nxt = buf[which];
-            coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
+            if (c.lds_bwd)
+                coupling_backward_lds(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
+            else
+                coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
             // every launch writing this layer's parameter gradients is ordered before anything enqueued
             // on st from here (its side streams joined st): the caller may reduce them now
             if (done != nullptr) done(user, c.index);

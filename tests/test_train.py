@@ -148,6 +148,9 @@ GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'in
               ('narrow', 3, {}),
               # every training convolution on the VALU kernels (k_tconv, k_wgrad; CNF_TRAIN_VALU=1, read per call)
               ('small', 3, {'_env': {'CNF_TRAIN_VALU': '1'}}),
+              # the multi-kernel backward for the k_net_lds layers too (CNF_LDS_BWD=0 at plan creation; by
+              # default they run the fused k_lds_bwd over the training forward's saved activations)
+              ('small', 3, {'_plan_env': {'CNF_LDS_BWD': '0'}}), ('cfg2', 2, {'_plan_env': {'CNF_LDS_BWD': '0'}}),
               # the benched training batch (bench.py --mode train): the batch-sliced LN backward (up to 8
               # workgroups per image), the multi-unit band weight gradients and the four-stream schedule
               # all see their full-size partitions only here
@@ -163,6 +166,7 @@ def test_gradients_match_oracle(gpu, name, B, extra):
     import os
     extra = dict(extra)
     env = extra.pop('_env', {})
+    plan_env = extra.pop('_plan_env', {})
     cfg = PRESETS[name]
     kw = dict(cfg.kwargs(), **extra)
     ora = OracleCFlow(**kw)
@@ -180,7 +184,12 @@ def test_gradients_match_oracle(gpu, name, B, extra):
                 Gp, _ = oracle_grads(kw, P, np.asarray(xy, np.float64) * (1.0 + eps * rng.standard_normal(xy.shape)))
                 for k in G_spread:
                     G_spread[k] = np.maximum(G_spread[k], np.abs(Gp[k].reshape(-1) - G_ref[k].reshape(-1)))
-    flow = _gpu_flow(kw, P, gpu)
+    os.environ.update(plan_env)
+    try:
+        flow = _gpu_flow(kw, P, gpu)
+    finally:
+        for k in plan_env:
+            os.environ.pop(k, None)
     os.environ.update(env)
     try:
         g, terms = flow.gradients(torch.from_numpy(xy).to(gpu))
