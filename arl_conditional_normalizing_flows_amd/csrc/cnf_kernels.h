@@ -310,6 +310,9 @@ void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int
 // LN partial slots [B][part_stride][LNP] of one tensor (two nets: part0, part1 or null) merged into
 // slot 0 of each image (k_ln_merge): consumers then read nparts = 1
 void launch_ln_merge(float* part0, float* part1, int nparts, int part_stride, int B, hipStream_t st);
+// (mean, rstd) [B][2] per net of one LN tensor from its producer's partial slots (as in_ln)
+void launch_ln_final(const float* part0, const float* part1, int nparts, int part_stride, int B, float* st0, float* st1,
+                     hipStream_t st);
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st);
 void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
                         int B, hipStream_t st);
@@ -437,9 +440,12 @@ struct LdsBwdArgs {
     int br_cin_off[NETLDS_MAXBR], br_cin[NETLDS_MAXBR], br_cout[NETLDS_MAXBR], br_out_off[NETLDS_MAXBR],
         br_dil[NETLDS_MAXBR];
     int sy, st, sa, ac_chunk;                                   // LDS pixel strides (floats); conv_b staging chunk
-    int off_gt, off_ac, off_w, off_kt, off_red, off_ot, lds_bytes;   // LDS byte offsets (GY at 0)
+    int wmax;                                                   // floats of the W region (weight-gradient scratch too)
+    int stamps;                                                 // diagnostics: phase clock stamps (CNF_LDSBWD_STAMPS)
+    int off_gt, off_ac, off_w, off_kt, off_red, off_ot, off_z, lds_bytes;   // LDS byte offsets (GY at 0)
 };
 void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st);
+int read_bwd_stamps(long long* host, int n);   // [0] = count, [1..] = s_memtime per phase boundary
 // dparams[lo_n + i] += sum_b part[n][b][i] (i < len_n, n = 0, 1; row floats per (net, image) row)
 void launch_grad_rows(const float* part, int B, int row, int64_t lo0, int64_t lo1, int len0, int len1, float* dparams,
                       hipStream_t st);

@@ -50,34 +50,57 @@ __device__ __forceinline__ void build_kt(int* kt, int K, int Kp, int cpt, int ta
 }
 
 // A(p, k) of a k-table entry t for pixel (pr, pc): a[(p + shift) * sa + a_off + c], 0 outside the image
+constexpr int KT_ONE = -2;   // k-table entry of the bias row of a weight gradient: A = 1
+
 __device__ __forceinline__ float kt_load(const float* a, int sa, int a_off, int t, int pr, int pc, int H, int W) {
-    if (t < 0) return 0.f;
+    if (t < 0) return t == KT_ONE ? 1.f : 0.f;
     const int y = pr + (t & 127) - 64, x = pc + ((t >> 7) & 127) - 64;
     if ((unsigned)y >= (unsigned)H || (unsigned)x >= (unsigned)W) return 0.f;
     return a[(y * W + x) * sa + a_off + (t >> 14)];
 }
 
+// LDS address of A(p, k) for k-table entry t and pixel (pr, pc) (pv: the pixel exists): the element,
+// else the zero slot Z, or the one slot Z + 4 for the bias row (t == KT_ONE) — every operand is a load,
+// so a group's loads issue together with no branch between them
+__device__ __forceinline__ const float* kt_ptr(const float* a, int sa, int a_off, int t, int pr, int pc, bool pv,
+                                               int H, int W, const float* Z) {
+    const int y = pr + (t & 127) - 64, x = pc + ((t >> 7) & 127) - 64;
+    const bool in = t >= 0 && pv && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    return in ? a + (y * W + x) * sa + a_off + (t >> 14) : (t == KT_ONE && pv ? Z + 4 : Z);
+}
+
 // out[p][o_off + n] (= or +=) sum_k A(p, k) * Wl[k][n] for n < N: units of one 16-pixel subtile x
-// NR 16-column blocks, dealt round-robin over the waves (acc[m][r] = out[p0 + 4kq + r][n0 + 16m + i16])
+// NR 16-column blocks, dealt round-robin over the waves (acc[m][r] = out[p0 + 4kq + r][n0 + 16m + i16]).
+// K in groups of four MFMA steps: the group's table entries, then its A and B loads, then its MFMAs.
 template <int NR>
 __device__ void gemm_px(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np, float* out,
-                        int so, int o_off, int N, int H, int W, bool accum) {
+                        int so, int o_off, int N, int H, int W, bool accum, const float* Z) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W, nsub = (HW + 15) >> 4, ngrp = (np / 16 + NR - 1) / NR;
     for (int unit = wave; unit < nsub * ngrp; unit += BWN) {
         const int s = unit % nsub, n0 = (unit / nsub) * 16 * NR;
         const int p = s * 16 + i16;
         const bool pv = p < HW;
-        const int pr = pv ? p / W : -4096, pc = pv ? p - (p / W) * W : -4096;
+        const int pr = pv ? p / W : 0, pc = pv ? p - (p / W) * W : 0;
         f4 acc[NR];
 #pragma unroll
         for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
-        for (int k0 = 0; k0 < Kp; k0 += 4) {
-            const float av = kt_load(a, sa, a_off, kt[k0 + kq], pr, pc, H, W);
-            const float* brow = wl + (size_t)(k0 + kq) * np + n0 + i16;
+        for (int k0 = 0; k0 < Kp; k0 += 16) {
+            int t[4];
 #pragma unroll
-            for (int m = 0; m < NR; m++)
-                if (n0 + 16 * m < np) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, brow[16 * m], acc[m], 0, 0, 0);
+            for (int j = 0; j < 4; j++) t[j] = k0 + 4 * j < Kp ? kt[k0 + 4 * j + kq] : -1;
+            float av[4], bv[4][NR];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                av[j] = *kt_ptr(a, sa, a_off, t[j], pr, pc, pv, H, W, Z);
+                const int kr = min(k0 + 4 * j, Kp - 4) + kq;   // (rows past Kp: A is 0)
+#pragma unroll
+                for (int m = 0; m < NR; m++) bv[j][m] = n0 + 16 * m < np ? wl[(size_t)kr * np + n0 + 16 * m + i16] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int m = 0; m < NR; m++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j][m], acc[m], 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -95,68 +118,80 @@ __device__ void gemm_px(const float* a, int sa, int a_off, const int* kt, int Kp
 }
 
 __device__ __forceinline__ void gemm_any(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np,
-                                         float* out, int so, int o_off, int N, int H, int W, bool accum) {
+                                         float* out, int so, int o_off, int N, int H, int W, bool accum, const float* Z) {
     if (np <= 16)
-        gemm_px<1>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+        gemm_px<1>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
     else if (np <= 32)
-        gemm_px<2>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+        gemm_px<2>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
     else
-        gemm_px<4>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum);
+        gemm_px<4>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
 }
 
 // dW[k][n] = sum_p A(p, k) * G[p][g_off + n] (k < K = taps * cin flat, n < N) for this image, stored to
-// row[bw_map[dw + k * N + n] - lo]; the bias gradient sum_p G[p][n] to row[bw_map[db + n] - lo].
-// Units: (16-row k block, 16-column n block); the pixel loop alternates two accumulators.
+// row[bw_map[dw + k * N + n] - lo]; with db >= 0 the bias gradient sum_p G[p][n] comes out of the same
+// MFMAs as an extra row k = K of A = 1, stored to row[bw_map[db + n] - lo]. Units: (16-row k block,
+// 16-column n block, pixel slice): the pixels are split into S slices when the tiles alone would
+// leave waves idle, their partial tiles summed in slice order through scr (scr_floats of LDS). Pixels
+// in groups of four MFMA steps: the group's A and G loads (branch-free, the row from a float
+// reciprocal of W) issue together, then four MFMAs into four accumulators.
 __device__ void wgrad_px(const float* a, int sa, int a_off, const int* kt, int K, const float* g, int sg, int g_off,
                          int N, int H, int W, const int64_t* __restrict__ bw_map, int64_t dw, int64_t db, int64_t lo,
-                         float* __restrict__ row) {
+                         float* __restrict__ row, float* scr, int scr_floats, const float* Z) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
-    const int HW = H * W, nkb = (K + 15) >> 4, nnb = (N + 15) >> 4;
-    for (int unit = wave; unit < nkb * nnb; unit += BWN) {
-        const int k0 = (unit % nkb) * 16, n0 = (unit / nkb) * 16;
-        const int t = k0 + i16 < K ? kt[k0 + i16] : -1;
-        const int n = n0 + i16;
-        const bool nv = n < N;
-        f4 acc0 = f4{0.f, 0.f, 0.f, 0.f}, acc1 = f4{0.f, 0.f, 0.f, 0.f};
-        int pr = 0, pc = kq;   // pixel p = p0 + kq, tracked incrementally
-        while (pc >= W) {
-            pc -= W;
-            pr++;
-        }
-        for (int p0 = 0; p0 < HW; p0 += 8) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int p = p0 + 4 * h + kq;
-                const bool pv = p < HW;
-                const float av = pv ? kt_load(a, sa, a_off, t, pr, pc, H, W) : 0.f;
-                const float bv = (pv && nv) ? g[p * sg + g_off + n] : 0.f;
-                if (h == 0)
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
-                else
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
-                pc += 4;
-                while (pc >= W) {
-                    pc -= W;
-                    pr++;
-                }
-            }
-        }
-        // acc[r] = dW[k0 + 4kq + r][n]
+    const int HW = H * W, Kb = K + (db >= 0 ? 1 : 0), nkb = (Kb + 15) >> 4, nnb = (N + 15) >> 4, tiles = nkb * nnb;
+    int S = 1;
+    while (tiles * S < 2 * BWN && 2 * S * 16 <= HW && tiles * 2 * S * 256 <= scr_floats) S *= 2;
+    const int q = ((HW + S - 1) / S + 15) / 16 * 16;   // pixels per slice
+    const float invW = 1.f / (float)W;
+    auto store = [&](int tile, const f4& v) {
+        const int k0 = (tile % nkb) * 16, n = (tile / nkb) * 16 + i16;
+        if (n >= N) return;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int k = k0 + 4 * kq + r;
-            if (k < K && nv) {
-                const int64_t dst = bw_map[dw + (int64_t)k * N + n];
-                if (dst >= 0) row[dst - lo] = acc0[r] + acc1[r];
-            }
+            int64_t dst = -1;
+            if (k < K)
+                dst = bw_map[dw + (int64_t)k * N + n];
+            else if (k == K && db >= 0)
+                dst = bw_map[db + n];
+            if (dst >= 0) row[dst - lo] = v[r];
         }
+    };
+    for (int unit = wave; unit < tiles * S; unit += BWN) {
+        const int tile = unit % tiles, s = unit / tiles;
+        const int k = (tile % nkb) * 16 + i16, n = (tile / nkb) * 16 + i16;
+        const int t = k < K ? kt[k] : (k == K && db >= 0 ? KT_ONE : -1);
+        const bool nv = n < N;
+        const int p_lo = s * q, p_hi = min(HW, p_lo + q);
+        f4 acc[4];
+#pragma unroll
+        for (int h = 0; h < 4; h++) acc[h] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int p0 = p_lo; p0 < p_hi; p0 += 16) {
+            float av[4], bv[4];
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int p = p0 + 4 * h + kq;
+                const bool pv = p < p_hi;
+                const int pr = (int)(((float)p + 0.5f) * invW), pc = p - pr * W;
+                av[h] = *kt_ptr(a, sa, a_off, t, pr, pc, pv, H, W, Z);
+                bv[h] = *((pv && nv) ? g + p * sg + g_off + n : Z);
+            }
+#pragma unroll
+            for (int h = 0; h < 4; h++) acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[h], bv[h], acc[h], 0, 0, 0);
+        }
+        const f4 v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        if (S == 1)
+            store(tile, v);
+        else
+            *reinterpret_cast<f4*>(scr + ((size_t)unit * 64 + lane) * 4) = v;
     }
-    if (db < 0) return;   // (a later row chunk of the same conv: its bias went with the first)
-    for (int j = threadIdx.x; j < N; j += BWT) {
-        float s = 0.f;
-        for (int p = 0; p < HW; p++) s += g[p * sg + g_off + j];
-        const int64_t dst = bw_map[db + j];
-        if (dst >= 0) row[dst - lo] = s;
+    if (S > 1) {
+        __syncthreads();
+        for (int tile = wave; tile < tiles; tile += BWN) {
+            f4 v = *reinterpret_cast<const f4*>(scr + ((size_t)tile * 64 + lane) * 4);
+            for (int s = 1; s < S; s++) v += *reinterpret_cast<const f4*>(scr + ((size_t)(s * tiles + tile) * 64 + lane) * 4);
+            store(tile, v);
+        }
     }
 }
 
@@ -199,11 +234,14 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
 // LayerNorm(LeakyReLU) backward of one image (as k_lnb_reduce / k_lnb_apply): d = dL/d(LN output) in
 // LDS ([HW][sd] at d_off, C channels), x the raw input (global, dense [HW][C]), gamma the per-element
 // scale; dx = dL/dx to out ([HW][so] at o_off, stored or added), and the image's dgamma = d * xhat,
-// dbeta = d to its row. ln == false: LeakyReLU only.
+// dbeta = d to its row. ln == false: LeakyReLU only. Channel quads when C % 4 == 0, LU of them per
+// thread with all their global loads issued before any is used (the passes are latency-bound).
+constexpr int LU = 8;
 __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const float* __restrict__ gam, const float* d,
                        int sd, int d_off, float* out, int so, int o_off, bool accum, int HW, int C, bool ln,
                        float* __restrict__ rg, float* __restrict__ rb, double* red) {
     const int n = HW * C;
+    const bool vq = ((C | sd | d_off | so | o_off) & 3) == 0;
     if (!ln) {
         for (int e = threadIdx.x; e < n; e += BWT) {
             const int p = e / C, c = e - p * C;
@@ -215,26 +253,85 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
         return;
     }
     double sg = 0.0, sgh = 0.0;
-    for (int e = threadIdx.x; e < n; e += BWT) {
-        const int p = e / C, c = e - p * C;
-        const float xh = (lrelu_b(x[e]) - mu) * rs;
-        const float g = d[p * sd + d_off + c] * gam[e];
-        sg += g;
-        sgh += (double)g * xh;
+    const int C4 = C >> 2, n4 = n >> 2;
+    const f4* x4 = reinterpret_cast<const f4*>(x);
+    if (vq) {
+        for (int i0 = threadIdx.x; i0 < n4; i0 += LU * BWT) {
+            f4 xv[LU], gv[LU];
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                xv[u] = i < n4 ? x4[i] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < 4; j++) gv[u][j] = i < n4 ? gam[4 * i + j] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                if (i >= n4) break;
+                const int p = i / C4, c = (i - p * C4) << 2;
+                const f4 dv = *reinterpret_cast<const f4*>(d + p * sd + d_off + c);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float xh = (lrelu_b(xv[u][j]) - mu) * rs;
+                    const float g = dv[j] * gv[u][j];
+                    sg += g;
+                    sgh += (double)g * xh;
+                }
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += BWT) {
+            const int p = e / C, c = e - p * C;
+            const float xh = (lrelu_b(x[e]) - mu) * rs;
+            const float g = d[p * sd + d_off + c] * gam[e];
+            sg += g;
+            sgh += (double)g * xh;
+        }
     }
     block_sum2(sg, sgh, red);
     const float inv_n = 1.f / (float)n;
     const float mg = (float)(sg * inv_n), mgh = (float)(sgh * inv_n);
-    for (int e = threadIdx.x; e < n; e += BWT) {
-        const int p = e / C, c = e - p * C;
-        const float xv = x[e];
-        const float xh = (lrelu_b(xv) - mu) * rs;
-        const float dv = d[p * sd + d_off + c];
-        rg[e] = dv * xh;
-        rb[e] = dv;
-        const float v = rs * (dv * gam[e] - mg - xh * mgh) * lrelu_d(xv);
-        float* o = out + p * so + o_off + c;
-        *o = accum ? *o + v : v;
+    if (vq) {
+        for (int i0 = threadIdx.x; i0 < n4; i0 += LU * BWT) {
+            f4 xv[LU], gv[LU];
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                xv[u] = i < n4 ? x4[i] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < 4; j++) gv[u][j] = i < n4 ? gam[4 * i + j] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                if (i >= n4) break;
+                const int p = i / C4, c = (i - p * C4) << 2;
+                const f4 dv = *reinterpret_cast<const f4*>(d + p * sd + d_off + c);
+                f4* o = reinterpret_cast<f4*>(out + p * so + o_off + c);
+                f4 ov = accum ? *o : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float xh = (lrelu_b(xv[u][j]) - mu) * rs;
+                    rg[4 * i + j] = dv[j] * xh;
+                    rb[4 * i + j] = dv[j];
+                    ov[j] += rs * (dv[j] * gv[u][j] - mg - xh * mgh) * lrelu_d(xv[u][j]);
+                }
+                *o = ov;
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += BWT) {
+            const int p = e / C, c = e - p * C;
+            const float xv = x[e];
+            const float xh = (lrelu_b(xv) - mu) * rs;
+            const float dv = d[p * sd + d_off + c];
+            rg[e] = dv * xh;
+            rb[e] = dv;
+            const float v = rs * (dv * gam[e] - mg - xh * mgh) * lrelu_d(xv);
+            float* o = out + p * so + o_off + c;
+            *o = accum ? *o + v : v;
+        }
     }
     __syncthreads();
 }
@@ -243,6 +340,38 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
 // x (global, dense) into dst [HW][sd] from channel 0
 __device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, int HW, float mu, float rs,
                           const float* __restrict__ gam, const float* __restrict__ bet, bool ln, float* dst, int sd) {
+    if (((C | c0 | nc | sd) & 3) == 0) {
+        const int nq = nc >> 2, n4 = HW * nq;
+        for (int i0 = threadIdx.x; i0 < n4; i0 += LU * BWT) {
+            f4 xv[LU], gv[LU], bv[LU];
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                const int p = i / nq, c = (i - p * nq) << 2;
+                const size_t gi = (size_t)p * C + c0 + c;
+                xv[u] = i < n4 ? *reinterpret_cast<const f4*>(x + gi) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    gv[u][j] = (ln && i < n4) ? gam[gi + j] : 0.f;
+                    bv[u][j] = (ln && i < n4) ? bet[gi + j] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * BWT;
+                if (i >= n4) break;
+                const int p = i / nq, c = (i - p * nq) << 2;
+                f4 v;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float h = lrelu_b(xv[u][j]);
+                    v[j] = ln ? (h - mu) * rs * gv[u][j] + bv[u][j] : h;
+                }
+                *reinterpret_cast<f4*>(dst + p * sd + c) = v;
+            }
+        }
+        return;
+    }
     const int n = HW * nc;
     for (int e = threadIdx.x; e < n; e += BWT) {
         const int p = e / nc, c = e - p * nc;
@@ -266,6 +395,15 @@ __device__ __forceinline__ int mask_pos_b(int m, int p, int c, int wc, int W, in
 
 }  // namespace
 
+// diagnostics (LdsBwdArgs::stamps != 0): thread 0 of workgroup (0, 0) records the shader clock at every
+// phase boundary of the last k_lds_bwd launch (cnf_debug_read_bwd_stamps)
+__device__ long long g_bwd_stamps[128];
+#define BSTAMP()                                                                                     \
+    do {                                                                                              \
+        if (a.stamps && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && nst < 127)          \
+            g_bwd_stamps[1 + nst++] = (long long)__builtin_amdgcn_s_memtime();                         \
+    } while (0)
+
 // offsets table per net (LdsBwdArgs::offs): see LDSBWD_* in cnf_kernels.h
 __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -279,9 +417,14 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     int* KT = reinterpret_cast<int*>(smem + a.off_kt);
     double* RED = reinterpret_cast<double*>(smem + a.off_red);
     int* OT = reinterpret_cast<int*>(smem + a.off_ot);
+    float* ZQ = reinterpret_cast<float*>(smem + a.off_z);   // 4 zeros, then 4 ones (kt_ptr)
+    if (threadIdx.x < 8) ZQ[threadIdx.x] = threadIdx.x < 4 ? 0.f : 1.f;
     const int SY = a.sy, ST = a.st, SA = a.sa;
+    int nst = 0;
+    BSTAMP();
     for (int i = threadIdx.x; i < a.offs_per_net; i += BWT) OT[i] = a.offs[net * a.offs_per_net + i];
     __syncthreads();
+        BSTAMP();
     const int64_t lo = OT[LDSBWD_LO];
     const float* sv = a.save + ((size_t)net * B + img) * a.save_img;
     const float* st = sv + a.save_st;
@@ -307,16 +450,21 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
                   ln, AC, SA);
         build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
         __syncthreads();
-        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row);
+        BSTAMP();
+        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row, WL, a.wmax, ZQ);
         __syncthreads();
+        BSTAMP();
         stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, kp4(taps * a.dc2), np16(nk), WL);
         build_kt(KT, taps * a.dc2, kp4(taps * a.dc2), a.dc2, taps, 1, -1);
         __syncthreads();
-        gemm_any(GT, ST, 0, KT, kp4(taps * a.dc2), WL, np16(nk), GY, SY, 0, nk, H, W, false);
+        BSTAMP();
+        gemm_any(GT, ST, 0, KT, kp4(taps * a.dc2), WL, np16(nk), GY, SY, 0, nk, H, W, false, ZQ);
         __syncthreads();
+        BSTAMP();
         // LN_out backward in place on GY
         ln_bwd(yR, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, GY, SY, 0, GY, SY, 0, false, HW, nk, ln,
                ln ? row + (OT[LDSBWD_LNO_G] - lo) : nullptr, ln ? row + (OT[LDSBWD_LNO_B] - lo) : nullptr, RED);
+        BSTAMP();
     }
     for (int r = R - 1; r >= 0; r--) {
         const int* o = rbo(r);
@@ -334,20 +482,25 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
                       ln, AC, SA);
             build_kt(KT, nc, kp4(nc), nc, 1, 1, 1);
             __syncthreads();
+        BSTAMP();
             // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
             // gradient once, with the first chunk)
             wgrad_px(AC, SA, 0, KT, nc, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
-                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row);
+                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ);
             __syncthreads();
+        BSTAMP();
         }
         stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, kp4(nk), np16(gc), WL);
         build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
         __syncthreads();
-        gemm_any(GY, SY, 0, KT, kp4(nk), WL, np16(gc), GT, ST, 0, gc, H, W, false);
+        BSTAMP();
+        gemm_any(GY, SY, 0, KT, kp4(nk), WL, np16(gc), GT, ST, 0, gc, H, W, false, ZQ);
         __syncthreads();
+        BSTAMP();
         // ---- LN3 backward in place on GT -> dL/dt2
         ln_bwd(t2r, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, GT, ST, 0, GT, ST, 0, false, HW, gc, ln,
                ln ? row + (o[LDSBWD_LN3G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN3B] - lo) : nullptr, RED);
+        BSTAMP();
         // ---- grouped branches: every wgrad (A = LN2(t1) window -> AC), then every dgrad into AC (zeroed)
         for (int bi = 0; bi < a.nbr; bi++) {
             const int cin = a.br_cin[bi], cout = a.br_cout[bi];
@@ -355,9 +508,11 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
                       ln ? P + o[LDSBWD_LN2B] : nullptr, ln, AC, SA);
             build_kt(KT, taps * cin, kp4(taps * cin), cin, taps, a.br_dil[bi], 1);
             __syncthreads();
+        BSTAMP();
             wgrad_px(AC, SA, 0, KT, taps * cin, GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
-                     o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row);
+                     o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row, WL, a.wmax, ZQ);
             __syncthreads();
+        BSTAMP();
         }
         for (int e = threadIdx.x; e < HW * nk; e += BWT) {
             const int p = e / nk, c = e - p * nk;
@@ -368,28 +523,36 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
             stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, kp4(taps * cout), np16(cin), WL);
             build_kt(KT, taps * cout, kp4(taps * cout), cout, taps, a.br_dil[bi], -1);
             __syncthreads();
+        BSTAMP();
             gemm_any(GT, ST, a.br_out_off[bi], KT, kp4(taps * cout), WL, np16(cin), AC, SA, a.br_cin_off[bi], cin, H, W,
-                     true);
+                     true, ZQ);
             __syncthreads();
+        BSTAMP();
         }
         // ---- LN2 backward: AC (dL/d LN2-out, zero outside the windows) -> dL/dt1 in GT
         ln_bwd(t1r, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr, AC, SA, 0, GT, ST, 0, false, HW, nk, ln,
                ln ? row + (o[LDSBWD_LN2G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN2B] - lo) : nullptr, RED);
+        BSTAMP();
         // ---- conv_a: A = LN1(y_r) -> AC; wgrad with GT; dgrad -> AC
         stage_act(yr, nk, 0, nk, HW, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, ln ? P + o[LDSBWD_LN1B] : nullptr, ln,
                   AC, SA);
         build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
         __syncthreads();
-        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row);
+        BSTAMP();
+        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL, a.wmax, ZQ);
         __syncthreads();
+        BSTAMP();
         stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, kp4(nk), np16(nk), WL);
         build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
         __syncthreads();
-        gemm_any(GT, ST, 0, KT, kp4(nk), WL, np16(nk), AC, SA, 0, nk, H, W, false);
+        BSTAMP();
+        gemm_any(GT, ST, 0, KT, kp4(nk), WL, np16(nk), AC, SA, 0, nk, H, W, false, ZQ);
         __syncthreads();
+        BSTAMP();
         // ---- LN1 backward: GY += dL/dy_r through conv_a (the identity path keeps GY)
         ln_bwd(yr, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, AC, SA, 0, GY, SY, 0, true, HW, nk, ln,
                ln ? row + (o[LDSBWD_LN1G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN1B] - lo) : nullptr, RED);
+        BSTAMP();
     }
     // ---- conv_in: A = u1c (gathered from the layer input) -> AC; wgrad with GY; dgrad -> GT -> du1c
     {
@@ -400,19 +563,30 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         }
         build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
         __syncthreads();
-        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row);
+        BSTAMP();
+        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row, WL, a.wmax, ZQ);
         __syncthreads();
+        BSTAMP();
         stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, kp4(taps * nk), np16(a.dc1), WL);
         build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, -1);
         __syncthreads();
-        gemm_any(GY, SY, 0, KT, kp4(taps * nk), WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false);
+        BSTAMP();
+        gemm_any(GY, SY, 0, KT, kp4(taps * nk), WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false, ZQ);
         __syncthreads();
+        BSTAMP();
         float* du = a.du1c[net] + (size_t)img * HW * a.dc1;
         for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
             const int p = e / a.dc1, c = e - p * a.dc1;
             du[e] = GT[p * ST + c];
         }
     }
+    BSTAMP();
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_bwd_stamps[0] = nst;
+}
+
+int read_bwd_stamps(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_stamps), sizeof(long long) * (n > 128 ? 128 : n)) == hipSuccess ? 0
+                                                                                                                   : -1;
 }
 
 void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st) {

@@ -206,6 +206,14 @@ struct TrainLayout {
     std::vector<size_t> act_save, so_save;
     size_t rows = 0;
     int row_max = 0;
+    // streamed layers: the training forward saves the activations the backward would otherwise recompute
+    // (when they fit the budget): per net y [R+1][B][HW][nk], full t1 [R][B][HW][nk], t2 [R][B][HW][gc],
+    // LN statistics [3R+1][B][2] (y_r: r, t1_r: R+1+r, t2_r: 2R+1+r) and the raw conv_out [2][B][HW][dc2]
+    struct StreamSave {
+        size_t y[2] = {}, t1[2] = {}, t2[2] = {}, st[2] = {}, so = 0;
+    };
+    std::vector<StreamSave> ssave;
+    std::vector<char> has_ssave;
 };
 
 struct Plan {

@@ -621,7 +621,8 @@ static double net_flops(const Coupling& c) {
 // raw activations and LN statistics to save (LdsSave blocks) and its s / t outputs to so_save[2]
 static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir,
                          const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr,
-                         float* save = nullptr, float* const* so_save = nullptr) {
+                         float* save = nullptr, float* const* so_save = nullptr,
+                         const TrainLayout::StreamSave* ss = nullptr) {
     const int B = E.B;
     const WsLayout& L = E.L;
     const float* P = E.params;
@@ -697,6 +698,23 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     float* t1[2] = {E.at<float>(L.t1[0]), E.at<float>(L.t1[1])};
     float* t2[2] = {E.at<float>(L.t2[0]), E.at<float>(L.t2[1])};
     float* so[2] = {E.at<float>(L.so[0]), E.at<float>(L.so[1])};
+    // training forward with saved activations (TrainLayout::StreamSave): y_r and t2_r live in per-block
+    // slices of the save area (conv_b writes y_{r+1} next to its residual y_r instead of in place), conv_a
+    // also stores the full t1_r, and every LN tensor's statistics are folded once into [B][2]
+    if (ss != nullptr && c.t2_mapped) throw std::logic_error("training save: mapped t2 layout");
+    const size_t npx = (size_t)c.hc * c.wc;
+    auto SY = [&](int n, int r) { return E.at<float>(ss->y[n]) + (size_t)r * B * npx * c.nk; };
+    auto ST1 = [&](int n, int r) { return E.at<float>(ss->t1[n]) + (size_t)r * B * npx * c.nk; };
+    auto ST2 = [&](int n, int r) { return E.at<float>(ss->t2[n]) + (size_t)r * B * npx * c.gc; };
+    auto SST = [&](int n, int i) { return E.at<float>(ss->st[n]) + (size_t)i * B * 2; };
+    if (ss != nullptr) {
+        for (int n = 0; n < 2; n++) {
+            y[n] = SY(n, 0);
+            t2[n] = ST2(n, 0);
+        }
+        so[0] = so0;   // (so_save: the save area's raw conv_out)
+        so[1] = so1;
+    }
     Slab sl[2][3];   // [net][y, t1, t2]
     for (int n = 0; n < 2; n++)
         for (int k = 0; k < 3; k++) {
@@ -721,6 +739,16 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             nparts = 1;
         }
         for (int n = 0; n < 2; n++) sl[n][k].nparts = nparts;
+    };
+    // training save: the statistics of LN tensor i (see TrainLayout::StreamSave) from slab k's slots
+    auto save_stats = [&](int k, int i) {
+        if (ss == nullptr || !ln) return;
+        const float* p0 = sl[0][k].part;
+        const float* p1 = sl[1][k].part;
+        float* s0 = SST(0, i);
+        float* s1 = SST(1, i);
+        const int np = sl[0][k].nparts, ps = L.st_parts;
+        E.record("k_ln_final", 0, 16.0 * B * np * 2, [=](void* st) { launch_ln_final(p0, p1, np, ps, B, s0, s1, (hipStream_t)st); });
     };
     auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };
     const float* none = nullptr;
@@ -753,7 +781,10 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         }
         set_parts(0, conv_launch(E, 3, ROLE_CONV_IN, c.hc, c.wc, pr));
     }
+    save_stats(0, 0);
     for (int r = 0; r < c.R; r++) {
+        if (ss != nullptr)
+            for (int n = 0; n < 2; n++) t2[n] = ST2(n, r);
         // conv_a: LN1(LReLU(y)) -> 1x1 -> t1
         {
             std::vector<ProbSpec> pr;
@@ -767,6 +798,18 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             // t1_compact); the LN2 statistics still cover all nk channels
             const int* t1map = c.t1_compact ? E.p.dtab(c.dev_t1_map) : nullptr;
             set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map));
+            if (ss != nullptr) {
+                // the full t1_r for the backward's LN2 (the compact t1 above holds only the branch windows)
+                std::vector<ProbSpec> pf;
+                for (int n = 0; n < 2; n++) {
+                    const RBParams& rb = c.net[n].rb[r];
+                    pf.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + rb.ln1g : none,
+                                          ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, ST1(n, r), c.nk, 0, c.nk,
+                                          none, Slab{}, 0, 1});
+                }
+                conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pf);
+                save_stats(1, c.R + 1 + r);
+            }
         }
         // grouped dilated branches: LN2(LReLU(t1)) -> 3x3 dil d -> t2[:, out_off:out_off+cout]. The k_gc
         // launch (when planned) takes its branches first; every other branch runs as a k_pw tap-mode
@@ -879,6 +922,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             if (!pr.empty()) base += nrest * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
             if (base > L.st_parts) throw std::runtime_error("grouped branches: LN partial slab too small");
             set_parts(2, base);
+            save_stats(2, 2 * c.R + 1 + r);
         }
         // conv_b: LN3(LReLU(t2)) -> 1x1 -> + shortcut -> y (in place)
         {
@@ -886,11 +930,15 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
                 pr.push_back(ProbSpec{t2[n], c.t2_cs, 0, c.gc, in_slab(n, 2), ln ? ln3g(rb) : none,
-                                      ln ? ln3b(rb) : none, 1, X + rb.cb.w, X + rb.cb.b, y[n], c.nk, 0, c.nk, y[n],
+                                      ln ? ln3b(rb) : none, 1, X + rb.cb.w, X + rb.cb.b,
+                                      ss != nullptr ? SY(n, r + 1) : y[n], c.nk, 0, c.nk, y[n],
                                       out_slab(n, 0, 4 * nt1), 0, 1});
             }
             set_parts(0, conv_launch(E, 1, ROLE_CONV_B, c.hc, c.wc, pr, ~0ull, nullptr, nullptr,
                                      c.t2_mapped ? dmap(c.dev_t2_qmap) : nullptr));
+            if (ss != nullptr)
+                for (int n = 0; n < 2; n++) y[n] = SY(n, r + 1);
+            save_stats(0, r + 1);
         }
     }
     // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b); > 64 outputs in 64-channel chunks
@@ -1186,8 +1234,14 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
                 so_save[0] = E.at<float>(TL.so_save[c.index]);
                 so_save[1] = so_save[0] + (size_t)B * c.hc * c.wc * c.dc2;
             }
+            const TrainLayout::StreamSave* ss =
+                save_inputs && !c.use_lds && TL.has_ssave[c.index] ? &TL.ssave[c.index] : nullptr;
+            if (ss != nullptr) {   // the raw conv_out (k_coupling's so_w in tap mode) into the save area
+                so_save[0] = E.at<float>(ss->so);
+                so_save[1] = so_save[0] + (size_t)B * c.hc * c.wc * c.dc2;
+            }
             run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1, have_pend ? &pend : nullptr,
-                         defer, &next, save, save ? so_save : nullptr);
+                         defer, &next, save, (save || ss) ? so_save : nullptr, ss);
             pend = next;
             have_pend = defer;
             cur = nxt;
@@ -1764,6 +1818,7 @@ int cnf_debug_t1_layout(const cnf_plan* plan, int coupling, int* words, int cap)
 }
 
 int cnf_debug_read_stamps(long long* out, int n) { return read_stamps(out, n); }
+int cnf_debug_read_bwd_stamps(long long* out, int n) { return read_bwd_stamps(out, n); }
 int cnf_debug_read_cycles(long long* out, int n) { return read_cycles(out, n); }
 int cnf_debug_read_gc_stamps(long long* out, int n) { return read_gc_stamps(out, n); }
 int cnf_debug_read_pw_stamps(long long* out) { return read_pw_stamps(out); }

@@ -109,6 +109,7 @@ size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
     a.off_ac = (int)off;
     off = al(off + (size_t)HW * a.sa * 4);
     a.off_w = (int)off;
+    a.wmax = (int)wmax;
     off = al(off + wmax * 4);
     a.off_kt = (int)off;
     off = al(off + (size_t)ktmax * 4);
@@ -116,6 +117,8 @@ size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
     off = al(off + 16 * 8);
     a.off_ot = (int)off;
     off = al(off + (size_t)c.bwd_offs_per_net * 4);
+    a.off_z = (int)off;   // 4 zeros + 4 ones
+    off = al(off + 32);
     if (off > 160 * 1024) return 0;
     a.lds_bytes = (int)off;
     a.offs_per_net = c.bwd_offs_per_net;
@@ -204,6 +207,33 @@ TrainLayout Plan::train_layout(int B) const {
         T.row_max = std::max<int>(T.row_max, (int)std::max(c.net[0].hi - c.net[0].lo, c.net[1].hi - c.net[1].lo));
     }
     if (T.row_max > 0) T.rows = take(2 * Bz * T.row_max * 4);
+    // streamed layers' saved activations, when all of them fit 16 GiB (CNF_TRAIN_SAVE=0: recompute)
+    T.ssave.assign(couplings.size(), TrainLayout::StreamSave{});
+    T.has_ssave.assign(couplings.size(), 0);
+    {
+        bool on = true;
+        if (const char* e = std::getenv("CNF_TRAIN_SAVE")) on = std::atoi(e) != 0;
+        size_t need = 0;
+        for (const Coupling& c : couplings) {
+            if (c.use_lds || c.t2_mapped) continue;
+            const size_t npx = (size_t)c.hc * c.wc;
+            need += 2 * Bz * npx * ((size_t)(c.R + 1) * c.nk + (size_t)c.R * c.nk + (size_t)c.R * c.gc + c.dc2) * 4;
+        }
+        if (on && need <= (16ull << 30))
+            for (const Coupling& c : couplings) {
+                if (c.use_lds || c.t2_mapped) continue;
+                const size_t npx = (size_t)c.hc * c.wc;
+                TrainLayout::StreamSave& s = T.ssave[c.index];
+                for (int n = 0; n < 2; n++) {
+                    s.y[n] = take((size_t)(c.R + 1) * Bz * npx * c.nk * 4);
+                    s.t1[n] = take((size_t)std::max(c.R, 1) * Bz * npx * c.nk * 4);
+                    s.t2[n] = take((size_t)std::max(c.R, 1) * Bz * npx * c.gc * 4);
+                    s.st[n] = take((size_t)(3 * c.R + 1) * Bz * 2 * 4);
+                }
+                s.so = take(2 * Bz * npx * c.dc2 * 4);
+                T.has_ssave[c.index] = 1;
+            }
+    }
     T.total = off;
     return T;
 }
@@ -221,6 +251,7 @@ struct TExec {
     hipStream_t st;
     float inv_batch_ = 0.f;
     const float* count = nullptr;   // device global image count (overrides inv_batch_)
+    bool saved = false;             // the training forward saved the streamed layers' activations (flow backward)
     int net = 0;   // which per-net scratch set (and stream) this executor's launches use
     hipStream_t wst = nullptr;   // weight-gradient stream (null: on st)
     const float* bw() const { return reinterpret_cast<const float*>(ws + T.bw); }
@@ -452,6 +483,11 @@ void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const fl
     a.offs = E.p.dev_table + c.dev_bwd_offs;
     a.part = E.at<float>(E.T.rows);
     a.row = E.T.row_max;
+    static const bool stamps = [] {   // diagnostics
+        const char* e = std::getenv("CNF_LDSBWD_STAMPS");
+        return e && std::atoi(e) != 0;
+    }();
+    a.stamps = stamps ? 1 : 0;
     launch_lds_bwd(a, B, E.st);
     const NetParams& n0 = c.net[0];
     const NetParams& n1 = c.net[1];
@@ -482,10 +518,15 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     launch_gather_u1c(u, u1c, B, c.H, c.W, c.D, c.mask, h, w, c.dc1, E.st);
     // activations of both nets: y_r (r = 0..R), t1_r, t2_r; LN stats st[0..R] (y), st[R+1+r] (t1),
     // st[2R+1+r] (t2), each [B][2]
-    auto Y = [&](int n, int r) { return E.at<float>(E.T.ys[n]) + (size_t)r * B * npx * nk; };
-    auto T1 = [&](int n, int r) { return E.at<float>(E.T.t1s[n]) + (size_t)r * B * npx * nk; };
-    auto T2 = [&](int n, int r) { return E.at<float>(E.T.t2s[n]) + (size_t)r * B * npx * gc; };
-    auto ST = [&](int n, int i) { return E.at<float>(E.T.stats[n]) + (size_t)i * B * 2; };
+    // the training forward's saved activations of this (streamed) layer, when it saved them (the backward
+    // of a lone layer, cnf_coupling_backward, always recomputes)
+    const bool saved = E.saved && E.T.has_ssave[c.index];
+    const TrainLayout::StreamSave& SS = E.T.ssave[c.index];
+    auto Y = [&](int n, int r) { return E.at<float>(saved ? SS.y[n] : E.T.ys[n]) + (size_t)r * B * npx * nk; };
+    auto T1 = [&](int n, int r) { return E.at<float>(saved ? SS.t1[n] : E.T.t1s[n]) + (size_t)r * B * npx * nk; };
+    auto T2 = [&](int n, int r) { return E.at<float>(saved ? SS.t2[n] : E.T.t2s[n]) + (size_t)r * B * npx * gc; };
+    auto ST = [&](int n, int i) { return E.at<float>(saved ? SS.st[n] : E.T.stats[n]) + (size_t)i * B * 2; };
+    auto SO = [&](int n) { return saved ? E.at<float>(SS.so) + (size_t)n * B * npx * c.dc2 : E.at<float>(E.T.so[n]); };
     auto lnin = [&](int n, int i, int64_t g, int64_t b) {
         LnIn l;
         l.act = 1;
@@ -498,7 +539,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     };
     const LnIn raw{};
     stream_wait(E.st, E1.st, E.p.ev_fork);   // u1c gathered
-    for (int n = 0; n < 2; n++) {
+    for (int n = 0; n < 2 && !saved; n++) {
         TExec& En = *X[n];
         const NetParams& np = c.net[n];
         conv_fwd(En, h, w, u1c, c.dc1, 0, c.dc1, raw, np.ci, nk, 1, nullptr, Y(n, 0), nk, 0);
@@ -518,7 +559,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
             if (ln) launch_ln_stats(Y(n, r + 1), npx * nk, B, 1, ST(n, r + 1), En.st);
         }
         conv_fwd(En, h, w, Y(n, R), nk, 0, nk, lnin(n, R, np.ln_out_g, np.ln_out_b), np.co, c.dc2, 1, nullptr,
-                 E.at<float>(E.T.so[n]), c.dc2, 0);
+                 SO(n), c.dc2, 0);
     }
     stream_wait(E1.st, E.st, E.p.ev_join);   // both nets' outputs
     // coupling law backward -> du (u2 part, u1 copy), dL/d s_pre, dL/dt, dL/dw
@@ -526,7 +567,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         CoupBwArgs a{};
         a.u = u;
         a.dv = dv;
-        a.s_pre = E.at<float>(E.T.so[0]);
+        a.s_pre = SO(0);
         a.tanh_w = P + c.net[0].tanh_w;
         a.du = du;
         a.ds_pre = E.at<float>(E.T.dso[0]);
@@ -610,6 +651,7 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     TExec E{p, params, dparams, (char*)workspace, p.layout(B), p.train_layout(B), B, st};
     E.inv_batch_ = inv_batch;
     E.count = count;
+    E.saved = true;
     const WsLayout& L = E.L;
     const int* T = p.dev_table;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
