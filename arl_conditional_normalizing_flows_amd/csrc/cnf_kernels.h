@@ -414,15 +414,17 @@ void launch_ln_backward(const float* x, const float* dxo, const float* gamma, co
 // (image, net). Offsets table per net (int32, `offs_per_net` entries): canonical parameter offsets
 // (LN gamma / beta, the net's first parameter, tanh scale or -1) and dense backward-image offsets
 // (conv weights _DW, biases _DB), laid out as the LDSBWD_* indices below (per residual block r at
-// LDSBWD_RB0 + r * (10 + 2 * nbr), branch bi's (dw, db) at LDSBWD_BR + 2 bi of it).
+// LDSBWD_RB0 + r * (LDSBWD_PER_RB0 + 2 * nbr), branch bi's (dw, db) at LDSBWD_BR + 2 bi of it).
 enum {
     LDSBWD_LO = 0, LDSBWD_CI_DW, LDSBWD_CI_DB, LDSBWD_LNO_G, LDSBWD_LNO_B, LDSBWD_CO_DW, LDSBWD_CO_DB, LDSBWD_TANH,
+    LDSBWD_CI_K, LDSBWD_CI_B, LDSBWD_CO_K, LDSBWD_CO_B,   // canonical kernel / bias offsets of the plain convs
     LDSBWD_RB0
 };
 enum {
     LDSBWD_LN1G = 0, LDSBWD_LN1B, LDSBWD_CA_DW, LDSBWD_CA_DB, LDSBWD_LN2G, LDSBWD_LN2B, LDSBWD_LN3G, LDSBWD_LN3B,
-    LDSBWD_CB_DW, LDSBWD_CB_DB, LDSBWD_BR
+    LDSBWD_CB_DW, LDSBWD_CB_DB, LDSBWD_CA_K, LDSBWD_CA_B, LDSBWD_CB_K, LDSBWD_CB_B, LDSBWD_BR
 };
+constexpr int LDSBWD_PER_RB0 = LDSBWD_BR;   // entries per residual block before its branches' (dw, db) pairs
 struct LdsBwdArgs {
     const float* save;        // the training forward's save area of the layer [net][B][save_img] (LdsSave)
     int save_img, save_t1, save_t2, save_st;

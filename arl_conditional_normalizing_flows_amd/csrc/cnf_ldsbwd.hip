@@ -134,33 +134,44 @@ __device__ __forceinline__ void gemm_any(const float* a, int sa, int a_off, cons
 // leave waves idle, their partial tiles summed in slice order through scr (scr_floats of LDS). Pixels
 // in groups of four MFMA steps: the group's A and G loads (branch-free, the row from a float
 // reciprocal of W) issue together, then four MFMAs into four accumulators.
+// Destinations: plain convs (direct) have the dense layout of their canonical HWIO kernel, so k * N + n
+// lands at ck + k * N + n and the bias at cbias + n; the grouped branches go through bw_map (dense image
+// dw / db), its entries loaded when the unit starts so their latency hides behind the MFMAs.
 __device__ void wgrad_px(const float* a, int sa, int a_off, const int* kt, int K, const float* g, int sg, int g_off,
                          int N, int H, int W, const int64_t* __restrict__ bw_map, int64_t dw, int64_t db, int64_t lo,
-                         float* __restrict__ row, float* scr, int scr_floats, const float* Z) {
+                         float* __restrict__ row, float* scr, int scr_floats, const float* Z, bool direct = false,
+                         int64_t ck = 0, int64_t cbias = 0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
     const int HW = H * W, Kb = K + (db >= 0 ? 1 : 0), nkb = (Kb + 15) >> 4, nnb = (N + 15) >> 4, tiles = nkb * nnb;
     int S = 1;
     while (tiles * S < 2 * BWN && 2 * S * 16 <= HW && tiles * 2 * S * 256 <= scr_floats) S *= 2;
     const int q = ((HW + S - 1) / S + 15) / 16 * 16;   // pixels per slice
     const float invW = 1.f / (float)W;
-    auto store = [&](int tile, const f4& v) {
+    // the lane's four destinations of tile `tile` (rows k0 + 4kq + r, column n), -1: none
+    auto dests = [&](int tile, int64_t (&dst)[4]) {
         const int k0 = (tile % nkb) * 16, n = (tile / nkb) * 16 + i16;
-        if (n >= N) return;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const int k = k0 + 4 * kq + r;
-            int64_t dst = -1;
+            dst[r] = -1;
+            if (n >= N) continue;
             if (k < K)
-                dst = bw_map[dw + (int64_t)k * N + n];
+                dst[r] = direct ? ck + (int64_t)k * N + n : bw_map[dw + (int64_t)k * N + n];
             else if (k == K && db >= 0)
-                dst = bw_map[db + n];
-            if (dst >= 0) row[dst - lo] = v[r];
+                dst[r] = direct ? cbias + n : bw_map[db + n];
         }
+    };
+    auto store = [&](const int64_t (&dst)[4], const f4& v) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (dst[r] >= 0) row[dst[r] - lo] = v[r];
     };
     for (int unit = wave; unit < tiles * S; unit += BWN) {
         const int tile = unit % tiles, s = unit / tiles;
         const int k = (tile % nkb) * 16 + i16, n = (tile / nkb) * 16 + i16;
         const int t = k < K ? kt[k] : (k == K && db >= 0 ? KT_ONE : -1);
+        int64_t dst[4];
+        if (S == 1) dests(tile, dst);   // (issued before the loop: the map loads complete behind the MFMAs)
         const bool nv = n < N;
         const int p_lo = s * q, p_hi = min(HW, p_lo + q);
         f4 acc[4];
@@ -181,16 +192,18 @@ __device__ void wgrad_px(const float* a, int sa, int a_off, const int* kt, int K
         }
         const f4 v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         if (S == 1)
-            store(tile, v);
+            store(dst, v);
         else
             *reinterpret_cast<f4*>(scr + ((size_t)unit * 64 + lane) * 4) = v;
     }
     if (S > 1) {
         __syncthreads();
         for (int tile = wave; tile < tiles; tile += BWN) {
+            int64_t dst[4];
+            dests(tile, dst);
             f4 v = *reinterpret_cast<const f4*>(scr + ((size_t)tile * 64 + lane) * 4);
             for (int s = 1; s < S; s++) v += *reinterpret_cast<const f4*>(scr + ((size_t)(s * tiles + tile) * 64 + lane) * 4);
-            store(tile, v);
+            store(dst, v);
         }
     }
 }
@@ -431,7 +444,7 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     const float* P = a.params;
     const float* BWI = a.bw;
     float* row = a.part + ((size_t)net * B + img) * a.row;
-    auto rbo = [&](int r) { return OT + LDSBWD_RB0 + r * (10 + 2 * a.nbr); };
+    auto rbo = [&](int r) { return OT + LDSBWD_RB0 + r * (LDSBWD_PER_RB0 + 2 * a.nbr); };
     auto kp4 = [](int K) { return (K + 3) & ~3; };
     auto np16 = [](int N) { return (N + 15) & ~15; };
     const int taps = a.taps;
@@ -451,7 +464,8 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row, WL, a.wmax, ZQ);
+        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row, WL, a.wmax, ZQ,
+                 true, OT[LDSBWD_CO_K], OT[LDSBWD_CO_B]);
         __syncthreads();
         BSTAMP();
         stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, kp4(taps * a.dc2), np16(nk), WL);
@@ -486,7 +500,8 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
             // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
             // gradient once, with the first chunk)
             wgrad_px(AC, SA, 0, KT, nc, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
-                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ);
+                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ, true, o[LDSBWD_CB_K] + (int64_t)c0 * nk,
+                     o[LDSBWD_CB_B]);
             __syncthreads();
         BSTAMP();
         }
@@ -539,7 +554,8 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL, a.wmax, ZQ);
+        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL, a.wmax, ZQ,
+                 true, o[LDSBWD_CA_K], o[LDSBWD_CA_B]);
         __syncthreads();
         BSTAMP();
         stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, kp4(nk), np16(nk), WL);
@@ -564,7 +580,8 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row, WL, a.wmax, ZQ);
+        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row, WL, a.wmax, ZQ,
+                 true, OT[LDSBWD_CI_K], OT[LDSBWD_CI_B]);
         __syncthreads();
         BSTAMP();
         stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, kp4(taps * nk), np16(a.dc1), WL);

@@ -967,10 +967,11 @@ Plan* build_plan(const cnf_flow_desc* d) {
             for (int net = 0; net < 2; net++) {
                 const NetParams& np = c.net[net];
                 std::vector<int> o = {(int)np.lo, (int)np.ci.dw, (int)np.ci.db, (int)np.ln_out_g, (int)np.ln_out_b,
-                                      (int)np.co.dw, (int)np.co.db, (int)np.tanh_w};
+                                      (int)np.co.dw, (int)np.co.db, (int)np.tanh_w, (int)np.conv_in_k, (int)np.conv_in_b,
+                                      (int)np.conv_out_k, (int)np.conv_out_b};
                 for (const auto& rb : np.rb) {
                     for (int64_t v : {rb.ln1g, rb.ln1b, rb.ca.dw, rb.ca.db, rb.ln2g, rb.ln2b, rb.ln3g, rb.ln3b, rb.cb.dw,
-                                      rb.cb.db})
+                                      rb.cb.db, rb.conv_a_k, rb.conv_a_b, rb.conv_b_k, rb.conv_b_b})
                         o.push_back((int)v);
                     for (const auto& g : rb.gc) {
                         o.push_back((int)g.dw);

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
 // ------------------------------------------------------------------------------------------------
 constexpr int TB_KS = 68;   // band pixel stride (floats)
 
-template <int NR>
+template <int NR, int SUB>
 __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all_taps) {
     extern __shared__ __attribute__((aligned(16))) float tsm[];
     constexpr int NS = 16 * NR;
@@ -261,15 +261,24 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
     const int d = a.dil, BW = W + 2 * d, BH = TH + 2 * d;
     float* band = tsm;                                   // [BH * BW][TB_KS]
     float* wl = tsm + (size_t)BH * BW * TB_KS;           // [tap][16 gq][NS][4] of the chunk (all_taps) or one tap
-    const int p = wave * 16 + i16;                       // the lane's A pixel inside the tile
-    const int tr = p / W, tc = p - tr * W;
-    const bool pav = p < TH * W && r0 + tr < H;
+    // the lane's A pixel of subtile s inside the tile: (wave + 4 s) * 16 + i16
+    int tr[SUB], tc[SUB];
+    bool pav[SUB];
+#pragma unroll
+    for (int s = 0; s < SUB; s++) {
+        const int p = (wave + 4 * s) * 16 + i16;
+        tr[s] = p / W;
+        tc[s] = p - tr[s] * W;
+        pav[s] = p < TH * W && r0 + tr[s] < H;
+    }
     const float* inb = a.in + (size_t)b * npx * a.in_cs + a.in_off;
     const bool ln = a.stats != nullptr;
     const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
-    f4 acc[NR];
+    f4 acc[SUB][NR];
 #pragma unroll
-    for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < SUB; s++)
+#pragma unroll
+        for (int m = 0; m < NR; m++) acc[s][m] = f4{0.f, 0.f, 0.f, 0.f};
     const bool vq = (a.in_cs & 3) == 0 && (a.in_off & 3) == 0;
     for (int kc = 0; kc < a.K; kc += 64) {
         // quads up to the 16-channel group boundary (the MFMA reads whole groups: zeros past K)
@@ -344,39 +353,49 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 __syncthreads();
             }
             const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-            const int br = tr + d + a.sgn * d * dr, bc = tc + d + a.sgn * d * dc;
-            const float* ap = band + (size_t)(br * BW + bc) * TB_KS + 4 * kq;
             const f4* wp = reinterpret_cast<const f4*>(wl) + (size_t)(all_taps ? tap : 0) * 16 * NS + (size_t)kq * NS + i16;
+            const float* ap[SUB];
+#pragma unroll
+            for (int s = 0; s < SUB; s++) {
+                const int br = tr[s] + d + a.sgn * d * dr, bc = tc[s] + d + a.sgn * d * dc;
+                ap[s] = band + (size_t)(br * BW + bc) * TB_KS + 4 * kq;
+            }
             for (int g = 0; g < G; g++) {
-                const f4 x = pav ? *reinterpret_cast<const f4*>(ap + 16 * g) : f4{0.f, 0.f, 0.f, 0.f};
+                f4 x[SUB];
+#pragma unroll
+                for (int s = 0; s < SUB; s++) x[s] = pav[s] ? *reinterpret_cast<const f4*>(ap[s] + 16 * g) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int m = 0; m < NR; m++) {
                     const f4 bv = wp[(size_t)4 * g * NS + 16 * m];
 #pragma unroll
                     for (int s4 = 0; s4 < 4; s4++)
-                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s4], bv[s4], acc[m], 0, 0, 0);
+#pragma unroll
+                        for (int s = 0; s < SUB; s++)
+                            acc[s][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s][s4], bv[s4], acc[s][m], 0, 0, 0);
                 }
             }
         }
     }
-    // acc[m][rr] = out[tile pixel 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
+    // acc[s][m][rr] = out[tile pixel (wave + 4s) * 16 + 4 kq + rr][channel n0 + 16 m + i16]
 #pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-        const int q = wave * 16 + 4 * kq + rr;
-        const int orow = r0 + q / W, ocol = q % W;
-        if (q >= TH * W || orow >= H) continue;
-        const size_t ob = ((size_t)b * npx + (size_t)orow * W + ocol) * a.out_cs + a.out_off;
+    for (int s = 0; s < SUB; s++)
 #pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const int n = n0 + 16 * m + i16;
-            if (n >= a.N) continue;
-            float v = acc[m][rr];
-            if (a.bias) v += a.bias[n];
-            if (a.res) v += a.res[ob + n];
-            if (a.accumulate) v += a.out[ob + n];
-            a.out[ob + n] = v;
+        for (int rr = 0; rr < 4; rr++) {
+            const int q = (wave + 4 * s) * 16 + 4 * kq + rr;
+            const int orow = r0 + q / W, ocol = q % W;
+            if (q >= TH * W || orow >= H) continue;
+            const size_t ob = ((size_t)b * npx + (size_t)orow * W + ocol) * a.out_cs + a.out_off;
+#pragma unroll
+            for (int m = 0; m < NR; m++) {
+                const int n = n0 + 16 * m + i16;
+                if (n >= a.N) continue;
+                float v = acc[s][m][rr];
+                if (a.bias) v += a.bias[n];
+                if (a.res) v += a.res[ob + n];
+                if (a.accumulate) v += a.out[ob + n];
+                a.out[ob + n] = v;
+            }
         }
-    }
 }
 
 static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (read per call: tests switch it)
@@ -394,17 +413,39 @@ void launch_tconv(const TConvArgs& a, hipStream_t st) {
     if (!train_valu() && !band_off && a.taps == 9 && a.dil <= 2 && a.W <= 64 && a.W >= 1) {
         const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
         const int NS = 16 * nr;
-        const int TH = std::max(1, std::min(a.H, 64 / a.W));
-        const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
         const size_t w1 = (size_t)16 * NS * 4 * 4;   // one tap of a 64-channel chunk
-        const int all_taps = band + 9 * w1 <= 80 * 1024 ? 1 : 0;
+        // subtiles per wave: tiles of 64 * SUB pixels amortise the weight staging and the halo rows over
+        // more outputs, while the launch keeps >= 512 workgroups (two per CU) and the band fits LDS
+        int sub = 1;
+        for (int s : {4, 2}) {
+            if (sub > 1 || s * nr > 4) continue;   // (acc registers: SUB * NR <= 4)
+            const int TH = std::max(1, std::min(a.H, 64 * s / a.W));
+            const long long wgs = (long long)((a.H + TH - 1) / TH) * a.B * ((a.N + NS - 1) / NS);
+            const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
+            // (measured at cfg2 B=64, 32x32 branch dgrads: SUB=2 at 512 workgroups was slower than 1024
+            // workgroups of one subtile per wave, so wider tiles only when they still leave >= 1024)
+            if (64 * s <= a.H * a.W && wgs >= 1024 && band + w1 <= 160 * 1024) sub = s;
+        }
+        const int TH = std::max(1, std::min(a.H, 64 * sub / a.W));
+        const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
+        const int all_taps = band + 9 * w1 <= (sub > 1 ? 156 : 80) * 1024 ? 1 : 0;
         const size_t lds = band + (all_taps ? 9 : 1) * w1;
         if (lds <= 160 * 1024) {
             const dim3 g((a.H + TH - 1) / TH, a.B, (a.N + NS - 1) / NS), blk(256);
-            if (nr == 1) hipLaunchKernelGGL(k_tconv_band<1>, g, blk, lds, st, a, TH, all_taps);
-            else if (nr == 2) hipLaunchKernelGGL(k_tconv_band<2>, g, blk, lds, st, a, TH, all_taps);
-            else if (nr == 3) hipLaunchKernelGGL(k_tconv_band<3>, g, blk, lds, st, a, TH, all_taps);
-            else hipLaunchKernelGGL(k_tconv_band<4>, g, blk, lds, st, a, TH, all_taps);
+            if (sub == 4)
+                hipLaunchKernelGGL((k_tconv_band<1, 4>), g, blk, lds, st, a, TH, all_taps);
+            else if (sub == 2 && nr == 1)
+                hipLaunchKernelGGL((k_tconv_band<1, 2>), g, blk, lds, st, a, TH, all_taps);
+            else if (sub == 2)
+                hipLaunchKernelGGL((k_tconv_band<2, 2>), g, blk, lds, st, a, TH, all_taps);
+            else if (nr == 1)
+                hipLaunchKernelGGL((k_tconv_band<1, 1>), g, blk, lds, st, a, TH, all_taps);
+            else if (nr == 2)
+                hipLaunchKernelGGL((k_tconv_band<2, 1>), g, blk, lds, st, a, TH, all_taps);
+            else if (nr == 3)
+                hipLaunchKernelGGL((k_tconv_band<3, 1>), g, blk, lds, st, a, TH, all_taps);
+            else
+                hipLaunchKernelGGL((k_tconv_band<4, 1>), g, blk, lds, st, a, TH, all_taps);
             return;
         }
     }
