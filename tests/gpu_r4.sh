@@ -15,3 +15,5 @@ timeout -k 10 300 python bench.py > $out/bench.json 2> $out/bench.err || { echo 
 cat $out/bench.json
 timeout -k 10 300 python bench.py --mode inverse > $out/inverse.json 2> $out/inverse.err || { echo "inverse bench failed"; tail -20 $out/inverse.err; exit 1; }
 cat $out/inverse.json
+timeout -k 10 300 python bench.py --mode train --steps 10 --warmup 3 > $out/train.json 2> $out/train.err || { echo "train bench failed"; tail -20 $out/train.err; exit 1; }
+cat $out/train.json
