@@ -20,6 +20,12 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
 __device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
 
+// n / d for n >= 0, n * d < 2^32 as one multiply-high: m = udiv_magic(d) = ceil(2^32 / d) (0 for d == 1)
+// — the runtime-shape training kernels divide flat indices per element, and the compiler's generic
+// 32-bit division is ~30 VALU instructions (it made those kernels VALU-issue-bound)
+__host__ __device__ __forceinline__ uint32_t udiv_magic(uint32_t d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }
+__device__ __forceinline__ int udiv(int n, uint32_t m) { return m == 0 ? n : (int)__umulhi((uint32_t)n, m); }
+
 // tanh and exp of the affine coupling law (s = w * tanh(A), exp(s): conv_cINN_make_model.py:1198-1205,
 // 1215-1253) on the hardware exp (v_exp_f32): an odd Taylor polynomial below |x| = 1/4 (truncation
 // < 1e-8 relative), 1 - 2 / (e^{2|x|} + 1) above (< 1e-6 relative). k_coupling, the deferred coupling

@@ -69,62 +69,111 @@ __device__ __forceinline__ const float* kt_ptr(const float* a, int sa, int a_off
     return in ? a + (y * W + x) * sa + a_off + (t >> 14) : (t == KT_ONE && pv ? Z + 4 : Z);
 }
 
-// out[p][o_off + n] (= or +=) sum_k A(p, k) * Wl[k][n] for n < N: units of one 16-pixel subtile x
-// NR 16-column blocks, dealt round-robin over the waves (acc[m][r] = out[p0 + 4kq + r][n0 + 16m + i16]).
-// K in groups of four MFMA steps: the group's table entries, then its A and B loads, then its MFMAs.
-template <int NR>
-__device__ void gemm_px(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np, float* out,
-                        int so, int o_off, int N, int H, int W, bool accum, const float* Z) {
+// out[p][o_off + n] (= or +=) sum over taps t and channels c < cpt of A[p + shift(t)][a_off + c] *
+// Wl[t * cpt4 + c][n] (cpt4 = cpt rounded up to 4; Wl's rows cpt..cpt4-1 of every tap are zero, and
+// the A values they meet are finite: LDS is zeroed at kernel start), shift(t) = sgn * d * (t / 3 - 1,
+// t % 3 - 1) for 3x3 convs. Units of SUB 16-pixel subtiles x NR 16-column blocks, dealt round-robin over
+// the waves; per tap the lane's shifted row pointer (or the zero row Z) is computed once, so a k-step
+// is one A load, NR B loads and NR x SUB MFMAs (no per-step table or address arithmetic).
+// acc[s][m][r] = out[p0(s) + 4kq + r][n0 + 16m + i16].
+template <int NR, int SUB>
+__device__ void gemm_tap(const float* a, int sa, int a_off, int taps, int cpt4, int d, int sgn, const float* wl, int np,
+                         float* out, int so, int o_off, int N, int H, int W, bool accum, const float* Z) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
-    const int HW = H * W, nsub = (HW + 15) >> 4, ngrp = (np / 16 + NR - 1) / NR;
-    for (int unit = wave; unit < nsub * ngrp; unit += BWN) {
-        const int s = unit % nsub, n0 = (unit / nsub) * 16 * NR;
-        const int p = s * 16 + i16;
-        const bool pv = p < HW;
-        const int pr = pv ? p / W : 0, pc = pv ? p - (p / W) * W : 0;
-        f4 acc[NR];
+    const int HW = H * W, nsub = (HW + 15) >> 4, ngrp = (np / 16 + NR - 1) / NR, nsg = (nsub + SUB - 1) / SUB;
+    const float invW = 1.f / (float)W;
+    for (int unit = wave; unit < nsg * ngrp; unit += BWN) {
+        const int sg = unit % nsg, n0 = (unit / nsg) * 16 * NR;
+        const int nb = min(NR, (np - n0) >> 4);   // column blocks of this unit (uniform)
+        int pr[SUB], pc[SUB];
+        bool pv[SUB];
 #pragma unroll
-        for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
-        for (int k0 = 0; k0 < Kp; k0 += 16) {
-            int t[4];
+        for (int s = 0; s < SUB; s++) {
+            const int p = (sg * SUB + s) * 16 + i16;
+            pv[s] = p < HW;
+            pr[s] = (int)(((float)p + 0.5f) * invW);
+            pc[s] = p - pr[s] * W;
+        }
+        f4 acc[SUB][NR];
 #pragma unroll
-            for (int j = 0; j < 4; j++) t[j] = k0 + 4 * j < Kp ? kt[k0 + 4 * j + kq] : -1;
-            float av[4], bv[4][NR];
+        for (int s = 0; s < SUB; s++)
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                av[j] = *kt_ptr(a, sa, a_off, t[j], pr, pc, pv, H, W, Z);
-                const int kr = min(k0 + 4 * j, Kp - 4) + kq;   // (rows past Kp: A is 0)
+            for (int m = 0; m < NR; m++) acc[s][m] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < taps; t++) {
+            const int dr = taps == 9 ? sgn * d * (t / 3 - 1) : 0, dc = taps == 9 ? sgn * d * (t % 3 - 1) : 0;
+            const float* ab[SUB];
 #pragma unroll
-                for (int m = 0; m < NR; m++) bv[j][m] = n0 + 16 * m < np ? wl[(size_t)kr * np + n0 + 16 * m + i16] : 0.f;
+            for (int s = 0; s < SUB; s++) {
+                const int y = pr[s] + dr, x = pc[s] + dc;
+                const bool in = pv[s] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+                ab[s] = (in ? a + (y * W + x) * sa + a_off : Z) + kq;
             }
+            const float* wt = wl + ((size_t)t * cpt4 + kq) * np + n0 + i16;
+            int c = 0;
+            for (; c + 16 <= cpt4; c += 16) {
+                float av[4][SUB], bv[4][NR];
 #pragma unroll
-            for (int j = 0; j < 4; j++)
+                for (int j = 0; j < 4; j++) {
 #pragma unroll
-                for (int m = 0; m < NR; m++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bv[j][m], acc[m], 0, 0, 0);
+                    for (int s = 0; s < SUB; s++) av[j][s] = ab[s][c + 4 * j];
+#pragma unroll
+                    for (int m = 0; m < NR; m++) bv[j][m] = m < nb ? wt[(size_t)(c + 4 * j) * np + 16 * m] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int m = 0; m < NR; m++)
+#pragma unroll
+                        for (int s = 0; s < SUB; s++)
+                            acc[s][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][s], bv[j][m], acc[s][m], 0, 0, 0);
+            }
+            for (; c < cpt4; c += 4) {
+                float av[SUB], bv[NR];
+#pragma unroll
+                for (int s = 0; s < SUB; s++) av[s] = ab[s][c];
+#pragma unroll
+                for (int m = 0; m < NR; m++) bv[m] = m < nb ? wt[(size_t)c * np + 16 * m] : 0.f;
+#pragma unroll
+                for (int m = 0; m < NR; m++)
+#pragma unroll
+                    for (int s = 0; s < SUB; s++) acc[s][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[m], acc[s][m], 0, 0, 0);
+            }
         }
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int q = s * 16 + 4 * kq + r;
-            if (q >= HW) continue;
+        for (int s = 0; s < SUB; s++)
 #pragma unroll
-            for (int m = 0; m < NR; m++) {
-                const int n = n0 + 16 * m + i16;
-                if (n >= N) continue;
-                float* o = out + q * so + o_off + n;
-                *o = accum ? *o + acc[m][r] : acc[m][r];
+            for (int r = 0; r < 4; r++) {
+                const int q = (sg * SUB + s) * 16 + 4 * kq + r;
+                if (q >= HW) continue;
+#pragma unroll
+                for (int m = 0; m < NR; m++) {
+                    const int n = n0 + 16 * m + i16;
+                    if (m >= nb || n >= N) continue;
+                    float* o = out + q * so + o_off + n;
+                    *o = accum ? *o + acc[s][m][r] : acc[s][m][r];
+                }
             }
-        }
     }
 }
 
-__device__ __forceinline__ void gemm_any(const float* a, int sa, int a_off, const int* kt, int Kp, const float* wl, int np,
-                                         float* out, int so, int o_off, int N, int H, int W, bool accum, const float* Z) {
-    if (np <= 16)
-        gemm_px<1>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
-    else if (np <= 32)
-        gemm_px<2>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
-    else
-        gemm_px<4>(a, sa, a_off, kt, Kp, wl, np, out, so, o_off, N, H, W, accum, Z);
+// gemm_tap with NR from the column count and SUB = 2 when that still leaves every wave a unit
+__device__ __forceinline__ void gemm_tap_any(const float* a, int sa, int a_off, int taps, int cpt, int d, int sgn,
+                                             const float* wl, int np, float* out, int so, int o_off, int N, int H, int W,
+                                             bool accum, const float* Z) {
+    const int cpt4 = (cpt + 3) & ~3, nsub = (H * W + 15) >> 4;
+    if (np <= 16) {
+        if (nsub >= 2 * BWN)
+            gemm_tap<1, 2>(a, sa, a_off, taps, cpt4, d, sgn, wl, np, out, so, o_off, N, H, W, accum, Z);
+        else
+            gemm_tap<1, 1>(a, sa, a_off, taps, cpt4, d, sgn, wl, np, out, so, o_off, N, H, W, accum, Z);
+    } else if (np <= 32) {
+        if (nsub >= 2 * BWN)
+            gemm_tap<2, 2>(a, sa, a_off, taps, cpt4, d, sgn, wl, np, out, so, o_off, N, H, W, accum, Z);
+        else
+            gemm_tap<2, 1>(a, sa, a_off, taps, cpt4, d, sgn, wl, np, out, so, o_off, N, H, W, accum, Z);
+    } else {
+        gemm_tap<4, 1>(a, sa, a_off, taps, cpt4, d, sgn, wl, np, out, so, o_off, N, H, W, accum, Z);
+    }
 }
 
 // dW[k][n] = sum_p A(p, k) * G[p][g_off + n] (k < K = taps * cin flat, n < N) for this image, stored to
@@ -208,19 +257,124 @@ __device__ void wgrad_px(const float* a, int sa, int a_off, const int* kt, int K
     }
 }
 
-// Wl[k][n] = W[tap][n][o] for k = tap * cout + o (the transposed conv's B operand: dgrad of a conv
-// with dense weights W[taps][cin][cout]); n < cin, zero padding to kp rows x np columns
-__device__ __forceinline__ void stage_wt(const float* __restrict__ w, int taps, int cin, int cout, int kp, int np,
-                                         float* wl) {
-    const int K = taps * cout;
-    for (int e = threadIdx.x; e < kp * np; e += BWT) {
-        const int k = e / np, n = e - k * np;
-        float v = 0.f;
-        if (k < K && n < cin) {
-            const int tap = k / cout, o = k - tap * cout;
-            v = w[((size_t)tap * cin + n) * cout + o];
+// wgrad_px for images whose width is a multiple of 4, pixels walked row by row: a k-step is 4 pixels
+// of one row, so the lane's A row pointer (its tap's shifted row, or Z) is set once per row and a step
+// costs a pointer increment and a column bounds test instead of a table entry and a full address.
+// K = taps * cin (k = tap * cin + c, the forward taps of dilation d), plus the bias row (A = 1 at ONE)
+// when db >= 0; destinations, pixel slices (here: row slices) and the fixed-order slice sum as wgrad_px.
+__device__ void wgrad_rows(const float* a, int sa, int a_off, int taps, int cin, int d, const float* g, int sg,
+                           int g_off, int N, int H, int W, const int64_t* __restrict__ bw_map, int64_t dw, int64_t db,
+                           int64_t lo, float* __restrict__ row, float* scr, int scr_floats, const float* Z,
+                           const float* ONE, bool direct = false, int64_t ck = 0, int64_t cbias = 0) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int K = taps * cin, Kb = K + (db >= 0 ? 1 : 0), nkb = (Kb + 15) >> 4, nnb = (N + 15) >> 4, tiles = nkb * nnb;
+    int S = 1;
+    while (tiles * S < 2 * BWN && 2 * S <= H && tiles * 2 * S * 256 <= scr_floats) S *= 2;
+    const int q = (H + S - 1) / S;   // rows per slice
+    auto dests = [&](int tile, int64_t (&dst)[4]) {
+        const int k0 = (tile % nkb) * 16, n = (tile / nkb) * 16 + i16;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int k = k0 + 4 * kq + r;
+            dst[r] = -1;
+            if (n >= N) continue;
+            if (k < K)
+                dst[r] = direct ? ck + (int64_t)k * N + n : bw_map[dw + (int64_t)k * N + n];
+            else if (k == K && db >= 0)
+                dst[r] = direct ? cbias + n : bw_map[db + n];
         }
-        wl[e] = v;
+    };
+    auto store = [&](const int64_t (&dst)[4], const f4& v) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if (dst[r] >= 0) row[dst[r] - lo] = v[r];
+    };
+    for (int unit = wave; unit < tiles * S; unit += BWN) {
+        const int tile = unit % tiles, s = unit / tiles;
+        const int k = (tile % nkb) * 16 + i16, n = (tile / nkb) * 16 + i16;
+        int64_t dst[4];
+        if (S == 1) dests(tile, dst);
+        const bool kv = k < K, kb = k == K && db >= 0;
+        const int tap = kv ? k / cin : 0, c = kv ? k - tap * cin : 0;
+        const int dr = taps == 9 ? d * (tap / 3 - 1) : 0, dc = taps == 9 ? d * (tap % 3 - 1) : 0;
+        const bool nv = n < N;
+        const float* gcol = nv ? g + g_off + n : Z;
+        const int gst = nv ? sg : 0;
+        const int r_lo = s * q, r_hi = min(H, r_lo + q);
+        f4 acc[4];
+#pragma unroll
+        for (int h = 0; h < 4; h++) acc[h] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int r = r_lo; r < r_hi; r++) {
+            const int y = r + dr;
+            const bool rv = kv && (unsigned)y < (unsigned)H;
+            // the lane's A at column x: arow + x * sa (valid when rv and 0 <= x < W), the bias lane ONE
+            const float* arow = a + (y * W + dc) * sa + a_off + c;
+            const float* grow = gcol + (r * W + kq) * gst;
+            for (int x0 = 0; x0 < W; x0 += 16) {
+                float av[4], bv[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const int xs = x0 + 4 * h;                 // the step's first column (uniform)
+                    const bool sv = xs < W;
+                    const int x = xs + kq + dc;                // the lane's source column
+                    const bool in = sv && rv && (unsigned)x < (unsigned)W;
+                    av[h] = *(in ? arow + (xs + kq) * sa : (kb && sv ? ONE : Z));
+                    bv[h] = *(sv ? grow + xs * gst : Z);
+                }
+#pragma unroll
+                for (int h = 0; h < 4; h++) acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[h], bv[h], acc[h], 0, 0, 0);
+            }
+        }
+        const f4 v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        if (S == 1)
+            store(dst, v);
+        else
+            *reinterpret_cast<f4*>(scr + ((size_t)unit * 64 + lane) * 4) = v;
+    }
+    if (S > 1) {
+        __syncthreads();
+        for (int tile = wave; tile < tiles; tile += BWN) {
+            int64_t dst[4];
+            dests(tile, dst);
+            f4 v = *reinterpret_cast<const f4*>(scr + ((size_t)tile * 64 + lane) * 4);
+            for (int s2 = 1; s2 < S; s2++) v += *reinterpret_cast<const f4*>(scr + ((size_t)(s2 * tiles + tile) * 64 + lane) * 4);
+            store(dst, v);
+        }
+    }
+}
+
+// weight gradient through wgrad_rows when the width allows it, else wgrad_px over the k-table kt
+// (built by the caller for K = taps * cin, cpt = cin, dilation d, sgn = +1)
+__device__ __forceinline__ void wgrad_any(const float* a, int sa, int a_off, const int* kt, int taps, int cin, int d,
+                                          const float* g, int sg, int g_off, int N, int H, int W,
+                                          const int64_t* __restrict__ bw_map, int64_t dw, int64_t db, int64_t lo,
+                                          float* __restrict__ row, float* scr, int scr_floats, const float* Z,
+                                          const float* ONE, bool direct = false, int64_t ck = 0, int64_t cbias = 0) {
+    if ((W & 3) == 0)
+        wgrad_rows(a, sa, a_off, taps, cin, d, g, sg, g_off, N, H, W, bw_map, dw, db, lo, row, scr, scr_floats, Z, ONE,
+                   direct, ck, cbias);
+    else
+        wgrad_px(a, sa, a_off, kt, taps * cin, g, sg, g_off, N, H, W, bw_map, dw, db, lo, row, scr, scr_floats, Z, direct,
+                 ck, cbias);
+}
+
+// Wl[t * cpt4 + o][n] = W[t][n][o] (the transposed conv's B operand: dgrad of a conv with dense weights
+// W[taps][cin][cout]), cpt4 = cout rounded up to 4; zero for o >= cout and n >= cin up to np columns
+__device__ __forceinline__ void stage_wt(const float* __restrict__ w, int taps, int cin, int cout, int np, float* wl) {
+    const int cpt4 = (cout + 3) & ~3, rows = taps * cpt4;
+    const uint32_t m_np = udiv_magic(np), m_c4 = udiv_magic(cpt4);
+    for (int e0 = threadIdx.x; e0 < rows * np; e0 += 4 * BWT) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int e = e0 + u * BWT;
+            const int k = udiv(e, m_np), n = e - k * np;
+            const int tap = udiv(k, m_c4), o = k - tap * cpt4;
+            v[u] = (e < rows * np && o < cout && n < cin) ? w[((size_t)tap * cin + n) * cout + o] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (e0 + u * BWT < rows * np) wl[e0 + u * BWT] = v[u];
     }
 }
 
@@ -249,15 +403,16 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
 // scale; dx = dL/dx to out ([HW][so] at o_off, stored or added), and the image's dgamma = d * xhat,
 // dbeta = d to its row. ln == false: LeakyReLU only. Channel quads when C % 4 == 0, LU of them per
 // thread with all their global loads issued before any is used (the passes are latency-bound).
-constexpr int LU = 8;
+constexpr int LU = 4;
 __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const float* __restrict__ gam, const float* d,
                        int sd, int d_off, float* out, int so, int o_off, bool accum, int HW, int C, bool ln,
                        float* __restrict__ rg, float* __restrict__ rb, double* red) {
     const int n = HW * C;
     const bool vq = ((C | sd | d_off | so | o_off) & 3) == 0;
     if (!ln) {
+        const uint32_t m_c0 = udiv_magic(C);
         for (int e = threadIdx.x; e < n; e += BWT) {
-            const int p = e / C, c = e - p * C;
+            const int p = udiv(e, m_c0), c = e - p * C;
             const float v = d[p * sd + d_off + c] * lrelu_d(x[e]);
             float* o = out + p * so + o_off + c;
             *o = accum ? *o + v : v;
@@ -267,6 +422,7 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
     }
     double sg = 0.0, sgh = 0.0;
     const int C4 = C >> 2, n4 = n >> 2;
+    const uint32_t m_c = udiv_magic(C), m_c4 = udiv_magic(C4);
     const f4* x4 = reinterpret_cast<const f4*>(x);
     if (vq) {
         for (int i0 = threadIdx.x; i0 < n4; i0 += LU * BWT) {
@@ -282,7 +438,7 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
             for (int u = 0; u < LU; u++) {
                 const int i = i0 + u * BWT;
                 if (i >= n4) break;
-                const int p = i / C4, c = (i - p * C4) << 2;
+                const int p = udiv(i, m_c4), c = (i - p * C4) << 2;
                 const f4 dv = *reinterpret_cast<const f4*>(d + p * sd + d_off + c);
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -295,7 +451,7 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
         }
     } else {
         for (int e = threadIdx.x; e < n; e += BWT) {
-            const int p = e / C, c = e - p * C;
+            const int p = udiv(e, m_c), c = e - p * C;
             const float xh = (lrelu_b(x[e]) - mu) * rs;
             const float g = d[p * sd + d_off + c] * gam[e];
             sg += g;
@@ -319,7 +475,7 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
             for (int u = 0; u < LU; u++) {
                 const int i = i0 + u * BWT;
                 if (i >= n4) break;
-                const int p = i / C4, c = (i - p * C4) << 2;
+                const int p = udiv(i, m_c4), c = (i - p * C4) << 2;
                 const f4 dv = *reinterpret_cast<const f4*>(d + p * sd + d_off + c);
                 f4* o = reinterpret_cast<f4*>(out + p * so + o_off + c);
                 f4 ov = accum ? *o : f4{0.f, 0.f, 0.f, 0.f};
@@ -335,7 +491,7 @@ __device__ void ln_bwd(const float* __restrict__ x, float mu, float rs, const fl
         }
     } else {
         for (int e = threadIdx.x; e < n; e += BWT) {
-            const int p = e / C, c = e - p * C;
+            const int p = udiv(e, m_c), c = e - p * C;
             const float xv = x[e];
             const float xh = (lrelu_b(xv) - mu) * rs;
             const float dv = d[p * sd + d_off + c];
@@ -355,12 +511,13 @@ __device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, in
                           const float* __restrict__ gam, const float* __restrict__ bet, bool ln, float* dst, int sd) {
     if (((C | c0 | nc | sd) & 3) == 0) {
         const int nq = nc >> 2, n4 = HW * nq;
+        const uint32_t m_nq = udiv_magic(nq);
         for (int i0 = threadIdx.x; i0 < n4; i0 += LU * BWT) {
             f4 xv[LU], gv[LU], bv[LU];
 #pragma unroll
             for (int u = 0; u < LU; u++) {
                 const int i = i0 + u * BWT;
-                const int p = i / nq, c = (i - p * nq) << 2;
+                const int p = udiv(i, m_nq), c = (i - p * nq) << 2;
                 const size_t gi = (size_t)p * C + c0 + c;
                 xv[u] = i < n4 ? *reinterpret_cast<const f4*>(x + gi) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -373,7 +530,7 @@ __device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, in
             for (int u = 0; u < LU; u++) {
                 const int i = i0 + u * BWT;
                 if (i >= n4) break;
-                const int p = i / nq, c = (i - p * nq) << 2;
+                const int p = udiv(i, m_nq), c = (i - p * nq) << 2;
                 f4 v;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -386,8 +543,9 @@ __device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, in
         return;
     }
     const int n = HW * nc;
+    const uint32_t m_nc = udiv_magic(nc);
     for (int e = threadIdx.x; e < n; e += BWT) {
-        const int p = e / nc, c = e - p * nc;
+        const int p = udiv(e, m_nc), c = e - p * nc;
         const size_t gi = (size_t)p * C + c0 + c;
         const float h = lrelu_b(x[gi]);
         dst[p * sd + c] = ln ? (h - mu) * rs * gam[gi] + bet[gi] : h;
@@ -430,7 +588,13 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     int* KT = reinterpret_cast<int*>(smem + a.off_kt);
     double* RED = reinterpret_cast<double*>(smem + a.off_red);
     int* OT = reinterpret_cast<int*>(smem + a.off_ot);
-    float* ZQ = reinterpret_cast<float*>(smem + a.off_z);   // 4 zeros, then 4 ones (kt_ptr)
+    float* ZQ = reinterpret_cast<float*>(smem + a.off_z);   // 4 zeros, then 4 ones (kt_ptr, wgrad_rows)
+    const float* ZR = ZQ + 8;                                  // a.zn zeros: gemm_tap's row outside the image
+    // zero the whole LDS image once: gemm_tap's padded channels read A values next to their windows, which
+    // must be finite
+    for (int i = threadIdx.x; i < (a.lds_bytes >> 4); i += BWT)
+        reinterpret_cast<f4*>(smem)[i] = f4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
     if (threadIdx.x < 8) ZQ[threadIdx.x] = threadIdx.x < 4 ? 0.f : 1.f;
     const int SY = a.sy, ST = a.st, SA = a.sa;
     int nst = 0;
@@ -448,13 +612,15 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     auto kp4 = [](int K) { return (K + 3) & ~3; };
     auto np16 = [](int N) { return (N + 15) & ~15; };
     const int taps = a.taps;
+    const uint32_t m_nk = udiv_magic(nk);
     if (OT[LDSBWD_TANH] >= 0 && threadIdx.x == 0) row[OT[LDSBWD_TANH] - lo] = 0.f;   // (k_dsum adds it)
 
     // ---- conv_out: G = dL/d so (dc2 ch) -> GT; A = LN_out(y_R) -> AC; wgrad; dgrad -> GY
     {
         const float* ds = a.dso[net] + (size_t)img * HW * a.dc2;
+        const uint32_t m_d2 = udiv_magic(a.dc2);
         for (int e = threadIdx.x; e < HW * a.dc2; e += BWT) {
-            const int p = e / a.dc2, c = e - p * a.dc2;
+            const int p = udiv(e, m_d2), c = e - p * a.dc2;
             GT[p * ST + c] = ds[e];
         }
         const float* yR = sv + (size_t)R * HW * nk;
@@ -464,15 +630,14 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, taps * nk, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row, WL, a.wmax, ZQ,
-                 true, OT[LDSBWD_CO_K], OT[LDSBWD_CO_B]);
+        wgrad_any(AC, SA, 0, KT, taps, nk, 1, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row,
+                  WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CO_K], OT[LDSBWD_CO_B]);
         __syncthreads();
         BSTAMP();
-        stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, kp4(taps * a.dc2), np16(nk), WL);
-        build_kt(KT, taps * a.dc2, kp4(taps * a.dc2), a.dc2, taps, 1, -1);
+        stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, np16(nk), WL);
         __syncthreads();
         BSTAMP();
-        gemm_any(GT, ST, 0, KT, kp4(taps * a.dc2), WL, np16(nk), GY, SY, 0, nk, H, W, false, ZQ);
+        gemm_tap_any(GT, ST, 0, taps, a.dc2, 1, -1, WL, np16(nk), GY, SY, 0, nk, H, W, false, ZR);
         __syncthreads();
         BSTAMP();
         // LN_out backward in place on GY
@@ -499,17 +664,16 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         BSTAMP();
             // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
             // gradient once, with the first chunk)
-            wgrad_px(AC, SA, 0, KT, nc, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
-                     c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ, true, o[LDSBWD_CB_K] + (int64_t)c0 * nk,
-                     o[LDSBWD_CB_B]);
+            wgrad_any(AC, SA, 0, KT, 1, nc, 1, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
+                      c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ, ZQ + 4, true,
+                      o[LDSBWD_CB_K] + (int64_t)c0 * nk, o[LDSBWD_CB_B]);
             __syncthreads();
         BSTAMP();
         }
-        stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, kp4(nk), np16(gc), WL);
-        build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
+        stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, np16(gc), WL);
         __syncthreads();
         BSTAMP();
-        gemm_any(GY, SY, 0, KT, kp4(nk), WL, np16(gc), GT, ST, 0, gc, H, W, false, ZQ);
+        gemm_tap_any(GY, SY, 0, 1, nk, 1, -1, WL, np16(gc), GT, ST, 0, gc, H, W, false, ZR);
         __syncthreads();
         BSTAMP();
         // ---- LN3 backward in place on GT -> dL/dt2
@@ -524,23 +688,22 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
             build_kt(KT, taps * cin, kp4(taps * cin), cin, taps, a.br_dil[bi], 1);
             __syncthreads();
         BSTAMP();
-            wgrad_px(AC, SA, 0, KT, taps * cin, GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
-                     o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row, WL, a.wmax, ZQ);
+            wgrad_any(AC, SA, 0, KT, taps, cin, a.br_dil[bi], GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
+                      o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row, WL, a.wmax, ZQ, ZQ + 4);
             __syncthreads();
         BSTAMP();
         }
         for (int e = threadIdx.x; e < HW * nk; e += BWT) {
-            const int p = e / nk, c = e - p * nk;
+            const int p = udiv(e, m_nk), c = e - p * nk;
             AC[p * SA + c] = 0.f;
         }
         for (int bi = 0; bi < a.nbr; bi++) {
             const int cin = a.br_cin[bi], cout = a.br_cout[bi];
-            stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, kp4(taps * cout), np16(cin), WL);
-            build_kt(KT, taps * cout, kp4(taps * cout), cout, taps, a.br_dil[bi], -1);
+            stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, np16(cin), WL);
             __syncthreads();
         BSTAMP();
-            gemm_any(GT, ST, a.br_out_off[bi], KT, kp4(taps * cout), WL, np16(cin), AC, SA, a.br_cin_off[bi], cin, H, W,
-                     true, ZQ);
+            gemm_tap_any(GT, ST, a.br_out_off[bi], taps, cout, a.br_dil[bi], -1, WL, np16(cin), AC, SA, a.br_cin_off[bi], cin,
+                         H, W, true, ZR);
             __syncthreads();
         BSTAMP();
         }
@@ -554,15 +717,14 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, nk, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL, a.wmax, ZQ,
-                 true, o[LDSBWD_CA_K], o[LDSBWD_CA_B]);
+        wgrad_any(AC, SA, 0, KT, 1, nk, 1, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL,
+                  a.wmax, ZQ, ZQ + 4, true, o[LDSBWD_CA_K], o[LDSBWD_CA_B]);
         __syncthreads();
         BSTAMP();
-        stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, kp4(nk), np16(nk), WL);
-        build_kt(KT, nk, kp4(nk), nk, 1, 1, -1);
+        stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, np16(nk), WL);
         __syncthreads();
         BSTAMP();
-        gemm_any(GT, ST, 0, KT, kp4(nk), WL, np16(nk), AC, SA, 0, nk, H, W, false, ZQ);
+        gemm_tap_any(GT, ST, 0, 1, nk, 1, -1, WL, np16(nk), AC, SA, 0, nk, H, W, false, ZR);
         __syncthreads();
         BSTAMP();
         // ---- LN1 backward: GY += dL/dy_r through conv_a (the identity path keeps GY)
@@ -573,27 +735,27 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     // ---- conv_in: A = u1c (gathered from the layer input) -> AC; wgrad with GY; dgrad -> GT -> du1c
     {
         const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
+        const uint32_t m_d1 = udiv_magic(a.dc1);
         for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
-            const int p = e / a.dc1, c = e - p * a.dc1;
+            const int p = udiv(e, m_d1), c = e - p * a.dc1;
             AC[p * SA + c] = ub[mask_pos_b(a.mask, p, c, W, a.W, a.D)];
         }
         build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
         __syncthreads();
         BSTAMP();
-        wgrad_px(AC, SA, 0, KT, taps * a.dc1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row, WL, a.wmax, ZQ,
-                 true, OT[LDSBWD_CI_K], OT[LDSBWD_CI_B]);
+        wgrad_any(AC, SA, 0, KT, taps, a.dc1, 1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row,
+                  WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CI_K], OT[LDSBWD_CI_B]);
         __syncthreads();
         BSTAMP();
-        stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, kp4(taps * nk), np16(a.dc1), WL);
-        build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, -1);
+        stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, np16(a.dc1), WL);
         __syncthreads();
         BSTAMP();
-        gemm_any(GY, SY, 0, KT, kp4(taps * nk), WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false, ZQ);
+        gemm_tap_any(GY, SY, 0, taps, nk, 1, -1, WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false, ZR);
         __syncthreads();
         BSTAMP();
         float* du = a.du1c[net] + (size_t)img * HW * a.dc1;
         for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
-            const int p = e / a.dc1, c = e - p * a.dc1;
+            const int p = udiv(e, m_d1), c = e - p * a.dc1;
             du[e] = GT[p * ST + c];
         }
     }

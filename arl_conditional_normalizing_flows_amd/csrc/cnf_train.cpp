@@ -91,16 +91,19 @@ size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
     a.ac_chunk = std::min(c.gc, ac / 4 * 4);
     auto kp4 = [](int K) { return (K + 3) / 4 * 4; };
     auto np16 = [](int N) { return (N + 15) / 16 * 16; };
-    // transposed-weight images of the data gradients, and the k-table lengths of every conv
-    size_t wmax = (size_t)kp4(taps * c.dc2) * np16(c.nk);
+    // transposed-weight images of the data gradients (rows: taps x the output channels rounded up to 4,
+    // stage_wt), the k-table lengths of the weight gradients, the zero row of gemm_tap (the widest A)
+    size_t wmax = (size_t)taps * kp4(c.dc2) * np16(c.nk);
     wmax = std::max(wmax, (size_t)kp4(c.nk) * np16(c.gc));
     wmax = std::max(wmax, (size_t)kp4(c.nk) * np16(c.nk));
-    wmax = std::max(wmax, (size_t)kp4(taps * c.nk) * np16(c.dc1));
-    int ktmax = std::max(kp4(taps * c.nk), std::max(kp4(taps * c.dc2), kp4(taps * c.dc1)));
+    wmax = std::max(wmax, (size_t)taps * kp4(c.nk) * np16(c.dc1));
+    int ktmax = std::max(kp4(taps * c.nk), kp4(taps * c.dc1));
     ktmax = std::max(ktmax, std::max(kp4(c.nk), kp4(a.ac_chunk)));
+    int zn = std::max(kp4(c.dc2), kp4(c.nk));
     for (const Branch& b : c.br) {
-        wmax = std::max(wmax, (size_t)kp4(taps * b.cout) * np16(b.cin));
-        ktmax = std::max(ktmax, std::max(kp4(taps * b.cout), kp4(taps * b.cin)));
+        wmax = std::max(wmax, (size_t)taps * kp4(b.cout) * np16(b.cin));
+        ktmax = std::max(ktmax, kp4(taps * b.cin));
+        zn = std::max(zn, kp4(b.cout));
     }
     auto al = [](size_t v) { return (v + 15) / 16 * 16; };
     size_t off = al((size_t)HW * a.sy * 4);
@@ -117,8 +120,8 @@ size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
     off = al(off + 16 * 8);
     a.off_ot = (int)off;
     off = al(off + (size_t)c.bwd_offs_per_net * 4);
-    a.off_z = (int)off;   // 4 zeros + 4 ones
-    off = al(off + 32);
+    a.off_z = (int)off;   // 4 zeros + 4 ones, then zn + 4 zeros (a lane reads up to kq + cpt4 - 1)
+    off = al(off + 32 + (size_t)(zn + 4) * 4);
     if (off > 160 * 1024) return 0;
     a.lds_bytes = (int)off;
     a.offs_per_net = c.bwd_offs_per_net;
@@ -321,9 +324,13 @@ void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, 
 
 // dW, db of a conv: X (cin channels at x_cs/x_off, LN-on-load) and dY (cout at dy_cs/dy_off)
 hipEvent_t tevent(Plan& p) {
+    static const int flags = [] {   // diagnostics: CNF_TRAIN_EVFLAGS=0 -> timing events
+        const char* e = std::getenv("CNF_TRAIN_EVFLAGS");
+        return e && std::atoi(e) == 0 ? (int)hipEventDefault : (int)hipEventDisableTiming;
+    }();
     if (p.tev_next == p.tev.size()) {
         hipEvent_t e;
-        hchk(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        hchk(hipEventCreateWithFlags(&e, flags), "hipEventCreate");
         p.tev.push_back(e);
     }
     return p.tev[p.tev_next++];
@@ -502,7 +509,6 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     const bool ln = E.p.desc.layer_norm != 0;
     const float* P = E.params;
     ensure_side(E.p);
-    E.p.tev_next = 0;   // every event of the previous coupling has been waited for (the join below)
     const bool wstreams = [] {   // A/B knob: weight gradients on the chain streams (read per call: tests switch it)
         const char* e = std::getenv("CNF_TRAIN_WSTREAM");
         return !(e && std::atoi(e) == 0);
@@ -538,7 +544,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         return l;
     };
     const LnIn raw{};
-    stream_wait(E.st, E1.st, E.p.ev_fork);   // u1c gathered
+    stream_wait(E.st, E1.st, tevent(E.p));   // u1c gathered
     for (int n = 0; n < 2 && !saved; n++) {
         TExec& En = *X[n];
         const NetParams& np = c.net[n];
@@ -561,7 +567,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         conv_fwd(En, h, w, Y(n, R), nk, 0, nk, lnin(n, R, np.ln_out_g, np.ln_out_b), np.co, c.dc2, 1, nullptr,
                  SO(n), c.dc2, 0);
     }
-    stream_wait(E1.st, E.st, E.p.ev_join);   // both nets' outputs
+    stream_wait(E1.st, E.st, tevent(E.p));   // both nets' outputs
     // coupling law backward -> du (u2 part, u1 copy), dL/d s_pre, dL/dt, dL/dw
     {
         CoupBwArgs a{};
@@ -588,8 +594,20 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         launch_coupling_backward(a, B, np, E.st);
         launch_dsum(a.dw_part, (long long)B * np, E.dparams + c.net[0].tanh_w, E.st);
     }
-    stream_wait(E.st, E1.st, E.p.ev_fork);   // dL/d s_pre, dL/dt
-    for (int n = 0; n < 2; n++) {
+    stream_wait(E.st, E1.st, tevent(E.p));   // dL/d s_pre, dL/dt
+    // The two chains are enqueued interleaved, phase by phase (conv_out; per residual block conv_b + LN3,
+    // the branches + LN2, conv_a + LN1; conv_in): the GPU starts a stream's kernels in about the order
+    // the host submitted them across streams (measured: no kernel ran more than ~15 submissions ahead of
+    // the newest finished one), so a chain enqueued whole after the other only overlapped it at the end.
+    // CNF_TRAIN_INTERLEAVE=0 enqueues net A's chain, then net b's (A/B).
+    const bool interleave = [] {
+        const char* e = std::getenv("CNF_TRAIN_INTERLEAVE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    hipEvent_t ev_gc[2] = {nullptr, nullptr}, ev_ca[2] = {nullptr, nullptr}, ev_cb[2] = {nullptr, nullptr};
+    // phase k of net n: 0 conv_out + LN_out; 1 + 3j + {0, 1, 2} residual block r = R - 1 - j: conv_b + LN3,
+    // the grouped branches + LN2, conv_a + LN1; 1 + 3R conv_in
+    auto phase = [&](int n, int k) {
         TExec& En = *X[n];
         float* dy = E.at<float>(E.T.dy[n]);
         float* dln = E.at<float>(E.T.dln[n]);
@@ -599,44 +617,57 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         float* dt2 = E.at<float>(E.T.dt2[n]);
         float* du1c = E.at<float>(E.T.du1c[n]);
         const NetParams& np = c.net[n];
-        const float* dso = E.at<float>(E.T.dso[n]);
-        const LnIn lo = lnin(n, R, np.ln_out_g, np.ln_out_b);
-        conv_wgrad(En, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
-        conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
-        ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+        if (k == 0) {
+            const float* dso = E.at<float>(E.T.dso[n]);
+            const LnIn lo = lnin(n, R, np.ln_out_g, np.ln_out_b);
+            conv_wgrad(En, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
+            conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
+            ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+            return;
+        }
+        if (k == 1 + 3 * R) {
+            conv_wgrad(En, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
+            conv_dgrad(En, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, 0);
+            return;
+        }
         // the weight gradients run behind the chain on En.wst; before the chain overwrites a dY buffer
         // it waits for the weight gradients reading it (of the block before: dt2, dt1; this block: dy)
-        hipEvent_t ev_gc = nullptr, ev_ca = nullptr;
-        for (int r = R - 1; r >= 0; r--) {
-            const RBParams& rb = np.rb[r];
-            // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
+        const int r = R - 1 - (k - 1) / 3, part = (k - 1) % 3;
+        const RBParams& rb = np.rb[r];
+        if (part == 0) {   // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
             const LnIn l3 = lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b);
-            const hipEvent_t ev_cb = conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
+            ev_cb[n] = conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
             conv_dgrad(En, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
-            chain_wait(En, ev_gc);
+            chain_wait(En, ev_gc[n]);
             ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
-            // grouped dilated branches
+        } else if (part == 1) {   // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
             hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
             for (size_t bi = 0; bi < c.br.size(); bi++) {
                 const Branch& b = c.br[bi];
-                ev_gc = conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout, rb.gc[bi],
-                                   b.dil);
+                ev_gc[n] = conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout,
+                                      rb.gc[bi], b.dil);
                 conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
             }
-            chain_wait(En, ev_ca);
+            chain_wait(En, ev_ca[n]);
             ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
-            // conv_a
+        } else {   // conv_a
             const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
-            ev_ca = conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
+            ev_ca[n] = conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
             conv_dgrad(En, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
-            chain_wait(En, ev_cb);
+            chain_wait(En, ev_cb[n]);
             ln_bwd(En, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
         }
-        conv_wgrad(En, h, w, u1c, c.dc1, 0, c.dc1, raw, dy, nk, 0, nk, np.ci, 1);
-        conv_dgrad(En, h, w, dy, nk, 0, nk, np.ci, c.dc1, 1, du1c, c.dc1, 0, 0);
+    };
+    const int nphase = 2 + 3 * R;
+    if (interleave) {
+        for (int k = 0; k < nphase; k++)
+            for (int n = 0; n < 2; n++) phase(n, k);
+    } else {
+        for (int n = 0; n < 2; n++)
+            for (int k = 0; k < nphase; k++) phase(n, k);
     }
-    stream_wait(E1.st, E.st, E.p.ev_join);   // net b's chain done
+    stream_wait(E1.st, E.st, tevent(E.p));   // net b's chain done
     for (int n = 0; n < 2; n++)                  // and both nets' weight gradients
         if (X[n]->wst) stream_wait(X[n]->wst, E.st, tevent(E.p));
     // du += the two nets' u1 gradients, net A's first (fixed order: bitwise reproducible)
@@ -652,6 +683,9 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     E.inv_batch_ = inv_batch;
     E.count = count;
     E.saved = true;
+    // pooled events: each record of this call gets its own (a re-recorded event that a queued wait still
+    // references serialised the two nets' chains on the GPU); the previous call's waits are all enqueued
+    p.tev_next = 0;
     const WsLayout& L = E.L;
     const int* T = p.dev_table;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
@@ -696,6 +730,7 @@ void coupling_layer_backward(Plan& p, int ci, const float* params, const float* 
                              float g_ld, void* workspace, int B, float* dparams, hipStream_t st) {
     TExec E{p, params, dparams, (char*)workspace, p.layout(B), p.train_layout(B), B, st};
     E.inv_batch_ = -g_ld;
+    p.tev_next = 0;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
     hchk(hipMemsetAsync(dparams, 0, (size_t)p.n_params * 4, st), "hipMemsetAsync");
     coupling_backward(E, p.couplings[ci], u, dv, du);

@@ -133,6 +133,11 @@ __global__ __launch_bounds__(256) void k_tconv(TConvArgs a) {
 // its (shifted) pixel, loaded straight from global with LN + LeakyReLU applied in registers. The
 // K order inside a group is permuted identically on both operands, so the sum is the conv's.
 // ------------------------------------------------------------------------------------------------
+#ifndef CNF_TW_U
+#define CNF_TW_U 8
+#endif
+constexpr int TW_U = CNF_TW_U;   // weight-staging loads in flight per thread
+
 template <int NR, bool VEC>
 __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     extern __shared__ __attribute__((aligned(16))) float wsm[];
@@ -151,17 +156,26 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
 #pragma unroll
     for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
     const int nw = G * 16 * NS;   // weight floats of one tap
+    // (TW_U loads in flight per thread: the transposed weight reads are scattered 4-byte loads, and one
+    // at a time they cost a memory round trip each)
     auto stage_w = [&](int tap, float* dst) {
-        for (int e = threadIdx.x; e < nw; e += 256) {
-            const int s4 = e & 3, j = (e >> 2) % NS, gq = (e >> 2) / NS;   // gq = 4g + kq'
-            const int k = 4 * gq + s4, n = n0 + j;
-            dst[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+        for (int e0 = threadIdx.x; e0 < nw; e0 += 256 * TW_U) {
+            float v[TW_U];
+#pragma unroll
+            for (int u = 0; u < TW_U; u++) {
+                const int e = e0 + 256 * u;
+                const int s4 = e & 3, j = (e >> 2) % NS, gq = (e >> 2) / NS;   // gq = 4g + kq'
+                const int k = 4 * gq + s4, n = n0 + j;
+                v[u] = (e < nw && k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < TW_U; u++)
+                if (e0 + 256 * u < nw) dst[e0 + 256 * u] = v[u];
         }
     };
     // A operand of flat step it = tap * G + g: raw channels 16g + 4kq .. +3 of the lane's shifted pixel
     // (+ its LN gamma / beta), loaded one step ahead so the loads overlap the previous step's MFMAs
-    auto load = [&](int it, f4& x, f4& gm, f4& bt) -> bool {
-        const int tap = it / G, g = it - tap * G;
+    auto load = [&](int tap, int g, f4& x, f4& gm, f4& bt) -> bool {
         const int dr = a.taps == 1 ? 0 : tap / 3 - 1, dc = a.taps == 1 ? 0 : tap % 3 - 1;
         const int r = pr + a.sgn * a.dil * dr, c = pc + a.sgn * a.dil * dc;
         const int k0 = 16 * g + 4 * kq;
@@ -193,16 +207,18 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     }
     const int total = a.taps * G;
     f4 xn, gn, bn;
-    bool vn = load(0, xn, gn, bn);
+    bool vn = load(0, 0, xn, gn, bn);
+    // (tap, g) of step it and of step it + 1, advanced incrementally: an integer division per step is
+    // ~30 VALU instructions even on uniform operands
+    int tap = 0, g = 0, tap1 = G == 1 ? 1 : 0, g1 = G == 1 ? 0 : 1;
     for (int it = 0; it < total; it++) {
-        const int tap = it / G, g = it - tap * G;
         f4 x = xn, gm = gn, bt = bn;
         const bool v = vn;
         if (g == 0 && !all_taps) {
             __syncthreads();   // the previous tap's B reads are done
             stage_w(tap, wsm);
         }
-        if (it + 1 < total) vn = load(it + 1, xn, gn, bn);
+        if (it + 1 < total) vn = load(tap1, g1, xn, gn, bn);
         if (g == 0 && (!all_taps ? true : tap == 0)) __syncthreads();
         if (v) {
             if (ln) {
@@ -219,6 +235,12 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
             const f4 bv = bw[16 * m];
 #pragma unroll
             for (int s = 0; s < 4; s++) acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], bv[s], acc[m], 0, 0, 0);
+        }
+        tap = tap1;
+        g = g1;
+        if (++g1 == G) {
+            g1 = 0;
+            tap1++;
         }
     }
     // acc[m][rr] = out[pixel p0 + 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
@@ -280,21 +302,25 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
 #pragma unroll
         for (int m = 0; m < NR; m++) acc[s][m] = f4{0.f, 0.f, 0.f, 0.f};
     const bool vq = (a.in_cs & 3) == 0 && (a.in_off & 3) == 0;
+    const uint32_t m_bw = udiv_magic(BW);
     for (int kc = 0; kc < a.K; kc += 64) {
         // quads up to the 16-channel group boundary (the MFMA reads whole groups: zeros past K)
         const int KC = min(64, a.K - kc), cq = ((KC + 15) >> 4) * 4;
         __syncthreads();   // the previous chunk's reads are done
         // band: quads of KC channels (zero beyond KC / outside the image), LN on load
         const int nq = BH * BW * cq;
+        const uint32_t m_cq = udiv_magic(cq);
         for (int e0 = threadIdx.x; e0 < nq; e0 += 256 * 4) {
             f4 v[4];
+            int lo[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int e = e0 + 256 * u;
                 v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                const int pb = udiv(e, m_cq), q = e - pb * cq;
+                lo[u] = pb * TB_KS + 4 * q;
                 if (e < nq) {
-                    const int q = e % cq, pb = e / cq;
-                    const int br = pb / BW, bc = pb - br * BW;
+                    const int br = udiv(pb, m_bw), bc = pb - br * BW;
                     const int r = r0 - d + br, c = bc - d;
                     if (r >= 0 && r < H && c >= 0 && c < W) {
                         const int k = kc + 4 * q;
@@ -326,20 +352,27 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int e = e0 + 256 * u;
-                if (e < nq) *reinterpret_cast<f4*>(band + (size_t)(e / cq) * TB_KS + 4 * (e % cq)) = v[u];
-            }
+            for (int u = 0; u < 4; u++)
+                if (e0 + 256 * u < nq) *reinterpret_cast<f4*>(band + lo[u]) = v[u];
         }
         // weights of the chunk: [tap][gq = 4g + kq'][j][s], k = kc + 16g + 4kq' + s (every tap at once
         // when they fit next to the band, else one tap at a time)
         auto stage_w = [&](int t0, int nt) {
             const int nwc = nt * 16 * NS * 4;
-            for (int e = threadIdx.x; e < nwc; e += 256) {
-                const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * 16 + gq
-                const int tap = t0 + (rest >> 4), gq = rest & 15;
-                const int k = kc + 4 * gq + s4, n = n0 + j;
-                wl[e] = (k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+            for (int e0 = threadIdx.x; e0 < nwc; e0 += 256 * TW_U) {
+                float v[TW_U];
+#pragma unroll
+                for (int u = 0; u < TW_U; u++) {
+                    const int e = e0 + 256 * u;
+                    const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * 16 + gq
+                    const int tap = t0 + (rest >> 4), gq = rest & 15;
+                    const int k = kc + 4 * gq + s4, n = n0 + j;
+                    v[u] = (e < nwc && k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn]
+                                                           : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < TW_U; u++)
+                    if (e0 + 256 * u < nwc) wl[e0 + 256 * u] = v[u];
             }
         };
         if (all_taps) stage_w(0, 9);
@@ -578,8 +611,15 @@ __host__ __device__ constexpr int wg_stride(int c) {   // LDS row stride == 16 (
     return ((c + 15) / 16 * 16) % 32 == 0 ? (c + 15) / 16 * 16 + 16 : (c + 15) / 16 * 16;
 }
 
+// (at least 3 waves per SIMD: the launch fits 2-3 workgroups per CU by LDS, and without the bound the
+// 8-deep staging loads took 266 registers, one wave per SIMD)
+#ifndef CNF_WG_U
+#define CNF_WG_U 4
+#endif
+constexpr int WG_U = CNF_WG_U;   // staging loads in flight per thread and array
 template <int TR>
-__global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nunits, int abl) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wgrad_band(WGradArgs a, int RB,
+                                                                                          int nunits, int abl) {
     extern __shared__ __attribute__((aligned(16))) float wsm[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i16 = lane & 15, kq = lane >> 4;
     const int H = a.H, W = a.W, npx = H * W;
@@ -612,6 +652,8 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
     const bool qx = (CIB & 3) == 0 && (a.x_cs & 3) == 0 && ((a.x_off + ci0) & 3) == 0 &&
                     (!ln || ((((uintptr_t)a.gamma) | ((uintptr_t)a.beta)) & 15) == 0);
     const bool qd = (COB & 3) == 0 && (a.dy_cs & 3) == 0 && ((a.dy_off + co0) & 3) == 0;
+    const uint32_t m_cq = udiv_magic(CIB >> 2), m_ci = udiv_magic(CIB), m_wb = udiv_magic(WB), m_dq = udiv_magic(COB >> 2),
+                   m_co = udiv_magic(COB);
     for (int unit = blockIdx.x; unit < nunits; unit += gridDim.x) {
         const int b = unit / bands, r0 = (unit - b * bands) * RB;
         const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
@@ -623,15 +665,17 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
         if (abl & 1) {
         } else if (qx) {
             const int cq = CIB >> 2, nxq = RB * WB * cq;
-            for (int e0 = t; e0 < nxq; e0 += 256 * 8) {
-                f4 v[8];
+            for (int e0 = t; e0 < nxq; e0 += 256 * WG_U) {
+                f4 v[WG_U];
+                int lo[WG_U];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < WG_U; u++) {
                     const int e = e0 + 256 * u;
                     v[u] = f4{0.f, 0.f, 0.f, 0.f};
+                    const int pb = udiv(e, m_cq), c = (e - pb * cq) * 4;
+                    lo[u] = pb * XS + c;
                     if (e < nxq) {
-                        const int c = (e % cq) * 4, pb = e / cq;
-                        const int br = pb / WB, bc = pb - br * WB;
+                        const int br = udiv(pb, m_wb), bc = pb - br * WB;
                         const int r = r0 + a.dil * dr + br, cc = bc - hx;
                         if (r >= 0 && r < H && cc >= 0 && cc < W) {
                             const size_t gi = ((size_t)r * W + cc) * a.x_cs + c;
@@ -650,22 +694,22 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int e = e0 + 256 * u;
-                    if (e < nxq) *reinterpret_cast<f4*>(Xs + (e / cq) * XS + (e % cq) * 4) = v[u];
-                }
+                for (int u = 0; u < WG_U; u++)
+                    if (e0 + 256 * u < nxq) *reinterpret_cast<f4*>(Xs + lo[u]) = v[u];
             }
         } else {
             const int nx = RB * WB * CIB;
-            for (int e0 = t; e0 < nx; e0 += 256 * 8) {
-                float v[8];
+            for (int e0 = t; e0 < nx; e0 += 256 * WG_U) {
+                float v[WG_U];
+                int lo[WG_U];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < WG_U; u++) {
                     const int e = e0 + 256 * u;
                     v[u] = 0.f;
+                    const int pb = udiv(e, m_ci), c = e - pb * CIB;
+                    lo[u] = pb * XS + c;
                     if (e < nx) {
-                        const int c = e % CIB, pb = e / CIB;
-                        const int br = pb / WB, bc = pb - br * WB;
+                        const int br = udiv(pb, m_wb), bc = pb - br * WB;
                         const int r = r0 + a.dil * dr + br, cc = bc - hx;
                         if (r >= 0 && r < H && cc >= 0 && cc < W) {
                             const size_t gi = ((size_t)r * W + cc) * a.x_cs + c;
@@ -680,50 +724,45 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int e = e0 + 256 * u;
-                    if (e < nx) Xs[(e / CIB) * XS + e % CIB] = v[u];
-                }
+                for (int u = 0; u < WG_U; u++)
+                    if (e0 + 256 * u < nx) Xs[lo[u]] = v[u];
             }
         }
         if (abl & 1) {
         } else if (qd) {
             const int cq = COB >> 2, ndq = RB * W * cq;
-            for (int e0 = t; e0 < ndq; e0 += 256 * 8) {
-                f4 v[8];
+            for (int e0 = t; e0 < ndq; e0 += 256 * WG_U) {
+                f4 v[WG_U];
+                int lo[WG_U];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < WG_U; u++) {
                     const int e = e0 + 256 * u;
                     v[u] = f4{0.f, 0.f, 0.f, 0.f};
-                    if (e < ndq) {
-                        const int c = (e % cq) * 4, p = e / cq;
-                        if (r0 + p / W < H) v[u] = *reinterpret_cast<const f4*>(db + ((size_t)r0 * W + p) * a.dy_cs + c);
-                    }
+                    const int p = udiv(e, m_dq), c = (e - p * cq) * 4;
+                    lo[u] = p * DS + c;
+                    if (e < ndq && r0 * W + p < npx)
+                        v[u] = *reinterpret_cast<const f4*>(db + ((size_t)r0 * W + p) * a.dy_cs + c);
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int e = e0 + 256 * u;
-                    if (e < ndq) *reinterpret_cast<f4*>(Ds + (e / cq) * DS + (e % cq) * 4) = v[u];
-                }
+                for (int u = 0; u < WG_U; u++)
+                    if (e0 + 256 * u < ndq) *reinterpret_cast<f4*>(Ds + lo[u]) = v[u];
             }
         } else {
             const int nd = RB * W * COB;
-            for (int e0 = t; e0 < nd; e0 += 256 * 8) {
-                float v[8];
+            for (int e0 = t; e0 < nd; e0 += 256 * WG_U) {
+                float v[WG_U];
+                int lo[WG_U];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < WG_U; u++) {
                     const int e = e0 + 256 * u;
                     v[u] = 0.f;
-                    if (e < nd) {
-                        const int c = e % COB, p = e / COB;
-                        if (r0 + p / W < H) v[u] = db[((size_t)r0 * W + p) * a.dy_cs + c];
-                    }
+                    const int p = udiv(e, m_co), c = e - p * COB;
+                    lo[u] = p * DS + c;
+                    if (e < nd && r0 * W + p < npx) v[u] = db[((size_t)r0 * W + p) * a.dy_cs + c];
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const int e = e0 + 256 * u;
-                    if (e < nd) Ds[(e / COB) * DS + e % COB] = v[u];
-                }
+                for (int u = 0; u < WG_U; u++)
+                    if (e0 + 256 * u < nd) Ds[lo[u]] = v[u];
             }
         }
         {   // zero the dY rows past the unit's last pixel up to the next multiple of 4
@@ -731,20 +770,18 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
             for (int e = t; e < (nk4 - nk) * DS; e += 256) Ds[(size_t)nk * DS + e] = 0.f;
         }
         __syncthreads();
-        // K = the unit's pixels, 4 per k-step: lane (i16, kq) reads pixel s + kq = (pr, pc), tracked
-        // incrementally (W >= 4: at most one row wrap per step, no division); past the unit's last
-        // pixel dY is zero (padded rows) and X any staged value
+        // K = the unit's pixels, 4 per k-step: lane (i16, kq) reads pixel p = s + kq of the unit, row
+        // pr = p / W from a float reciprocal (the 1x1 band has no halo: its pixel is p); past the unit's
+        // last pixel dY is zero (padded rows) and X pixel 0 (finite)
         if (kact && !(abl & 2)) {   // column blocks past the outputs have nothing to compute
             const int nk = RB * W, nk4 = (nk + 3) & ~3;
-            int pr = 0, pc = kq + 4 * ks;
-            while (pc >= W) {
-                pc -= W;
-                pr++;
-            }
+            const float invW = 1.f / (float)W;
             const float* xl = Xs + 16 * cw + i16;
             const float* dl = Ds + (size_t)kq * DS + i16;
             for (int s = 4 * ks; s < nk4; s += 4 * WPG) {
-                const int xo = s + kq < nk ? (pr * WB + pc) * XS : 0;
+                const int p = s + kq;
+                const int pb = TR == 1 ? p : p + (int)(((float)p + 0.5f) * invW) * 2 * hx;   // band pixel
+                const int xo = p < nk ? pb * XS : 0;
                 float bv[4];
 #pragma unroll
                 for (int m = 0; m < 4; m++) bv[m] = m < MB ? dl[s * DS + 16 * m] : 0.f;
@@ -754,11 +791,6 @@ __global__ __launch_bounds__(256) void k_wgrad_band(WGradArgs a, int RB, int nun
 #pragma unroll
                     for (int m = 0; m < 4; m++)
                         if (m < MB) acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[m], acc[u][m], 0, 0, 0);
-                }
-                pc += 4 * WPG;
-                while (pc >= W) {
-                    pc -= W;
-                    pr++;
                 }
             }
         }

@@ -328,8 +328,9 @@ def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
     if rank == 0:
         fl_img, _by, _n = algorithmic_per_image(flow, B)
         ms = el / args.steps * 1e3
-        # backward = recompute (1x the forward convs) + data and weight gradients (2x): 4x forward FLOPs
-        tf = 4.0 * fl_img * G / (ms / 1e3) / 1e12 / world
+        # forward_train (1x the forward convs, activations saved) + the backward's data and weight
+        # gradients (2x): 3x the forward FLOPs
+        tf = 3.0 * fl_img * G / (ms / 1e3) / 1e12 / world
         out = {'metric': f'images/sec NLL train step (fwd + bwd + Adam), {cfg.name}',
                'value': round(G * args.steps / el, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': scaling,
