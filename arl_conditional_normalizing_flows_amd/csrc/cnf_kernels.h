@@ -368,6 +368,7 @@ struct TConvArgs {
     float* out;
     int out_cs, out_off, N, accumulate;
     int H, W, taps, dil, sgn, B;
+    const float* zero;        // >= 16 bytes of zeros, 16-byte aligned: what out-of-image loads read
 };
 void launch_tconv(const TConvArgs& a, hipStream_t st);
 
@@ -386,6 +387,7 @@ struct WGradArgs {
     float* part;
     float* bpart;
     int H, W, taps, dil, B, chunks, chunk_px;
+    const float* zero;   // k_wgrad_direct: >= 1 float of zeros (what lanes outside the image read)
 };
 void launch_wgrad(const WGradArgs& a, hipStream_t st);
 // k_wgrad_band (the MFMA weight gradient): partial rows per launch (<= WGRAD_MAX_CHUNKS), each
@@ -397,6 +399,10 @@ bool train_valu_kernels();   // CNF_TRAIN_VALU=1: the register-blocked VALU conv
 // k_wgrad_band handles this conv (taps 1 / 9, width >= 4, staged band within 160 KiB); otherwise the
 // weight gradient runs on the VALU k_wgrad (WGradArgs::chunk_px > 0) with a separate bias scatter
 bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO);
+// k_wgrad_direct (register-operand MFMA weight gradient, WGradArgs::chunk_px == -1): width % 4 == 0,
+// taps 1 / 9; its partial-row count (<= WGRAD_MAX_CHUNKS) for a batch of B images of H rows
+bool wgrad_direct_ok(int H, int W, int taps);
+int wgrad_direct_chunks(int B, int H);
 // dparams[map[i]] += sum_c part[c][i] for i < n (map[i] >= 0)
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st);
 void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st);

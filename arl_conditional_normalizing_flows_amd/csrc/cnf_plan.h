@@ -201,6 +201,7 @@ struct TrainLayout {
     size_t dy[2] = {}, dln[2] = {}, dbuf[2] = {}, dt1[2] = {}, dc[2] = {}, dt2[2] = {}, du1c[2] = {};
     size_t u1c = 0, duv[2] = {}, dzy = 0;
     size_t lnsum[2] = {}, wpart[2] = {}, bpart[2] = {}, lnpart[2] = {}, dwpart = 0;
+    size_t zeros = 0;   // 64 floats of zeros (k_wgrad_direct's address for loads outside the image)
     // fused LDS-layer backward: per coupling index the forward's save area [2][B][LdsSave::img] and s/t
     // outputs [2][B][hc][wc][dc2] (0: none), and the per-(net, image) gradient rows [2][B][row_max]
     std::vector<size_t> act_save, so_save;

@@ -191,14 +191,18 @@ TrainLayout Plan::train_layout(int B) const {
         // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
         T.lnpart[n] = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
     }
-    int chunks = 1;
-    for (const Coupling& c : couplings) chunks = std::max(chunks, wgrad_chunks(B, c.hc * c.wc));
-    // the MFMA weight gradient writes up to WGRAD_MAX_CHUNKS rows of [weights | bias]
+    int chunks = 1, mchunks = WGRAD_MAX_CHUNKS;
+    for (const Coupling& c : couplings) {
+        chunks = std::max(chunks, wgrad_chunks(B, c.hc * c.wc));
+        mchunks = std::max(mchunks, wgrad_direct_chunks(B, c.hc));   // (B of them once B > WGRAD_MAX_CHUNKS)
+    }
+    // the MFMA weight gradients write up to mchunks rows of [weights | bias]
     for (int n = 0; n < 2; n++) {
-        T.wpart[n] = take((size_t)std::max(chunks, WGRAD_MAX_CHUNKS) * (m_dense + m_co) * 4);
+        T.wpart[n] = take((size_t)std::max(chunks, mchunks) * (m_dense + m_co) * 4);
         T.bpart[n] = take((size_t)chunks * m_co * 4);
     }
     T.dwpart = take(Bz * std::max(1, L.ld_parts) * 8);
+    T.zeros = take(64 * 4);
     T.act_save.assign(couplings.size(), 0);
     T.so_save.assign(couplings.size(), 0);
     for (const Coupling& c : couplings) {
@@ -293,6 +297,7 @@ void conv_fwd(TExec& E, int h, int w, const float* in, int in_cs, int in_off, in
     a.dil = dil;
     a.sgn = 1;
     a.B = E.B;
+    a.zero = E.at<float>(E.T.zeros);
     launch_tconv(a, E.st);
 }
 
@@ -319,6 +324,7 @@ void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, 
     a.dil = dil;
     a.sgn = -1;
     a.B = E.B;
+    a.zero = E.at<float>(E.T.zeros);
     launch_tconv(a, E.st);
 }
 
@@ -394,9 +400,20 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
         launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
         return nullptr;
     }
-    // k_wgrad_band: rows of [weights | bias]; the dense image keeps the bias right after the
-    // weights (pc.db == pc.dw + taps * cin * cout), so one scatter reduces both
-    a.chunks = wgrad_band_chunks(E.B, h, w, pc.taps, cin, cout);
+    // k_wgrad_direct (k_wgrad_band with CNF_WGRAD_DIRECT=0): rows of [weights | bias]; the dense image
+    // keeps the bias right after the weights (pc.db == pc.dw + taps * cin * cout), so one scatter
+    // reduces both
+    const bool direct = [] {   // (read per call: tests switch it)
+        const char* e = std::getenv("CNF_WGRAD_DIRECT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (direct && wgrad_direct_ok(h, w, pc.taps)) {
+        a.chunks = wgrad_direct_chunks(E.B, h);
+        a.chunk_px = -1;
+        a.zero = E.at<float>(E.T.zeros);
+    } else {
+        a.chunks = wgrad_band_chunks(E.B, h, w, pc.taps, cin, cout);
+    }
     launch_wgrad(a, E.st);
     if (pc.db != pc.dw + nw) throw std::logic_error("dense image: bias not after the weights");
     launch_grad_scatter(a.part, a.chunks, nw + cout, map + pc.dw, E.dparams, E.st);
@@ -690,6 +707,7 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     const int* T = p.dev_table;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
     hchk(hipMemsetAsync(dparams, 0, (size_t)p.n_params * 4, st), "hipMemsetAsync");
+    hchk(hipMemsetAsync(E.at<float>(E.T.zeros), 0, 64 * 4, st), "hipMemsetAsync");
     const int nuv = (int)L.n_uv;
     const cnf_flow_desc& d = p.desc;
     float* dzy = E.at<float>(E.T.dzy);
@@ -733,6 +751,7 @@ void coupling_layer_backward(Plan& p, int ci, const float* params, const float* 
     p.tev_next = 0;
     if (p.n_bw > 0) launch_pack(params, p.dev_bw_map, E.at<float>(E.T.bw), (long long)p.n_bw, st);
     hchk(hipMemsetAsync(dparams, 0, (size_t)p.n_params * 4, st), "hipMemsetAsync");
+    hchk(hipMemsetAsync(E.at<float>(E.T.zeros), 0, 64 * 4, st), "hipMemsetAsync");
     coupling_backward(E, p.couplings[ci], u, dv, du);
     hchk(hipGetLastError(), "training kernel launch");
 }

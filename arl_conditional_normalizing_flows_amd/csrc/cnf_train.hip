@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
                 const int e = e0 + 256 * u;
                 const int s4 = e & 3, j = (e >> 2) % NS, gq = (e >> 2) / NS;   // gq = 4g + kq'
                 const int k = 4 * gq + s4, n = n0 + j;
-                v[u] = (e < nw && k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn] : 0.f;
+                const bool ok = e < nw && k < a.K && n < a.N;
+                v[u] = *(ok ? a.w + (tap * a.wt + (long long)k * a.wk + (long long)n * a.wn) : a.zero);
             }
 #pragma unroll
             for (int u = 0; u < TW_U; u++)
@@ -180,16 +181,19 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
         const int r = pr + a.sgn * a.dil * dr, c = pc + a.sgn * a.dil * dc;
         const int k0 = 16 * g + 4 * kq;
         const bool sv = pav && r >= 0 && r < a.H && c >= 0 && c < a.W && k0 < a.K;
+        const size_t gi = ((size_t)r * a.W + c) * a.in_cs + k0;
+        if (VEC) {   // branch-free: an invalid lane reads zeros (the caller's LN / LeakyReLU maps them to 0)
+            x = *reinterpret_cast<const f4*>(sv ? inb + gi : a.zero);
+            gm = bt = f4{0.f, 0.f, 0.f, 0.f};
+            if (ln) {
+                gm = *reinterpret_cast<const f4*>(sv ? a.gamma + a.in_off + gi : a.zero);
+                bt = *reinterpret_cast<const f4*>(sv ? a.beta + a.in_off + gi : a.zero);
+            }
+            return sv;
+        }
         x = gm = bt = f4{0.f, 0.f, 0.f, 0.f};
         if (!sv) return false;
-        const size_t gi = ((size_t)r * a.W + c) * a.in_cs + k0;
-        if (VEC) {
-            x = *reinterpret_cast<const f4*>(inb + gi);
-            if (ln) {
-                gm = *reinterpret_cast<const f4*>(a.gamma + a.in_off + gi);
-                bt = *reinterpret_cast<const f4*>(a.beta + a.in_off + gi);
-            }
-        } else {
+        {
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 if (k0 + j < a.K) {
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
         }
         if (it + 1 < total) vn = load(tap1, g1, xn, gn, bn);
         if (g == 0 && (!all_taps ? true : tap == 0)) __syncthreads();
-        if (v) {
+        if (VEC || v) {   // (VEC: invalid lanes hold zeros, which this maps to 0)
             if (ln) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) x[j] = (lrelu(x[j]) - mu) * rs * gm[j] + bt[j];
@@ -302,6 +306,8 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
 #pragma unroll
         for (int m = 0; m < NR; m++) acc[s][m] = f4{0.f, 0.f, 0.f, 0.f};
     const bool vq = (a.in_cs & 3) == 0 && (a.in_off & 3) == 0;
+    // whole quads of K from 16-byte loads (and aligned gamma / beta): the branch-free staging path
+    const bool fullq = vq && (a.K & 3) == 0 && (!ln || ((((uintptr_t)a.gamma) | ((uintptr_t)a.beta)) & 15) == 0);
     const uint32_t m_bw = udiv_magic(BW);
     for (int kc = 0; kc < a.K; kc += 64) {
         // quads up to the 16-channel group boundary (the MFMA reads whole groups: zeros past K)
@@ -319,11 +325,26 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 v[u] = f4{0.f, 0.f, 0.f, 0.f};
                 const int pb = udiv(e, m_cq), q = e - pb * cq;
                 lo[u] = pb * TB_KS + 4 * q;
-                if (e < nq) {
-                    const int br = udiv(pb, m_bw), bc = pb - br * BW;
-                    const int r = r0 - d + br, c = bc - d;
-                    if (r >= 0 && r < H && c >= 0 && c < W) {
-                        const int k = kc + 4 * q;
+                const int br = udiv(pb, m_bw), bc = pb - br * BW;
+                const int r = r0 - d + br, c = bc - d, k = kc + 4 * q;
+                const bool in = e < nq && r >= 0 && r < H && c >= 0 && c < W;
+                if (fullq) {
+                    // branch-free: lanes outside the image (or past K) read zeros for x, gamma and beta,
+                    // which the LN / LeakyReLU map to exactly 0
+                    const bool ok = in && k < a.K;
+                    const size_t gi = ((size_t)r * W + c) * a.in_cs + k;
+                    const f4 x = *reinterpret_cast<const f4*>(ok ? inb + gi : a.zero);
+                    if (ln) {
+                        const f4 gq = *reinterpret_cast<const f4*>(ok ? a.gamma + a.in_off + gi : a.zero);
+                        const f4 bq = *reinterpret_cast<const f4*>(ok ? a.beta + a.in_off + gi : a.zero);
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++) v[u][jj] = (lrelu(x[jj]) - mu) * rs * gq[jj] + bq[jj];
+                    } else {
+#pragma unroll
+                        for (int jj = 0; jj < 4; jj++) v[u][jj] = a.act ? lrelu(x[jj]) : x[jj];
+                    }
+                } else if (in) {
+                    {
                         const size_t gi = ((size_t)r * W + c) * a.in_cs + k;
                         f4 x = f4{0.f, 0.f, 0.f, 0.f}, gm = f4{1.f, 1.f, 1.f, 1.f}, bt = f4{0.f, 0.f, 0.f, 0.f};
                         if (vq && k + 4 <= a.K) {
@@ -367,8 +388,8 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                     const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * 16 + gq
                     const int tap = t0 + (rest >> 4), gq = rest & 15;
                     const int k = kc + 4 * gq + s4, n = n0 + j;
-                    v[u] = (e < nwc && k < a.K && n < a.N) ? a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn]
-                                                           : 0.f;
+                    const bool ok = e < nwc && k < a.K && n < a.N;
+                    v[u] = *(ok ? a.w + (tap * a.wt + (long long)k * a.wk + (long long)n * a.wn) : a.zero);
                 }
 #pragma unroll
                 for (int u = 0; u < TW_U; u++)
@@ -849,6 +870,196 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     if (do_bias && t < COB) part[(size_t)a.taps * a.CI * a.CO + co0 + t] = bacc;
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_wgrad_direct: weight (and bias) gradient of a 1x1 (TR = 1) or 3x3 (TR = 3) conv on MFMA with both
+// operands loaded straight from global memory into registers (no LDS staging, no barriers in the
+// loop). The GEMM is dW[r][n] = sum over pixels of A(p, r) G(p, n), r = tap * CI + ci the kernel row
+// (A = LN(LeakyReLU(x)) at the tap's shifted pixel, zero outside the image), n < CO. A workgroup owns
+// one (image, band of RB rows) unit — its partial row is the unit's — and MT x NT 16x16 blocks of
+// (r, n) (grid.y / grid.z tile the rest); its 4 waves take alternate 4-pixel steps along the band's
+// rows (width % 4 == 0), each step's loads issued one step ahead of its MFMAs, and their sums are
+// added in wave order through LDS (deterministic). The bias gradient (sum of G) is summed on the VALU
+// from the same G loads by the grid.y == 0 workgroups. Partial rows as k_wgrad_band: [taps][CI][CO]
+// then [CO], reduced by k_grad_scatter.
+// ------------------------------------------------------------------------------------------------
+template <int MT, int NT, int TR>
+__global__ __launch_bounds__(256) void k_wgrad_direct(WGradArgs a, int RB, int nbands) {
+    extern __shared__ __attribute__((aligned(16))) float wdsm[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, kq = lane >> 4;
+    const int H = a.H, W = a.W, npx = H * W, CI = a.CI, CO = a.CO;
+    const int chunk = blockIdx.x, b = chunk / nbands, y0 = (chunk - b * nbands) * RB, y1 = min(H, y0 + RB);
+    const int rows = a.taps * CI, r0 = blockIdx.y * MT * 16, n0 = blockIdx.z * NT * 16;
+    const bool ln = a.stats != nullptr, act = ln || a.act;
+    const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+    // the lane's kernel rows: channel offset, tap shift, validity
+    int cof[MT], dr[MT], dc[MT];
+    bool rv[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++) {
+        const int r = r0 + 16 * mt + i16;
+        rv[mt] = r < rows;
+        const int t = rv[mt] ? r / CI : 0;
+        cof[mt] = r - t * CI;
+        dr[mt] = TR == 3 ? a.dil * (t / 3 - 1) : 0;
+        dc[mt] = TR == 3 ? a.dil * (t % 3 - 1) : 0;
+    }
+    bool nv[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) nv[nt] = n0 + 16 * nt + i16 < CO;
+    const float* xb = a.x + (size_t)b * npx * a.x_cs + a.x_off;
+    const float* gm = ln ? a.gamma + a.x_off : nullptr;
+    const float* bt = ln ? a.beta + a.x_off : nullptr;
+    const float* gb = a.dy + (size_t)b * npx * a.dy_cs + a.dy_off + n0 + i16;
+    const int W4 = W >> 2, nsteps = (y1 - y0) * W4;
+    const uint32_t m_w4 = udiv_magic(W4);
+    const bool do_bias = a.bpart != nullptr && blockIdx.y == 0;
+    f4 acc[MT][NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+    float bsum[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) bsum[nt] = 0.f;
+    // raw operands of step j: x (+ gamma, beta) per kernel row, G per column block. Branch-free and with
+    // no select after a load: a lane outside the image (or past CO) reads the zero float a.zero for every
+    // operand, so x = gamma = beta = 0 and its A is exactly 0; the next step's loads are issued before
+    // this step's MFMAs and waited for only at the next step
+    const float* zp = a.zero;
+    float xr[MT], gr[MT], br[MT], gv[NT];
+    auto load = [&](int j) {
+        const int q = udiv(j, m_w4), yy = y0 + q, xx = 4 * (j - q * W4) + kq;
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) {
+            const int y = yy + dr[mt], x = xx + dc[mt];
+            const bool ok = rv[mt] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+            const int idx = (y * W + x) * a.x_cs + cof[mt];
+            xr[mt] = *(ok ? xb + idx : zp);
+            if (ln) {
+                gr[mt] = *(ok ? gm + idx : zp);
+                br[mt] = *(ok ? bt + idx : zp);
+            }
+        }
+        const int gi = (yy * W + xx) * a.dy_cs;
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) gv[nt] = *(nv[nt] ? gb + gi + 16 * nt : zp);
+    };
+    int j = wave;
+    if (j < nsteps) load(j);
+    for (; j < nsteps; j += 4) {
+        float av[MT], g[NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++) {
+            const float h = act ? lrelu(xr[mt]) : xr[mt];
+            av[mt] = ln ? (h - mu) * rs * gr[mt] + br[mt] : h;
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) g[nt] = gv[nt];
+        if (j + 4 < nsteps) load(j + 4);
+#pragma unroll
+        for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[mt], g[nt], acc[mt][nt], 0, 0, 0);
+        if (do_bias) {
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) bsum[nt] += g[nt];
+        }
+    }
+    // waves 3, 2, 1 add their sums into LDS in that order; wave 0 adds its own and stores the row
+    f4* red = reinterpret_cast<f4*>(wdsm);   // [MT * NT][64]
+    float* bred = wdsm + MT * NT * 64 * 4;   // [NT][64]
+    for (int w = 3; w >= 1; w--) {
+        if (wave == w) {
+#pragma unroll
+            for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+                for (int nt = 0; nt < NT; nt++) {
+                    f4& d = red[(mt * NT + nt) * 64 + lane];
+                    d = w == 3 ? acc[mt][nt] : d + acc[mt][nt];
+                }
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) bred[nt * 64 + lane] = w == 3 ? bsum[nt] : bred[nt * 64 + lane] + bsum[nt];
+        }
+        __syncthreads();
+    }
+    if (wave != 0) return;
+    float* part = a.part + (size_t)chunk * ((size_t)rows * CO + CO);
+#pragma unroll
+    for (int mt = 0; mt < MT; mt++)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) {
+            const f4 v = red[(mt * NT + nt) * 64 + lane] + acc[mt][nt];
+            const int n = n0 + 16 * nt + i16;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int r = r0 + 16 * mt + 4 * kq + q;
+                if (r < rows && n < CO) part[(size_t)r * CO + n] = v[q];
+            }
+        }
+    if (do_bias) {
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) {
+            // lanes i16 + 16 kq hold slices of column n0 + 16 nt + i16: add them in kq order
+            float v = bred[nt * 64 + lane] + bsum[nt];
+            const float v1 = __shfl(v, i16 + 16), v2 = __shfl(v, i16 + 32), v3 = __shfl(v, i16 + 48);
+            v = ((v + v1) + v2) + v3;
+            const int n = n0 + 16 * nt + i16;
+            if (kq == 0 && n < CO) part[(size_t)rows * CO + n] = v;
+        }
+    }
+}
+
+// k_wgrad_direct's unit split: bands of rows per image so that the launch writes <= WGRAD_MAX_CHUNKS
+// partial rows; its tiling: MT row blocks (<= 8) x NT column blocks (<= 4) per workgroup
+static void wgrad_direct_shape(const WGradArgs& a, int& RB, int& nbands, int& mt, int& nt, int& gy, int& gz) {
+    const int per_img = std::max(1, WGRAD_MAX_CHUNKS / std::max(1, a.B));
+    nbands = std::min(a.H, per_img);
+    RB = (a.H + nbands - 1) / nbands;
+    nbands = (a.H + RB - 1) / RB;
+    const int rb = (a.taps * a.CI + 15) / 16, cb = (a.CO + 15) / 16;
+    gy = (rb + 7) / 8;
+    mt = (rb + gy - 1) / gy;
+    gz = (cb + 3) / 4;
+    nt = (cb + gz - 1) / gz;
+    if (nt == 3) nt = 4;
+}
+
+bool wgrad_direct_ok(int H, int W, int taps) { return (W & 3) == 0 && W >= 4 && (taps == 1 || taps == 9); }
+
+int wgrad_direct_chunks(int B, int H) {
+    WGradArgs a{};
+    a.B = B;
+    a.H = H;
+    a.W = 4;
+    a.taps = 1;
+    a.CI = 1;
+    a.CO = 1;
+    int RB, nb, mt, nt, gy, gz;
+    wgrad_direct_shape(a, RB, nb, mt, nt, gy, gz);
+    return B * nb;
+}
+
+static void launch_wgrad_direct(const WGradArgs& a, hipStream_t st) {
+    int RB, nbands, mt, nt, gy, gz;
+    wgrad_direct_shape(a, RB, nbands, mt, nt, gy, gz);
+    if (a.B * nbands != a.chunks) throw std::logic_error("k_wgrad_direct: chunk count mismatch");
+    const dim3 g(a.B * nbands, gy, gz), blk(256);
+    const size_t lds = ((size_t)mt * nt * 64 * 4 + (size_t)nt * 64) * 4;
+#define CNF_WD(MT_, NT_)                                                                                   \
+    if (mt == MT_ && nt == NT_) {                                                                          \
+        if (a.taps == 9)                                                                                   \
+            hipLaunchKernelGGL((k_wgrad_direct<MT_, NT_, 3>), g, blk, lds, st, a, RB, nbands);              \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_wgrad_direct<MT_, NT_, 1>), g, blk, lds, st, a, RB, nbands);              \
+        return;                                                                                            \
+    }
+#define CNF_WD_N(MT_) CNF_WD(MT_, 1) CNF_WD(MT_, 2) CNF_WD(MT_, 4)
+    CNF_WD_N(1) CNF_WD_N(2) CNF_WD_N(3) CNF_WD_N(4) CNF_WD_N(5) CNF_WD_N(6) CNF_WD_N(7) CNF_WD_N(8)
+#undef CNF_WD_N
+#undef CNF_WD
+    throw std::logic_error("k_wgrad_direct: no instantiation for this tiling");
+}
+
 // rows per work unit (about 128 pixels) and the unit count of a wgrad launch
 static void wgrad_units(const WGradArgs& a, int& RB, int& nunits) {
     RB = a.W >= 128 ? 1 : 128 / a.W;
@@ -898,6 +1109,10 @@ bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO) {
 }
 
 void launch_wgrad(const WGradArgs& a, hipStream_t st) {
+    if (a.chunk_px == -1) {   // k_wgrad_direct (the caller checked wgrad_direct_ok and sized chunks)
+        launch_wgrad_direct(a, st);
+        return;
+    }
     if (a.chunk_px > 0) {   // k_wgrad, the VALU kernel: the caller chose it (CNF_TRAIN_VALU, or !wgrad_band_ok)
         const dim3 g(a.chunks, a.taps, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
         hipLaunchKernelGGL(k_wgrad, g, blk, 0, st, a);

@@ -151,6 +151,9 @@ GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'in
               # the multi-kernel backward for the k_net_lds layers too (CNF_LDS_BWD=0 at plan creation; by
               # default they run the fused k_lds_bwd over the training forward's saved activations)
               ('small', 3, {'_plan_env': {'CNF_LDS_BWD': '0'}}), ('cfg2', 2, {'_plan_env': {'CNF_LDS_BWD': '0'}}),
+              # the LDS-staged band weight gradients (k_wgrad_band) instead of the register-operand
+              # k_wgrad_direct (CNF_WGRAD_DIRECT=0, read per call)
+              ('cfg2', 2, {'_env': {'CNF_WGRAD_DIRECT': '0'}}),
               # the benched training batch (bench.py --mode train): the batch-sliced LN backward (up to 8
               # workgroups per image), the multi-unit band weight gradients and the four-stream schedule
               # all see their full-size partitions only here
