@@ -369,8 +369,18 @@ struct TConvArgs {
     int out_cs, out_off, N, accumulate;
     int H, W, taps, dil, sgn, B;
     const float* zero;        // >= 16 bytes of zeros, 16-byte aligned: what out-of-image loads read
+    // LN-backward reduction of the output (lnr_part non-null): the output v is dL/d(LN output) of the
+    // LayerNorm(LeakyReLU) whose raw input lnr_x has the output's layout; each workgroup adds sum v * gamma
+    // and sum v * gamma * xhat over its elements and writes them to lnr_part[b][tile][2] (fixed order)
+    const float* lnr_x;
+    const float* lnr_gamma;
+    const float* lnr_stats;
+    double* lnr_part;
 };
-void launch_tconv(const TConvArgs& a, hipStream_t st);
+// returns the LN-reduction partials per image the launch wrote (0: none — the kernel has no fused
+// reduction, the caller runs k_lnb_reduce)
+int launch_tconv(const TConvArgs& a, hipStream_t st);
+constexpr int LNR_MAXPARTS = 64;   // per image, k_tconv_* fused LN reductions
 
 // weight gradient: part[chunk][(tap*CI + ci)*CO + co] = sum over the chunk's pixels of
 // X[b, p + dil*off(tap), ci] * dY[b, p, co] (X with LN-on-load as in TConvArgs); bpart[chunk][co]
@@ -413,9 +423,10 @@ constexpr int LNB_SLICES = 8;
 // k_lnb_reduce splits each image over up to LNB_RS workgroups (partial sums [B][rs][2], summed in slice
 // order where they are read)
 constexpr int LNB_RS = 8;
+// presum > 0: sums already holds [B][presum][2] partials (a k_tconv_* fused LN reduction), no k_lnb_reduce
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st);
+                        float* scratch, hipStream_t st, int presum = 0);
 // Fused training backward of a k_net_lds layer (cnf_ldsbwd.hip): grid (B, 2 nets), one workgroup per
 // (image, net). Offsets table per net (int32, `offs_per_net` entries): canonical parameter offsets
 // (LN gamma / beta, the net's first parameter, tanh scale or -1) and dense backward-image offsets
@@ -451,6 +462,12 @@ struct LdsBwdArgs {
     int wmax;                                                   // floats of the W region (weight-gradient scratch too)
     int stamps;                                                 // diagnostics: phase clock stamps (CNF_LDSBWD_STAMPS)
     int off_gt, off_ac, off_w, off_kt, off_red, off_ot, off_z, lds_bytes;   // LDS byte offsets (GY at 0)
+    // split mode (CNF_LDS_SPLIT): 0 the whole backward; 1 the data-gradient chain only, storing the
+    // gradients the weight gradients contract with to gsave; 2 the weight gradients only, from gsave
+    int mode;
+    float* gsave;                       // [2][B][gsave_img] per (net, image)
+    int gsave_img, gs_rb, g_t3, g_t2, g_in;   // per residual block r: dL/dy_{r+1} at r * gs_rb, dL/dt2 at
+                                             // + g_t3, dL/dt1 at + g_t2; dL/dy_0 (conv_in's) at g_in
 };
 void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st);
 int read_bwd_stamps(long long* host, int n);   // [0] = count, [1..] = s_memtime per phase boundary

@@ -552,6 +552,52 @@ __device__ void stage_act(const float* __restrict__ x, int C, int c0, int nc, in
     }
 }
 
+// dst[p * C + c] = src[p * ss + c] (LDS -> global, dense) and back; C % 4 == 0 and ss % 4 == 0 take quads
+__device__ void store_lds(float* __restrict__ dst, const float* src, int ss, int HW, int C) {
+    if (((C | ss) & 3) == 0) {
+        const int cq = C >> 2, n = HW * cq;
+        const uint32_t m = udiv_magic(cq);
+        for (int i = threadIdx.x; i < n; i += BWT) {
+            const int p = udiv(i, m), c = (i - p * cq) << 2;
+            *reinterpret_cast<f4*>(dst + (size_t)p * C + c) = *reinterpret_cast<const f4*>(src + p * ss + c);
+        }
+        return;
+    }
+    const uint32_t m = udiv_magic(C);
+    for (int i = threadIdx.x; i < HW * C; i += BWT) {
+        const int p = udiv(i, m), c = i - p * C;
+        dst[i] = src[p * ss + c];
+    }
+}
+__device__ void load_lds(float* dst, int ss, const float* __restrict__ src, int HW, int C) {
+    if (((C | ss) & 3) == 0) {
+        const int cq = C >> 2, n = HW * cq;
+        const uint32_t m = udiv_magic(cq);
+        for (int i0 = threadIdx.x; i0 < n; i0 += 4 * BWT) {
+            f4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = min(i0 + u * BWT, n - 1);
+                const int p = udiv(i, m), c = (i - p * cq) << 2;
+                v[u] = *reinterpret_cast<const f4*>(src + (size_t)p * C + c);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * BWT;
+                if (i >= n) break;
+                const int p = udiv(i, m), c = (i - p * cq) << 2;
+                *reinterpret_cast<f4*>(dst + p * ss + c) = v[u];
+            }
+        }
+        return;
+    }
+    const uint32_t m = udiv_magic(C);
+    for (int i = threadIdx.x; i < HW * C; i += BWT) {
+        const int p = udiv(i, m), c = i - p * C;
+        dst[p * ss + c] = src[i];
+    }
+}
+
 // position in u of element (pixel p, channel c) of the mask-compressed u1c (mask compress, :720-759)
 __device__ __forceinline__ int mask_pos_b(int m, int p, int c, int wc, int W, int D) {
     const int pr = p / wc, pc = p - pr * wc;
@@ -613,7 +659,11 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
     auto np16 = [](int N) { return (N + 15) & ~15; };
     const int taps = a.taps;
     const uint32_t m_nk = udiv_magic(nk);
-    if (OT[LDSBWD_TANH] >= 0 && threadIdx.x == 0) row[OT[LDSBWD_TANH] - lo] = 0.f;   // (k_dsum adds it)
+    // split mode: CH = the data-gradient chain (+ LN gamma / beta rows), WG = the weight gradients; mode 1
+    // stores the gradients each weight gradient contracts with, mode 2 reads them back (a.gsave)
+    const bool CH = a.mode != 2, WG = a.mode != 1, store = a.mode == 1, load = a.mode == 2;
+    float* gs = a.gsave ? a.gsave + ((size_t)net * B + img) * a.gsave_img : nullptr;
+    if (CH && OT[LDSBWD_TANH] >= 0 && threadIdx.x == 0) row[OT[LDSBWD_TANH] - lo] = 0.f;   // (k_dsum adds it)
 
     // ---- conv_out: G = dL/d so (dc2 ch) -> GT; A = LN_out(y_R) -> AC; wgrad; dgrad -> GY
     {
@@ -625,25 +675,29 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         }
         const float* yR = sv + (size_t)R * HW * nk;
         const float mu = st[6 * R], rs = st[6 * R + 1];
-        stage_act(yR, nk, 0, nk, HW, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, ln ? P + OT[LDSBWD_LNO_B] : nullptr,
-                  ln, AC, SA);
-        build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
-        __syncthreads();
-        BSTAMP();
-        wgrad_any(AC, SA, 0, KT, taps, nk, 1, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo, row,
-                  WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CO_K], OT[LDSBWD_CO_B]);
-        __syncthreads();
-        BSTAMP();
-        stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, np16(nk), WL);
-        __syncthreads();
-        BSTAMP();
-        gemm_tap_any(GT, ST, 0, taps, a.dc2, 1, -1, WL, np16(nk), GY, SY, 0, nk, H, W, false, ZR);
-        __syncthreads();
-        BSTAMP();
-        // LN_out backward in place on GY
-        ln_bwd(yR, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, GY, SY, 0, GY, SY, 0, false, HW, nk, ln,
-               ln ? row + (OT[LDSBWD_LNO_G] - lo) : nullptr, ln ? row + (OT[LDSBWD_LNO_B] - lo) : nullptr, RED);
-        BSTAMP();
+        if (WG) {
+            stage_act(yR, nk, 0, nk, HW, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr,
+                      ln ? P + OT[LDSBWD_LNO_B] : nullptr, ln, AC, SA);
+            build_kt(KT, taps * nk, kp4(taps * nk), nk, taps, 1, 1);
+            __syncthreads();
+            BSTAMP();
+            wgrad_any(AC, SA, 0, KT, taps, nk, 1, GT, ST, 0, a.dc2, H, W, a.bw_map, OT[LDSBWD_CO_DW], OT[LDSBWD_CO_DB], lo,
+                      row, WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CO_K], OT[LDSBWD_CO_B]);
+            __syncthreads();
+            BSTAMP();
+        }
+        if (CH) {
+            stage_wt(BWI + OT[LDSBWD_CO_DW], taps, nk, a.dc2, np16(nk), WL);
+            __syncthreads();
+            BSTAMP();
+            gemm_tap_any(GT, ST, 0, taps, a.dc2, 1, -1, WL, np16(nk), GY, SY, 0, nk, H, W, false, ZR);
+            __syncthreads();
+            BSTAMP();
+            // LN_out backward in place on GY
+            ln_bwd(yR, mu, rs, ln ? P + OT[LDSBWD_LNO_G] : nullptr, GY, SY, 0, GY, SY, 0, false, HW, nk, ln,
+                   ln ? row + (OT[LDSBWD_LNO_G] - lo) : nullptr, ln ? row + (OT[LDSBWD_LNO_B] - lo) : nullptr, RED);
+            BSTAMP();
+        }
     }
     for (int r = R - 1; r >= 0; r--) {
         const int* o = rbo(r);
@@ -653,110 +707,145 @@ __global__ __launch_bounds__(BWT) void k_lds_bwd(LdsBwdArgs a) {
         const float mu1 = st[2 * r], rs1 = st[2 * r + 1];
         const float mu2 = st[2 * (R + r)], rs2 = st[2 * (R + r) + 1];
         const float mu3 = st[2 * (2 * R + r)], rs3 = st[2 * (2 * R + r) + 1];
+        float* gr = gs ? gs + (size_t)r * a.gs_rb : nullptr;
+        if (store) store_lds(gr, GY, SY, HW, nk);   // dL/dy_{r+1}: conv_b's weight gradient
+        if (load) {
+            load_lds(GY, SY, gr, HW, nk);
+            __syncthreads();
+        }
         // ---- conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r))): wgrad in channel chunks of the staged LN3(t2),
         // dgrad dL/d LN3-out -> GT
-        for (int c0 = 0; c0 < gc; c0 += a.ac_chunk) {
-            const int nc = gc - c0 < a.ac_chunk ? gc - c0 : a.ac_chunk;
-            stage_act(t2r, gc, c0, nc, HW, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, ln ? P + o[LDSBWD_LN3B] : nullptr,
-                      ln, AC, SA);
-            build_kt(KT, nc, kp4(nc), nc, 1, 1, 1);
+        if (WG)
+            for (int c0 = 0; c0 < gc; c0 += a.ac_chunk) {
+                const int nc = gc - c0 < a.ac_chunk ? gc - c0 : a.ac_chunk;
+                stage_act(t2r, gc, c0, nc, HW, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr,
+                          ln ? P + o[LDSBWD_LN3B] : nullptr, ln, AC, SA);
+                build_kt(KT, nc, kp4(nc), nc, 1, 1, 1);
+                __syncthreads();
+                BSTAMP();
+                // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
+                // gradient once, with the first chunk)
+                wgrad_any(AC, SA, 0, KT, 1, nc, 1, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
+                          c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ, ZQ + 4, true,
+                          o[LDSBWD_CB_K] + (int64_t)c0 * nk, o[LDSBWD_CB_B]);
+                __syncthreads();
+                BSTAMP();
+            }
+        if (CH) {
+            stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, np16(gc), WL);
             __syncthreads();
-        BSTAMP();
-            // rows c0.. of conv_b's dense [gc][nk] image: offset the dense base by c0 * nk (the bias
-            // gradient once, with the first chunk)
-            wgrad_any(AC, SA, 0, KT, 1, nc, 1, GY, SY, 0, nk, H, W, a.bw_map, o[LDSBWD_CB_DW] + (int64_t)c0 * nk,
-                      c0 == 0 ? (int64_t)o[LDSBWD_CB_DB] : -1, lo, row, WL, a.wmax, ZQ, ZQ + 4, true,
-                      o[LDSBWD_CB_K] + (int64_t)c0 * nk, o[LDSBWD_CB_B]);
+            BSTAMP();
+            gemm_tap_any(GY, SY, 0, 1, nk, 1, -1, WL, np16(gc), GT, ST, 0, gc, H, W, false, ZR);
             __syncthreads();
-        BSTAMP();
+            BSTAMP();
+            // ---- LN3 backward in place on GT -> dL/dt2
+            ln_bwd(t2r, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, GT, ST, 0, GT, ST, 0, false, HW, gc, ln,
+                   ln ? row + (o[LDSBWD_LN3G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN3B] - lo) : nullptr, RED);
+            BSTAMP();
         }
-        stage_wt(BWI + o[LDSBWD_CB_DW], 1, gc, nk, np16(gc), WL);
-        __syncthreads();
-        BSTAMP();
-        gemm_tap_any(GY, SY, 0, 1, nk, 1, -1, WL, np16(gc), GT, ST, 0, gc, H, W, false, ZR);
-        __syncthreads();
-        BSTAMP();
-        // ---- LN3 backward in place on GT -> dL/dt2
-        ln_bwd(t2r, mu3, rs3, ln ? P + o[LDSBWD_LN3G] : nullptr, GT, ST, 0, GT, ST, 0, false, HW, gc, ln,
-               ln ? row + (o[LDSBWD_LN3G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN3B] - lo) : nullptr, RED);
-        BSTAMP();
+        if (store) store_lds(gr + a.g_t3, GT, ST, HW, gc);   // dL/dt2: the branches' weight gradients
+        if (load) {
+            load_lds(GT, ST, gr + a.g_t3, HW, gc);
+            __syncthreads();
+        }
         // ---- grouped branches: every wgrad (A = LN2(t1) window -> AC), then every dgrad into AC (zeroed)
-        for (int bi = 0; bi < a.nbr; bi++) {
-            const int cin = a.br_cin[bi], cout = a.br_cout[bi];
-            stage_act(t1r, nk, a.br_cin_off[bi], cin, HW, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr,
-                      ln ? P + o[LDSBWD_LN2B] : nullptr, ln, AC, SA);
-            build_kt(KT, taps * cin, kp4(taps * cin), cin, taps, a.br_dil[bi], 1);
-            __syncthreads();
-        BSTAMP();
-            wgrad_any(AC, SA, 0, KT, taps, cin, a.br_dil[bi], GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
-                      o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row, WL, a.wmax, ZQ, ZQ + 4);
-            __syncthreads();
-        BSTAMP();
+        if (WG)
+            for (int bi = 0; bi < a.nbr; bi++) {
+                const int cin = a.br_cin[bi], cout = a.br_cout[bi];
+                stage_act(t1r, nk, a.br_cin_off[bi], cin, HW, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr,
+                          ln ? P + o[LDSBWD_LN2B] : nullptr, ln, AC, SA);
+                build_kt(KT, taps * cin, kp4(taps * cin), cin, taps, a.br_dil[bi], 1);
+                __syncthreads();
+                BSTAMP();
+                wgrad_any(AC, SA, 0, KT, taps, cin, a.br_dil[bi], GT, ST, a.br_out_off[bi], cout, H, W, a.bw_map,
+                          o[LDSBWD_BR + 2 * bi], o[LDSBWD_BR + 2 * bi + 1], lo, row, WL, a.wmax, ZQ, ZQ + 4);
+                __syncthreads();
+                BSTAMP();
+            }
+        if (CH) {
+            for (int e = threadIdx.x; e < HW * nk; e += BWT) {
+                const int p = udiv(e, m_nk), c = e - p * nk;
+                AC[p * SA + c] = 0.f;
+            }
+            for (int bi = 0; bi < a.nbr; bi++) {
+                const int cin = a.br_cin[bi], cout = a.br_cout[bi];
+                stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, np16(cin), WL);
+                __syncthreads();
+                BSTAMP();
+                gemm_tap_any(GT, ST, a.br_out_off[bi], taps, cout, a.br_dil[bi], -1, WL, np16(cin), AC, SA, a.br_cin_off[bi],
+                             cin, H, W, true, ZR);
+                __syncthreads();
+                BSTAMP();
+            }
+            // ---- LN2 backward: AC (dL/d LN2-out, zero outside the windows) -> dL/dt1 in GT
+            ln_bwd(t1r, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr, AC, SA, 0, GT, ST, 0, false, HW, nk, ln,
+                   ln ? row + (o[LDSBWD_LN2G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN2B] - lo) : nullptr, RED);
+            BSTAMP();
         }
-        for (int e = threadIdx.x; e < HW * nk; e += BWT) {
-            const int p = udiv(e, m_nk), c = e - p * nk;
-            AC[p * SA + c] = 0.f;
-        }
-        for (int bi = 0; bi < a.nbr; bi++) {
-            const int cin = a.br_cin[bi], cout = a.br_cout[bi];
-            stage_wt(BWI + o[LDSBWD_BR + 2 * bi], taps, cin, cout, np16(cin), WL);
+        if (store) store_lds(gr + a.g_t2, GT, ST, HW, nk);   // dL/dt1: conv_a's weight gradient
+        if (load) {
+            load_lds(GT, ST, gr + a.g_t2, HW, nk);
             __syncthreads();
-        BSTAMP();
-            gemm_tap_any(GT, ST, a.br_out_off[bi], taps, cout, a.br_dil[bi], -1, WL, np16(cin), AC, SA, a.br_cin_off[bi], cin,
-                         H, W, true, ZR);
-            __syncthreads();
-        BSTAMP();
         }
-        // ---- LN2 backward: AC (dL/d LN2-out, zero outside the windows) -> dL/dt1 in GT
-        ln_bwd(t1r, mu2, rs2, ln ? P + o[LDSBWD_LN2G] : nullptr, AC, SA, 0, GT, ST, 0, false, HW, nk, ln,
-               ln ? row + (o[LDSBWD_LN2G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN2B] - lo) : nullptr, RED);
-        BSTAMP();
         // ---- conv_a: A = LN1(y_r) -> AC; wgrad with GT; dgrad -> AC
-        stage_act(yr, nk, 0, nk, HW, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, ln ? P + o[LDSBWD_LN1B] : nullptr, ln,
-                  AC, SA);
-        build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
-        __syncthreads();
-        BSTAMP();
-        wgrad_any(AC, SA, 0, KT, 1, nk, 1, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row, WL,
-                  a.wmax, ZQ, ZQ + 4, true, o[LDSBWD_CA_K], o[LDSBWD_CA_B]);
-        __syncthreads();
-        BSTAMP();
-        stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, np16(nk), WL);
-        __syncthreads();
-        BSTAMP();
-        gemm_tap_any(GT, ST, 0, 1, nk, 1, -1, WL, np16(nk), AC, SA, 0, nk, H, W, false, ZR);
-        __syncthreads();
-        BSTAMP();
-        // ---- LN1 backward: GY += dL/dy_r through conv_a (the identity path keeps GY)
-        ln_bwd(yr, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, AC, SA, 0, GY, SY, 0, true, HW, nk, ln,
-               ln ? row + (o[LDSBWD_LN1G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN1B] - lo) : nullptr, RED);
-        BSTAMP();
+        if (WG) {
+            stage_act(yr, nk, 0, nk, HW, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, ln ? P + o[LDSBWD_LN1B] : nullptr,
+                      ln, AC, SA);
+            build_kt(KT, nk, kp4(nk), nk, 1, 1, 1);
+            __syncthreads();
+            BSTAMP();
+            wgrad_any(AC, SA, 0, KT, 1, nk, 1, GT, ST, 0, nk, H, W, a.bw_map, o[LDSBWD_CA_DW], o[LDSBWD_CA_DB], lo, row,
+                      WL, a.wmax, ZQ, ZQ + 4, true, o[LDSBWD_CA_K], o[LDSBWD_CA_B]);
+            __syncthreads();
+            BSTAMP();
+        }
+        if (CH) {
+            stage_wt(BWI + o[LDSBWD_CA_DW], 1, nk, nk, np16(nk), WL);
+            __syncthreads();
+            BSTAMP();
+            gemm_tap_any(GT, ST, 0, 1, nk, 1, -1, WL, np16(nk), AC, SA, 0, nk, H, W, false, ZR);
+            __syncthreads();
+            BSTAMP();
+            // ---- LN1 backward: GY += dL/dy_r through conv_a (the identity path keeps GY)
+            ln_bwd(yr, mu1, rs1, ln ? P + o[LDSBWD_LN1G] : nullptr, AC, SA, 0, GY, SY, 0, true, HW, nk, ln,
+                   ln ? row + (o[LDSBWD_LN1G] - lo) : nullptr, ln ? row + (o[LDSBWD_LN1B] - lo) : nullptr, RED);
+            BSTAMP();
+        }
     }
     // ---- conv_in: A = u1c (gathered from the layer input) -> AC; wgrad with GY; dgrad -> GT -> du1c
     {
-        const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
-        const uint32_t m_d1 = udiv_magic(a.dc1);
-        for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
-            const int p = udiv(e, m_d1), c = e - p * a.dc1;
-            AC[p * SA + c] = ub[mask_pos_b(a.mask, p, c, W, a.W, a.D)];
+        if (store) store_lds(gs + a.g_in, GY, SY, HW, nk);   // dL/dy_0: conv_in's weight gradient
+        if (load) {
+            load_lds(GY, SY, gs + a.g_in, HW, nk);
+            __syncthreads();
         }
-        build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
-        __syncthreads();
-        BSTAMP();
-        wgrad_any(AC, SA, 0, KT, taps, a.dc1, 1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo, row,
-                  WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CI_K], OT[LDSBWD_CI_B]);
-        __syncthreads();
-        BSTAMP();
-        stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, np16(a.dc1), WL);
-        __syncthreads();
-        BSTAMP();
-        gemm_tap_any(GY, SY, 0, taps, nk, 1, -1, WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false, ZR);
-        __syncthreads();
-        BSTAMP();
-        float* du = a.du1c[net] + (size_t)img * HW * a.dc1;
-        for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
-            const int p = udiv(e, m_d1), c = e - p * a.dc1;
-            du[e] = GT[p * ST + c];
+        const uint32_t m_d1 = udiv_magic(a.dc1);
+        if (WG) {
+            const float* ub = a.u + (size_t)img * a.H * a.W * a.D;
+            for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
+                const int p = udiv(e, m_d1), c = e - p * a.dc1;
+                AC[p * SA + c] = ub[mask_pos_b(a.mask, p, c, W, a.W, a.D)];
+            }
+            build_kt(KT, taps * a.dc1, kp4(taps * a.dc1), a.dc1, taps, 1, 1);
+            __syncthreads();
+            BSTAMP();
+            wgrad_any(AC, SA, 0, KT, taps, a.dc1, 1, GY, SY, 0, nk, H, W, a.bw_map, OT[LDSBWD_CI_DW], OT[LDSBWD_CI_DB], lo,
+                      row, WL, a.wmax, ZQ, ZQ + 4, true, OT[LDSBWD_CI_K], OT[LDSBWD_CI_B]);
+            __syncthreads();
+            BSTAMP();
+        }
+        if (CH) {
+            stage_wt(BWI + OT[LDSBWD_CI_DW], taps, a.dc1, nk, np16(a.dc1), WL);
+            __syncthreads();
+            BSTAMP();
+            gemm_tap_any(GY, SY, 0, taps, nk, 1, -1, WL, np16(a.dc1), GT, ST, 0, a.dc1, H, W, false, ZR);
+            __syncthreads();
+            BSTAMP();
+            float* du = a.du1c[net] + (size_t)img * HW * a.dc1;
+            for (int e = threadIdx.x; e < HW * a.dc1; e += BWT) {
+                const int p = udiv(e, m_d1), c = e - p * a.dc1;
+                du[e] = GT[p * ST + c];
+            }
         }
     }
     BSTAMP();

@@ -207,6 +207,12 @@ struct TrainLayout {
     std::vector<size_t> act_save, so_save;
     size_t rows = 0;
     int row_max = 0;
+    // split LDS backward (chain and weight gradients as two launches, CNF_LDS_SPLIT): per parity of the LDS
+    // layer count a second row set (rows2), the stored chain gradients [2][B][gsave_max] and the coupling
+    // gradients dL/d(so) [net]: layer k's weight gradients run behind layer k+1's chain, so their buffers
+    // alternate
+    size_t rows2 = 0, gsave[2] = {}, dso_l[2][2] = {};
+    int gsave_max = 0;
     // streamed layers: the training forward saves the activations the backward would otherwise recompute
     // (when they fit the budget): per net y [R+1][B][HW][nk], full t1 [R][B][HW][nk], t2 [R][B][HW][gc],
     // LN statistics [3R+1][B][2] (y_r: r, t1_r: R+1+r, t2_r: 2R+1+r) and the raw conv_out [2][B][HW][dc2]

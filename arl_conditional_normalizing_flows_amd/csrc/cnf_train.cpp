@@ -41,6 +41,11 @@ struct LnIn {
     int act = 0;
 };
 
+bool fused_lnr() {   // A/B knob: the LN backward's reduction in the producing data-gradient kernel (per call)
+    const char* e = std::getenv("CNF_LNR_FUSE");
+    return !(e && std::atoi(e) == 0);
+}
+
 int wgrad_chunks(int B, int npx) {
     const long long total = (long long)B * npx;
     return (int)std::max<long long>(1, std::min<long long>(64, (total + 511) / 512));
@@ -131,6 +136,11 @@ size_t ldsbwd_setup(const Plan& p, const Coupling& c, LdsBwdArgs& a) {
     a.save_t2 = s.t2;
     a.save_st = s.st;
     a.row = (int)std::max(c.net[0].hi - c.net[0].lo, c.net[1].hi - c.net[1].lo);
+    a.gs_rb = HW * (2 * c.nk + c.gc);
+    a.g_t3 = HW * c.nk;
+    a.g_t2 = HW * (c.nk + c.gc);
+    a.g_in = c.R * a.gs_rb;
+    a.gsave_img = (a.g_in + HW * c.nk + 3) / 4 * 4;
     return off;
 }
 
@@ -187,7 +197,7 @@ TrainLayout Plan::train_layout(int B) const {
     for (int k = 0; k < 2; k++) T.duv[k] = take(Bz * L.n_uv * 4);
     T.dzy = take(Bz * L.n_uv * 4);
     for (int n = 0; n < 2; n++) {
-        T.lnsum[n] = take(Bz * LNB_RS * 2 * 8);
+        T.lnsum[n] = take(Bz * std::max(LNB_RS, LNR_MAXPARTS) * 2 * 8);
         // LN backward: per batch slice partial gamma / beta gradients [2][LNB_SLICES][n]
         T.lnpart[n] = take((size_t)2 * LNB_SLICES * std::max(m_nk, m_gc) * 4);
     }
@@ -213,7 +223,19 @@ TrainLayout Plan::train_layout(int B) const {
         T.so_save[c.index] = take(2 * Bz * HW * c.dc2 * 4);
         T.row_max = std::max<int>(T.row_max, (int)std::max(c.net[0].hi - c.net[0].lo, c.net[1].hi - c.net[1].lo));
     }
-    if (T.row_max > 0) T.rows = take(2 * Bz * T.row_max * 4);
+    if (T.row_max > 0) {
+        T.rows = take(2 * Bz * T.row_max * 4);
+        T.rows2 = take(2 * Bz * T.row_max * 4);
+        for (const Coupling& c : couplings) {
+            if (!c.lds_bwd) continue;
+            const int HW = c.hc * c.wc;
+            T.gsave_max = std::max(T.gsave_max, ((c.R * (2 * c.nk + c.gc) + c.nk) * HW + 3) / 4 * 4);
+        }
+        for (int par = 0; par < 2; par++) {
+            T.gsave[par] = take(2 * Bz * T.gsave_max * 4);
+            for (int n = 0; n < 2; n++) T.dso_l[par][n] = take(Bz * m_so * 4);
+        }
+    }
     // streamed layers' saved activations, when all of them fit 16 GiB (CNF_TRAIN_SAVE=0: recompute)
     T.ssave.assign(couplings.size(), TrainLayout::StreamSave{});
     T.has_ssave.assign(couplings.size(), 0);
@@ -302,9 +324,23 @@ void conv_fwd(TExec& E, int h, int w, const float* in, int in_cs, int in_off, in
 }
 
 // dx (=|+=) conv^T(dy): dy has cout channels at (dy_cs, dy_off), dx gets cin channels at (dx_cs, dx_off)
-void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int cin,
-                int dil, float* dx, int dx_cs, int dx_off, int accumulate) {
+// With lr (an LN whose input has dx's layout and whose output gradient dx is), the kernel also writes the
+// LN backward's per-image reduction partials to the net's lnsum; returns their count per image (0: not
+// fused — ln_bwd runs k_lnb_reduce)
+struct LnRed {
+    const float* x = nullptr;
+    const float* gamma = nullptr;
+    const float* stats = nullptr;
+};
+int conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int cin,
+               int dil, float* dx, int dx_cs, int dx_off, int accumulate, const LnRed* lr = nullptr) {
     TConvArgs a{};
+    if (lr != nullptr && lr->stats != nullptr && fused_lnr()) {
+        a.lnr_x = lr->x;
+        a.lnr_gamma = lr->gamma;
+        a.lnr_stats = lr->stats;
+        a.lnr_part = E.at<double>(E.T.lnsum[E.net]);
+    }
     a.in = dy;
     a.in_cs = dy_cs;
     a.in_off = dy_off;
@@ -325,7 +361,7 @@ void conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, 
     a.sgn = -1;
     a.B = E.B;
     a.zero = E.at<float>(E.T.zeros);
-    launch_tconv(a, E.st);
+    return launch_tconv(a, E.st);
 }
 
 // dW, db of a conv: X (cin channels at x_cs/x_off, LN-on-load) and dY (cout at dy_cs/dy_off)
@@ -421,10 +457,10 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
 }
 
 void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
-            int64_t g_off, int64_t b_off) {
+            int64_t g_off, int64_t b_off, int presum = 0) {
     launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum[E.net]), n, E.B, 1, dx, accumulate,
                        ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr,
-                       E.at<float>(E.T.lnpart[E.net]), E.st);
+                       E.at<float>(E.T.lnpart[E.net]), E.st, presum);
 }
 
 // the plan's side stream and fork / join events (created on first use on the current device)
@@ -462,11 +498,20 @@ void stream_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
 // small, latency-bound launches of the two chains overlap.
 // the fused backward of a k_net_lds layer (cnf_ldsbwd.hip) from the activations the training forward
 // saved: coupling law backward, one k_lds_bwd launch for both nets, the batch sum of the gradient rows
-void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
+// the fused backward of a k_net_lds layer (cnf_ldsbwd.hip) from the activations the training forward
+// saved: coupling law backward, k_lds_bwd for both nets, the batch sum of the gradient rows. Split
+// (par >= 0): the data-gradient chain (k_lds_bwd mode 1, storing the gradients the weight gradients
+// need) on the caller's stream, then the weight gradients (mode 2) and the row sum on the side stream
+// wside[1] behind an event, so they run on the CUs the next layer's chain leaves idle (one workgroup per
+// (image, net) fills half the GPU at B = 64); returns the event of the row sum (the layer's parameter
+// gradients complete), null unsplit. par selects the alternating buffer set.
+hipEvent_t coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const float* dv, float* du, int par) {
     const int B = E.B;
     const float* P = E.params;
+    const bool split = par >= 0;
     const float* so0 = E.at<float>(E.T.so_save[c.index]);
-    const size_t so_n = (size_t)B * c.hc * c.wc * c.dc2;
+    float* dso0 = E.at<float>(split ? E.T.dso_l[par][0] : E.T.dso[0]);
+    float* dso1 = E.at<float>(split ? E.T.dso_l[par][1] : E.T.dso[1]);
     {
         CoupBwArgs a{};
         a.u = u;
@@ -474,8 +519,8 @@ void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const fl
         a.s_pre = so0;
         a.tanh_w = P + c.net[0].tanh_w;
         a.du = du;
-        a.ds_pre = E.at<float>(E.T.dso[0]);
-        a.dt = E.at<float>(E.T.dso[1]);
+        a.ds_pre = dso0;
+        a.dt = dso1;
         a.dw_part = E.at<double>(E.T.dwpart);
         a.g_ld = -E.inv_batch_;
         a.count = E.count;
@@ -492,12 +537,11 @@ void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const fl
         launch_coupling_backward(a, B, np, E.st);
         launch_dsum(a.dw_part, (long long)B * np, E.dparams + c.net[0].tanh_w, E.st);
     }
-    (void)so_n;
     LdsBwdArgs a;
     if (ldsbwd_setup(E.p, c, a) == 0) throw std::logic_error("fused LDS backward planned for a layer it does not fit");
     a.save = E.at<float>(E.T.act_save[c.index]);
-    a.dso[0] = E.at<float>(E.T.dso[0]);
-    a.dso[1] = E.at<float>(E.T.dso[1]);
+    a.dso[0] = dso0;
+    a.dso[1] = dso1;
     a.u = u;
     a.du1c[0] = E.at<float>(E.T.du1c[0]);
     a.du1c[1] = E.at<float>(E.T.du1c[1]);
@@ -505,19 +549,38 @@ void coupling_backward_lds(TExec& E, const Coupling& c, const float* u, const fl
     a.bw = E.bw();
     a.bw_map = E.p.dev_bw_map;
     a.offs = E.p.dev_table + c.dev_bwd_offs;
-    a.part = E.at<float>(E.T.rows);
+    a.part = E.at<float>(split && par == 1 ? E.T.rows2 : E.T.rows);
     a.row = E.T.row_max;
     static const bool stamps = [] {   // diagnostics
         const char* e = std::getenv("CNF_LDSBWD_STAMPS");
         return e && std::atoi(e) != 0;
     }();
     a.stamps = stamps ? 1 : 0;
-    launch_lds_bwd(a, B, E.st);
     const NetParams& n0 = c.net[0];
     const NetParams& n1 = c.net[1];
-    launch_grad_rows(a.part, B, a.row, n0.lo, n1.lo, (int)(n0.hi - n0.lo), (int)(n1.hi - n1.lo), E.dparams, E.st);
+    if (!split) {
+        a.mode = 0;
+        launch_lds_bwd(a, B, E.st);
+        launch_grad_rows(a.part, B, a.row, n0.lo, n1.lo, (int)(n0.hi - n0.lo), (int)(n1.hi - n1.lo), E.dparams, E.st);
+        launch_scatter_add_u1c(a.du1c[0], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
+        launch_scatter_add_u1c(a.du1c[1], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
+        return nullptr;
+    }
+    ensure_side(E.p);
+    a.gsave = E.at<float>(E.T.gsave[par]);
+    a.mode = 1;
+    launch_lds_bwd(a, B, E.st);
     launch_scatter_add_u1c(a.du1c[0], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
     launch_scatter_add_u1c(a.du1c[1], du, B, c.H, c.W, c.D, c.mask, c.hc, c.wc, c.dc1, E.st);
+    hipStream_t ws = E.p.wside[1];
+    stream_wait(E.st, ws, tevent(E.p));   // the chain's stored gradients and LN rows
+    a.mode = 2;
+    a.stamps = 0;
+    launch_lds_bwd(a, B, ws);
+    launch_grad_rows(a.part, B, a.row, n0.lo, n1.lo, (int)(n0.hi - n0.lo), (int)(n1.hi - n1.lo), E.dparams, ws);
+    hipEvent_t done = tevent(E.p);
+    hchk(hipEventRecord(done, ws), "hipEventRecord");
+    return done;
 }
 
 void coupling_backward(TExec& E, const Coupling& c, const float* u, const float* dv, float* du) {
@@ -638,8 +701,9 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
             const float* dso = E.at<float>(E.T.dso[n]);
             const LnIn lo = lnin(n, R, np.ln_out_g, np.ln_out_b);
             conv_wgrad(En, h, w, Y(n, R), nk, 0, nk, lo, dso, c.dc2, 0, c.dc2, np.co, 1);
-            conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0);
-            ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b);
+            const LnRed ro{Y(n, R), lo.gamma, lo.stats};
+            const int ps = conv_dgrad(En, h, w, dso, c.dc2, 0, c.dc2, np.co, nk, 1, dln, nk, 0, 0, &ro);
+            ln_bwd(En, Y(n, R), dln, lo, npx * nk, dy, 0, np.ln_out_g, np.ln_out_b, ps);
             return;
         }
         if (k == 1 + 3 * R) {
@@ -654,26 +718,37 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         if (part == 0) {   // conv_b (y_{r+1} = y_r + conv_b(LN3(t2_r)))
             const LnIn l3 = lnin(n, 2 * R + 1 + r, rb.ln3g, rb.ln3b);
             ev_cb[n] = conv_wgrad(En, h, w, T2(n, r), gc, 0, gc, l3, dy, nk, 0, nk, rb.cb, 1);
-            conv_dgrad(En, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0);
+            const LnRed r3{T2(n, r), l3.gamma, l3.stats};
+            const int ps = conv_dgrad(En, h, w, dy, nk, 0, nk, rb.cb, gc, 1, dcb, gc, 0, 0, &r3);
             chain_wait(En, ev_gc[n]);
-            ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b);
+            ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b, ps);
         } else if (part == 1) {   // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
             hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
+            // the LN2 reduction rides on the last branch's data gradient when every branch writes the same
+            // window (the reference group mode): only then does that launch see the final dbuf everywhere it
+            // is non-zero
+            bool one_window = true;
+            for (const Branch& b : c.br) one_window = one_window && b.cin_off == c.br[0].cin_off && b.cin == c.br[0].cin;
+            const LnRed r2{T1(n, r), l2.gamma, l2.stats};
+            int ps = 0;
             for (size_t bi = 0; bi < c.br.size(); bi++) {
                 const Branch& b = c.br[bi];
                 ev_gc[n] = conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout,
                                       rb.gc[bi], b.dil);
-                conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1);
+                const bool last = bi + 1 == c.br.size();
+                ps = conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1,
+                                last && one_window ? &r2 : nullptr);
             }
             chain_wait(En, ev_ca[n]);
-            ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b);
+            ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b, ps);
         } else {   // conv_a
             const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
             ev_ca[n] = conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);
-            conv_dgrad(En, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0);
+            const LnRed r1{Y(n, r), l1.gamma, l1.stats};
+            const int ps = conv_dgrad(En, h, w, dt1, nk, 0, nk, rb.ca, nk, 1, dln, nk, 0, 0, &r1);
             chain_wait(En, ev_cb[n]);
-            ln_bwd(En, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b);
+            ln_bwd(En, Y(n, r), dln, l1, npx * nk, dy, 1, rb.ln1g, rb.ln1b, ps);
         }
     };
     const int nphase = 2 + 3 * R;
@@ -718,18 +793,43 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     float* cur = buf[which];
     which ^= 1;
     int bi = (int)p.boundaries.size() - 1;
+    // split LDS layers: their weight gradients finish behind the next layers on a side stream; a layer's
+    // buffer set (parity of its LDS-layer count) is reused two LDS layers later, when the caller's stream
+    // first waits for them — that is also when the layer's gradients are complete for `done`
+    const bool split = [] {   // (read per call: tests switch it)
+        const char* e = std::getenv("CNF_LDS_SPLIT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    struct Pending {
+        int ci = -1;
+        hipEvent_t ev = nullptr;
+    } pend[2];
+    auto flush = [&](int par) {
+        if (pend[par].ci < 0) return;
+        hchk(hipStreamWaitEvent(st, pend[par].ev, 0), "hipStreamWaitEvent");
+        if (done != nullptr) done(user, pend[par].ci);
+        pend[par].ci = -1;
+    };
+    int lds_k = 0;
     for (int li = (int)p.layers.size() - 1; li >= 0; li--) {
         const Layer& ly = p.layers[li];
         if (ly.kind == CNF_LAYER_COUPLING) {
             const Coupling& c = p.couplings[ly.ci];
             float* nxt = buf[which];
-            if (c.lds_bwd)
-                coupling_backward_lds(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
-            else
-                coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
-            // every launch writing this layer's parameter gradients is ordered before anything enqueued
-            // on st from here (its side streams joined st): the caller may reduce them now
-            if (done != nullptr) done(user, c.index);
+            if (c.lds_bwd && split) {
+                const int par = lds_k++ & 1;
+                flush(par);
+                pend[par].ev = coupling_backward_lds(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt, par);
+                pend[par].ci = c.index;
+            } else {
+                if (c.lds_bwd)
+                    coupling_backward_lds(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt, -1);
+                else
+                    coupling_backward(E, c, E.at<float>(E.T.save_u[c.index]), cur, nxt);
+                // every launch writing this layer's parameter gradients is ordered before anything enqueued
+                // on st from here (its side streams joined st): the caller may reduce them now
+                if (done != nullptr) done(user, c.index);
+            }
             cur = nxt;
             which ^= 1;
         } else if (ly.kind == CNF_LAYER_FACTOR) {
@@ -741,6 +841,10 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
             which ^= 1;
         }
     }
+    // the last split layers (the older first)
+    const int last = lds_k & 1;
+    flush(last);
+    flush(last ^ 1);
     hchk(hipGetLastError(), "training kernel launch");
 }
 

@@ -133,6 +133,38 @@ __global__ __launch_bounds__(256) void k_tconv(TConvArgs a) {
 // its (shifted) pixel, loaded straight from global with LN + LeakyReLU applied in registers. The
 // K order inside a group is permuted identically on both operands, so the sum is the conv's.
 // ------------------------------------------------------------------------------------------------
+// fused LN-backward reduction (TConvArgs::lnr_part): the workgroup's (sum g, sum g * xhat), fixed order
+__device__ __forceinline__ void lnr_finish(const TConvArgs& a, double sg, double sgh, int b) {
+    __shared__ double lred[8];
+    sg = wave_sum(sg);
+    sgh = wave_sum(sgh);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();   // (the kernel's LDS reads are done; lred is static, disjoint anyway)
+    if (lane == 0) {
+        lred[2 * wave] = sg;
+        lred[2 * wave + 1] = sgh;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int w = 0; w < 4; w++) {
+            s0 += lred[2 * w];
+            s1 += lred[2 * w + 1];
+        }
+        const int tile = blockIdx.x + gridDim.x * blockIdx.z, np = gridDim.x * gridDim.z;
+        a.lnr_part[2 * ((size_t)b * np + tile)] = s0;
+        a.lnr_part[2 * ((size_t)b * np + tile) + 1] = s1;
+    }
+}
+// one output element's share: g = v * gamma, xhat of the raw LN input at the same element
+__device__ __forceinline__ void lnr_add(const TConvArgs& a, size_t oi, size_t gi, float v, float mu, float rs,
+                                        double& sg, double& sgh) {
+    const float g = v * a.lnr_gamma[gi];
+    const float xh = (lrelu(a.lnr_x[oi]) - mu) * rs;
+    sg += g;
+    sgh += (double)g * xh;
+}
+
 #ifndef CNF_TW_U
 #define CNF_TW_U 8
 #endif
@@ -248,6 +280,9 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
         }
     }
     // acc[m][rr] = out[pixel p0 + 16 wave + 4 kq + rr][channel n0 + 16 m + i16]
+    const bool lnr = a.lnr_part != nullptr;
+    const float lmu = lnr ? a.lnr_stats[2 * b] : 0.f, lrs = lnr ? a.lnr_stats[2 * b + 1] : 0.f;
+    double sg = 0.0, sgh = 0.0;
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
         const int p = p0 + wave * 16 + 4 * kq + rr;
@@ -262,8 +297,10 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
             if (a.res) v += a.res[ob + n];
             if (a.accumulate) v += a.out[ob + n];
             a.out[ob + n] = v;
+            if (lnr) lnr_add(a, ob + n, (size_t)p * a.out_cs + a.out_off + n, v, lmu, lrs, sg, sgh);
         }
     }
+    if (lnr) lnr_finish(a, sg, sgh, b);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -431,6 +468,9 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
         }
     }
     // acc[s][m][rr] = out[tile pixel (wave + 4s) * 16 + 4 kq + rr][channel n0 + 16 m + i16]
+    const bool lnr = a.lnr_part != nullptr;
+    const float lmu = lnr ? a.lnr_stats[2 * b] : 0.f, lrs = lnr ? a.lnr_stats[2 * b + 1] : 0.f;
+    double sg = 0.0, sgh = 0.0;
 #pragma unroll
     for (int s = 0; s < SUB; s++)
 #pragma unroll
@@ -438,7 +478,8 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
             const int q = (wave + 4 * s) * 16 + 4 * kq + rr;
             const int orow = r0 + q / W, ocol = q % W;
             if (q >= TH * W || orow >= H) continue;
-            const size_t ob = ((size_t)b * npx + (size_t)orow * W + ocol) * a.out_cs + a.out_off;
+            const size_t pix = (size_t)orow * W + ocol;
+            const size_t ob = ((size_t)b * npx + pix) * a.out_cs + a.out_off;
 #pragma unroll
             for (int m = 0; m < NR; m++) {
                 const int n = n0 + 16 * m + i16;
@@ -448,8 +489,10 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 if (a.res) v += a.res[ob + n];
                 if (a.accumulate) v += a.out[ob + n];
                 a.out[ob + n] = v;
+                if (lnr) lnr_add(a, ob + n, pix * a.out_cs + a.out_off + n, v, lmu, lrs, sg, sgh);
             }
         }
+    if (lnr) lnr_finish(a, sg, sgh, b);
 }
 
 static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (read per call: tests switch it)
@@ -458,8 +501,14 @@ static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (rea
 }
 bool train_valu_kernels() { return train_valu(); }
 
-void launch_tconv(const TConvArgs& a, hipStream_t st) {
+int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
+    TConvArgs a = a_in;
     const int npx = a.H * a.W;
+    // a fused LN reduction writes one partial per workgroup of an image: drop it where there are too many
+    auto lnr_ok = [&](const dim3& g) {
+        if (a.lnr_part != nullptr && (int)(g.x * g.z) > LNR_MAXPARTS) a.lnr_part = nullptr;
+        return a.lnr_part != nullptr ? (int)(g.x * g.z) : 0;
+    };
     static const bool band_off = [] {   // A/B knob: no band-staged 3x3 kernel
         const char* e = std::getenv("CNF_TCONV_BAND");
         return e && std::atoi(e) == 0;
@@ -486,6 +535,7 @@ void launch_tconv(const TConvArgs& a, hipStream_t st) {
         const size_t lds = band + (all_taps ? 9 : 1) * w1;
         if (lds <= 160 * 1024) {
             const dim3 g((a.H + TH - 1) / TH, a.B, (a.N + NS - 1) / NS), blk(256);
+            const int np = lnr_ok(g);
             if (sub == 4)
                 hipLaunchKernelGGL((k_tconv_band<1, 4>), g, blk, lds, st, a, TH, all_taps);
             else if (sub == 2 && nr == 1)
@@ -500,7 +550,7 @@ void launch_tconv(const TConvArgs& a, hipStream_t st) {
                 hipLaunchKernelGGL((k_tconv_band<3, 1>), g, blk, lds, st, a, TH, all_taps);
             else
                 hipLaunchKernelGGL((k_tconv_band<4, 1>), g, blk, lds, st, a, TH, all_taps);
-            return;
+            return np;
         }
     }
     if (!train_valu()) {
@@ -514,13 +564,14 @@ void launch_tconv(const TConvArgs& a, hipStream_t st) {
             const size_t lds = all_taps ? lds1 * a.taps : lds1;
             const bool vec = a.K % 4 == 0 && a.in_cs % 4 == 0 && a.in_off % 4 == 0;
             const dim3 g((npx + 63) / 64, a.B, (a.N + NS - 1) / NS), blk(256);
+            const int np = lnr_ok(g);
 #define CNF_TM(NR_)                                                                                   \
     if (nr == NR_) {                                                                                  \
         if (vec)                                                                                      \
             hipLaunchKernelGGL((k_tconv_mfma<NR_, true>), g, blk, lds, st, a, all_taps);            \
         else                                                                                          \
             hipLaunchKernelGGL((k_tconv_mfma<NR_, false>), g, blk, lds, st, a, all_taps);           \
-        return;                                                                                       \
+        return np;                                                                                    \
     }
             CNF_TM(1) CNF_TM(2) CNF_TM(3) CNF_TM(4)
 #undef CNF_TM
@@ -535,6 +586,7 @@ void launch_tconv(const TConvArgs& a, hipStream_t st) {
         hipLaunchKernelGGL(k_tconv<16>, g, blk, 0, st, a);
     else
         hipLaunchKernelGGL(k_tconv<64>, g, blk, 0, st, a);
+    return 0;   // (the VALU kernel has no fused LN reduction)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1379,14 +1431,17 @@ __global__ __launch_bounds__(256) void k_lnb_gsum(const float* __restrict__ gpar
 
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st) {
+                        float* scratch, hipStream_t st, int presum) {
     // slices per image: at least two full passes of the workgroup each (64 images x 8 slices fill the
     // GPU where one workgroup per image used a quarter of it)
 #ifndef CNF_LNB_RS
 #define CNF_LNB_RS LNB_RS
 #endif
-    const int rsl = (int)std::min<long long>(CNF_LNB_RS, std::max<long long>(1, (n / 4) / (2LL * LNT)));
-    if (stats) hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
+    int rsl = (int)std::min<long long>(CNF_LNB_RS, std::max<long long>(1, (n / 4) / (2LL * LNT)));
+    if (presum > 0)
+        rsl = presum;
+    else if (stats)
+        hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
     const int S = B < LNB_SLICES ? B : LNB_SLICES;
     float* gpart = scratch;
     float* bpart = scratch + (size_t)LNB_SLICES * n;

@@ -186,7 +186,10 @@ int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, cons
  *    `stream` (the backward's side streams have joined it). Work the callback
  *    enqueues behind that point on `stream` (or on a stream waiting for it), e.g.
  *    cnf_allreduce_sum_f32 of that range, overlaps the backward of the layers
- *    before it. Layers complete in reverse index order. */
+ *    before it. Every coupling layer is reported exactly once, in an order that is
+ *    the same on every rank: reverse index order, except that a layer whose
+ *    weight gradients run on a side stream (the split LDS-layer backward) is
+ *    reported when the stream first waits for them, two such layers later. */
 typedef void (*cnf_layer_done_fn)(void* user, int coupling_index);
 int cnf_flow_backward_ex(cnf_plan* plan, const float* params, const float* xy, const float* zy,
                          void* train_workspace, int B, const float* global_count, float* dparams,

@@ -154,6 +154,12 @@ GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'in
               # the LDS-staged band weight gradients (k_wgrad_band) instead of the register-operand
               # k_wgrad_direct (CNF_WGRAD_DIRECT=0, read per call)
               ('cfg2', 2, {'_env': {'CNF_WGRAD_DIRECT': '0'}}),
+              # the LDS layers' backward as one launch per layer (CNF_LDS_SPLIT=0) instead of the data-gradient
+              # chain and the weight gradients as two launches on two streams (read per call)
+              ('cfg2', 2, {'_env': {'CNF_LDS_SPLIT': '0'}}), ('small', 3, {'_env': {'CNF_LDS_SPLIT': '0'}}),
+              # the streamed layers' LN-backward reduction as its own kernel (k_lnb_reduce) instead of fused
+              # into the producing data-gradient kernel (CNF_LNR_FUSE=0, read per call)
+              ('cfg2', 2, {'_env': {'CNF_LNR_FUSE': '0'}}),
               # the benched training batch (bench.py --mode train): the batch-sliced LN backward (up to 8
               # workgroups per image), the multi-unit band weight gradients and the four-stream schedule
               # all see their full-size partitions only here
