@@ -156,15 +156,6 @@ __device__ __forceinline__ void lnr_finish(const TConvArgs& a, double sg, double
         a.lnr_part[2 * ((size_t)b * np + tile) + 1] = s1;
     }
 }
-// one output element's share: g = v * gamma, xhat of the raw LN input at the same element
-__device__ __forceinline__ void lnr_add(const TConvArgs& a, size_t oi, size_t gi, float v, float mu, float rs,
-                                        double& sg, double& sgh) {
-    const float g = v * a.lnr_gamma[gi];
-    const float xh = (lrelu(a.lnr_x[oi]) - mu) * rs;
-    sg += g;
-    sgh += (double)g * xh;
-}
-
 #ifndef CNF_TW_U
 #define CNF_TW_U 8
 #endif
@@ -283,6 +274,20 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     const bool lnr = a.lnr_part != nullptr;
     const float lmu = lnr ? a.lnr_stats[2 * b] : 0.f, lrs = lnr ? a.lnr_stats[2 * b + 1] : 0.f;
     double sg = 0.0, sgh = 0.0;
+    // the LN reduction's operands (raw LN input, gamma) of every element, loaded before any store
+    float lx[4][NR], lg[4][NR];
+    if (lnr) {
+#pragma unroll
+        for (int rr = 0; rr < 4; rr++) {
+            const int p = min(p0 + wave * 16 + 4 * kq + rr, npx - 1);
+#pragma unroll
+            for (int m = 0; m < NR; m++) {
+                const int n = min(n0 + 16 * m + i16, a.N - 1);
+                lx[rr][m] = a.lnr_x[((size_t)b * npx + p) * a.out_cs + a.out_off + n];
+                lg[rr][m] = a.lnr_gamma[(size_t)p * a.out_cs + a.out_off + n];
+            }
+        }
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; rr++) {
         const int p = p0 + wave * 16 + 4 * kq + rr;
@@ -297,7 +302,11 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
             if (a.res) v += a.res[ob + n];
             if (a.accumulate) v += a.out[ob + n];
             a.out[ob + n] = v;
-            if (lnr) lnr_add(a, ob + n, (size_t)p * a.out_cs + a.out_off + n, v, lmu, lrs, sg, sgh);
+            if (lnr) {
+                const float g = v * lg[rr][m], xh = (lrelu(lx[rr][m]) - lmu) * lrs;
+                sg += g;
+                sgh += (double)g * xh;
+            }
         }
     }
     if (lnr) lnr_finish(a, sg, sgh, b);
@@ -471,6 +480,24 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
     const bool lnr = a.lnr_part != nullptr;
     const float lmu = lnr ? a.lnr_stats[2 * b] : 0.f, lrs = lnr ? a.lnr_stats[2 * b + 1] : 0.f;
     double sg = 0.0, sgh = 0.0;
+    // the LN reduction's operands (raw LN input, gamma) of every element, loaded before any store
+    float lx[SUB][4][NR], lg[SUB][4][NR];
+    if (lnr) {
+#pragma unroll
+        for (int s = 0; s < SUB; s++)
+#pragma unroll
+            for (int rr = 0; rr < 4; rr++) {
+                const int q = (wave + 4 * s) * 16 + 4 * kq + rr;
+                const int orow = min(r0 + q / W, H - 1), ocol = q % W;
+                const size_t pix = (size_t)orow * W + ocol;
+#pragma unroll
+                for (int m = 0; m < NR; m++) {
+                    const int n = min(n0 + 16 * m + i16, a.N - 1);
+                    lx[s][rr][m] = a.lnr_x[((size_t)b * npx + pix) * a.out_cs + a.out_off + n];
+                    lg[s][rr][m] = a.lnr_gamma[pix * a.out_cs + a.out_off + n];
+                }
+            }
+    }
 #pragma unroll
     for (int s = 0; s < SUB; s++)
 #pragma unroll
@@ -489,7 +516,11 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 if (a.res) v += a.res[ob + n];
                 if (a.accumulate) v += a.out[ob + n];
                 a.out[ob + n] = v;
-                if (lnr) lnr_add(a, ob + n, pix * a.out_cs + a.out_off + n, v, lmu, lrs, sg, sgh);
+                if (lnr) {
+                    const float g = v * lg[s][rr][m], xh = (lrelu(lx[s][rr][m]) - lmu) * lrs;
+                    sg += g;
+                    sgh += (double)g * xh;
+                }
             }
         }
     if (lnr) lnr_finish(a, sg, sgh, b);
