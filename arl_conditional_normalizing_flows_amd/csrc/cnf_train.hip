@@ -422,17 +422,20 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
             for (int u = 0; u < 4; u++)
                 if (e0 + 256 * u < nq) *reinterpret_cast<f4*>(band + lo[u]) = v[u];
         }
-        // weights of the chunk: [tap][gq = 4g + kq'][j][s], k = kc + 16g + 4kq' + s (every tap at once
-        // when they fit next to the band, else one tap at a time)
+        // weights of the chunk: [tap][gq = 4g + kq'][j][s], k = kc + 16g + 4kq' + s, gq < GQ = 4 * the
+        // chunk's 16-channel groups (every tap at once when they fit next to the band, else one tap at a
+        // time; a 2-channel K stages 4 gq rows per tap, not 16)
+        const int GQ = 4 * ((KC + 15) >> 4);
+        const uint32_t m_gq = udiv_magic(GQ);
         auto stage_w = [&](int t0, int nt) {
-            const int nwc = nt * 16 * NS * 4;
+            const int nwc = nt * GQ * NS * 4;
             for (int e0 = threadIdx.x; e0 < nwc; e0 += 256 * TW_U) {
                 float v[TW_U];
 #pragma unroll
                 for (int u = 0; u < TW_U; u++) {
                     const int e = e0 + 256 * u;
-                    const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * 16 + gq
-                    const int tap = t0 + (rest >> 4), gq = rest & 15;
+                    const int s4 = e & 3, j = (e >> 2) % NS, rest = (e >> 2) / NS;   // rest = tap' * GQ + gq
+                    const int tq = udiv(rest, m_gq), tap = t0 + tq, gq = rest - tq * GQ;
                     const int k = kc + 4 * gq + s4, n = n0 + j;
                     const bool ok = e < nwc && k < a.K && n < a.N;
                     v[u] = *(ok ? a.w + (tap * a.wt + (long long)k * a.wk + (long long)n * a.wn) : a.zero);
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 __syncthreads();
             }
             const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-            const f4* wp = reinterpret_cast<const f4*>(wl) + (size_t)(all_taps ? tap : 0) * 16 * NS + (size_t)kq * NS + i16;
+            const f4* wp = reinterpret_cast<const f4*>(wl) + (size_t)(all_taps ? tap : 0) * GQ * NS + (size_t)kq * NS + i16;
             const float* ap[SUB];
 #pragma unroll
             for (int s = 0; s < SUB; s++) {
@@ -547,7 +550,8 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
     if (!train_valu() && !band_off && a.taps == 9 && a.dil <= 2 && a.W <= 64 && a.W >= 1) {
         const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
         const int NS = 16 * nr;
-        const size_t w1 = (size_t)16 * NS * 4 * 4;   // one tap of a 64-channel chunk
+        // one tap of a chunk's weights: 4 gq rows per 16-channel group of the (at most 64) chunk channels
+        const size_t w1 = (size_t)4 * ((std::min(64, a.K) + 15) / 16) * NS * 4 * 4;
         // subtiles per wave: tiles of 64 * SUB pixels amortise the weight staging and the halo rows over
         // more outputs, while the launch keeps >= 512 workgroups (two per CU) and the band fits LDS
         int sub = 1;
@@ -558,7 +562,11 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
             const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
             // (measured at cfg2 B=64, 32x32 branch dgrads: SUB=2 at 512 workgroups was slower than 1024
             // workgroups of one subtile per wave, so wider tiles only when they still leave >= 1024)
-            if (64 * s <= a.H * a.W && wgs >= 1024 && band + w1 <= 160 * 1024) sub = s;
+            static const long long minwg = [] {   // A/B knob
+                const char* e = std::getenv("CNF_TBAND_MINWG");
+                return e ? std::atoll(e) : 1024LL;
+            }();
+            if (64 * s <= a.H * a.W && wgs >= minwg && band + w1 <= 160 * 1024) sub = s;
         }
         const int TH = std::max(1, std::min(a.H, 64 * sub / a.W));
         const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
@@ -992,7 +1000,6 @@ __global__ __launch_bounds__(256) void k_wgrad_direct(WGradArgs a, int RB, int n
     const float* xb = a.x + (size_t)b * npx * a.x_cs + a.x_off;
     const float* gm = ln ? a.gamma + a.x_off : nullptr;
     const float* bt = ln ? a.beta + a.x_off : nullptr;
-    const float* gb = a.dy + (size_t)b * npx * a.dy_cs + a.dy_off + n0 + i16;
     const int W4 = W >> 2, nsteps = (y1 - y0) * W4;
     const uint32_t m_w4 = udiv_magic(W4);
     const bool do_bias = a.bpart != nullptr && blockIdx.y == 0;
@@ -1008,7 +1015,13 @@ __global__ __launch_bounds__(256) void k_wgrad_direct(WGradArgs a, int RB, int n
     // no select after a load: a lane outside the image (or past CO) reads the zero float a.zero for every
     // operand, so x = gamma = beta = 0 and its A is exactly 0; the next step's loads are issued before
     // this step's MFMAs and waited for only at the next step
-    const float* zp = a.zero;
+    // (buffer loads over the image's range: an out-of-range offset, BUF_OOB for a lane outside the
+    // image or past CO, returns 0 — no selects, 32-bit offsets)
+    const uint32_t xbytes = (uint32_t)(npx * a.x_cs - a.x_off) * 4u;
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xb, xbytes);
+    const __amdgpu_buffer_rsrc_t rgm = buf_rsrc(ln ? gm : xb, xbytes), rbt = buf_rsrc(ln ? bt : xb, xbytes);
+    const float* gbase = a.dy + (size_t)b * npx * a.dy_cs + a.dy_off;
+    const __amdgpu_buffer_rsrc_t rG = buf_rsrc(gbase, (uint32_t)(npx * a.dy_cs - a.dy_off) * 4u);
     float xr[MT], gr[MT], br[MT], gv[NT];
     auto load = [&](int j) {
         const int q = udiv(j, m_w4), yy = y0 + q, xx = 4 * (j - q * W4) + kq;
@@ -1016,16 +1029,16 @@ __global__ __launch_bounds__(256) void k_wgrad_direct(WGradArgs a, int RB, int n
         for (int mt = 0; mt < MT; mt++) {
             const int y = yy + dr[mt], x = xx + dc[mt];
             const bool ok = rv[mt] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-            const int idx = (y * W + x) * a.x_cs + cof[mt];
-            xr[mt] = *(ok ? xb + idx : zp);
+            const uint32_t off = ok ? (uint32_t)((y * W + x) * a.x_cs + cof[mt]) * 4u : BUF_OOB;
+            xr[mt] = buf_load1(rx, off);
             if (ln) {
-                gr[mt] = *(ok ? gm + idx : zp);
-                br[mt] = *(ok ? bt + idx : zp);
+                gr[mt] = buf_load1(rgm, off);
+                br[mt] = buf_load1(rbt, off);
             }
         }
-        const int gi = (yy * W + xx) * a.dy_cs;
+        const int gi = (yy * W + xx) * a.dy_cs + n0 + i16;
 #pragma unroll
-        for (int nt = 0; nt < NT; nt++) gv[nt] = *(nv[nt] ? gb + gi + 16 * nt : zp);
+        for (int nt = 0; nt < NT; nt++) gv[nt] = buf_load1(rG, nv[nt] ? (uint32_t)(gi + 16 * nt) * 4u : BUF_OOB);
     };
     int j = wave;
     if (j < nsteps) load(j);
