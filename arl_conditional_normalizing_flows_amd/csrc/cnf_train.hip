@@ -175,6 +175,10 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     const float* inb = a.in + (size_t)b * npx * a.in_cs + a.in_off;
     const bool ln = a.stats != nullptr;
     const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+    const uint32_t inbytes = (uint32_t)(npx * a.in_cs - a.in_off) * 4u;
+    const __amdgpu_buffer_rsrc_t rin = buf_rsrc(inb, inbytes);
+    const __amdgpu_buffer_rsrc_t rgm = buf_rsrc(ln ? a.gamma + a.in_off : inb, inbytes);
+    const __amdgpu_buffer_rsrc_t rbt = buf_rsrc(ln ? a.beta + a.in_off : inb, inbytes);
     f4 acc[NR];
 #pragma unroll
     for (int m = 0; m < NR; m++) acc[m] = f4{0.f, 0.f, 0.f, 0.f};
@@ -205,12 +209,13 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
         const int k0 = 16 * g + 4 * kq;
         const bool sv = pav && r >= 0 && r < a.H && c >= 0 && c < a.W && k0 < a.K;
         const size_t gi = ((size_t)r * a.W + c) * a.in_cs + k0;
-        if (VEC) {   // branch-free: an invalid lane reads zeros (the caller's LN / LeakyReLU maps them to 0)
-            x = *reinterpret_cast<const f4*>(sv ? inb + gi : a.zero);
+        if (VEC) {   // branch-free buffer loads: an invalid lane's offset is out of range and reads zeros
+            const uint32_t off = sv ? (uint32_t)gi * 4u : BUF_OOB;
+            x = buf_load4(rin, off);
             gm = bt = f4{0.f, 0.f, 0.f, 0.f};
             if (ln) {
-                gm = *reinterpret_cast<const f4*>(sv ? a.gamma + a.in_off + gi : a.zero);
-                bt = *reinterpret_cast<const f4*>(sv ? a.beta + a.in_off + gi : a.zero);
+                gm = buf_load4(rgm, off);
+                bt = buf_load4(rbt, off);
             }
             return sv;
         }
@@ -352,6 +357,10 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
 #pragma unroll
         for (int m = 0; m < NR; m++) acc[s][m] = f4{0.f, 0.f, 0.f, 0.f};
     const bool vq = (a.in_cs & 3) == 0 && (a.in_off & 3) == 0;
+    const uint32_t inbytes = (uint32_t)(npx * a.in_cs - a.in_off) * 4u;
+    const __amdgpu_buffer_rsrc_t rin = buf_rsrc(inb, inbytes);
+    const __amdgpu_buffer_rsrc_t rgm = buf_rsrc(ln ? a.gamma + a.in_off : inb, inbytes);
+    const __amdgpu_buffer_rsrc_t rbt = buf_rsrc(ln ? a.beta + a.in_off : inb, inbytes);
     // whole quads of K from 16-byte loads (and aligned gamma / beta): the branch-free staging path
     const bool fullq = vq && (a.K & 3) == 0 && (!ln || ((((uintptr_t)a.gamma) | ((uintptr_t)a.beta)) & 15) == 0);
     const uint32_t m_bw = udiv_magic(BW);
@@ -378,11 +387,11 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                     // branch-free: lanes outside the image (or past K) read zeros for x, gamma and beta,
                     // which the LN / LeakyReLU map to exactly 0
                     const bool ok = in && k < a.K;
-                    const size_t gi = ((size_t)r * W + c) * a.in_cs + k;
-                    const f4 x = *reinterpret_cast<const f4*>(ok ? inb + gi : a.zero);
+                    const uint32_t off = ok ? (uint32_t)((r * W + c) * a.in_cs + k) * 4u : BUF_OOB;
+                    const f4 x = buf_load4(rin, off);
                     if (ln) {
-                        const f4 gq = *reinterpret_cast<const f4*>(ok ? a.gamma + a.in_off + gi : a.zero);
-                        const f4 bq = *reinterpret_cast<const f4*>(ok ? a.beta + a.in_off + gi : a.zero);
+                        const f4 gq = buf_load4(rgm, off);
+                        const f4 bq = buf_load4(rbt, off);
 #pragma unroll
                         for (int jj = 0; jj < 4; jj++) v[u][jj] = (lrelu(x[jj]) - mu) * rs * gq[jj] + bq[jj];
                     } else {
