@@ -376,6 +376,7 @@ struct TConvArgs {
     const float* lnr_gamma;
     const float* lnr_stats;
     double* lnr_part;
+    int lnr_base, lnr_stride;   // the launch's partials at [b][lnr_base + tile] of a [B][lnr_stride] array
 };
 // returns the LN-reduction partials per image the launch wrote (0: none — the kernel has no fused
 // reduction, the caller runs k_lnb_reduce)
@@ -423,10 +424,11 @@ constexpr int LNB_SLICES = 8;
 // k_lnb_reduce splits each image over up to LNB_RS workgroups (partial sums [B][rs][2], summed in slice
 // order where they are read)
 constexpr int LNB_RS = 8;
-// presum > 0: sums already holds [B][presum][2] partials (a k_tconv_* fused LN reduction), no k_lnb_reduce
+// presum > 0: sums already holds presum partials per image at [b][k] of a [B][pstride][2] array (k_tconv_*
+// fused LN reductions), no k_lnb_reduce
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st, int presum = 0);
+                        float* scratch, hipStream_t st, int presum = 0, int pstride = 0);
 // Fused training backward of a k_net_lds layer (cnf_ldsbwd.hip): grid (B, 2 nets), one workgroup per
 // (image, net). Offsets table per net (int32, `offs_per_net` entries): canonical parameter offsets
 // (LN gamma / beta, the net's first parameter, tanh scale or -1) and dense backward-image offsets

@@ -331,6 +331,7 @@ struct LnRed {
     const float* x = nullptr;
     const float* gamma = nullptr;
     const float* stats = nullptr;
+    int base = 0;   // this launch's first partial (several launches that write disjoint windows share one LN)
 };
 int conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, int cout, const PackedConv& pc, int cin,
                int dil, float* dx, int dx_cs, int dx_off, int accumulate, const LnRed* lr = nullptr) {
@@ -340,6 +341,8 @@ int conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, i
         a.lnr_gamma = lr->gamma;
         a.lnr_stats = lr->stats;
         a.lnr_part = E.at<double>(E.T.lnsum[E.net]);
+        a.lnr_base = lr->base;
+        a.lnr_stride = LNR_MAXPARTS;
     }
     a.in = dy;
     a.in_cs = dy_cs;
@@ -460,7 +463,7 @@ void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long lon
             int64_t g_off, int64_t b_off, int presum = 0) {
     launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum[E.net]), n, E.B, 1, dx, accumulate,
                        ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr,
-                       E.at<float>(E.T.lnpart[E.net]), E.st, presum);
+                       E.at<float>(E.T.lnpart[E.net]), E.st, presum, LNR_MAXPARTS);
 }
 
 // the plan's side stream and fork / join events (created on first use on the current device)
@@ -725,21 +728,30 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
         } else if (part == 1) {   // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
             hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
-            // the LN2 reduction rides on the last branch's data gradient when every branch writes the same
-            // window (the reference group mode): only then does that launch see the final dbuf everywhere it
-            // is non-zero
-            bool one_window = true;
-            for (const Branch& b : c.br) one_window = one_window && b.cin_off == c.br[0].cin_off && b.cin == c.br[0].cin;
-            const LnRed r2{T1(n, r), l2.gamma, l2.stats};
+            // the LN2 reduction rides on the branches' data gradients when their windows are pairwise disjoint
+            // (the reference group mode's closure windows [(card - 1) w, card w) of each branch width w): each
+            // element of dbuf is then final after the one launch that writes it, and each launch adds its
+            // window's partials after the previous launches'
+            const int nb = (int)c.br.size();
+            bool disjoint = true;
+            for (int i = 0; i < nb; i++)
+                for (int j = i + 1; j < nb; j++)
+                    disjoint = disjoint && (c.br[i].cin_off + c.br[i].cin <= c.br[j].cin_off ||
+                                            c.br[j].cin_off + c.br[j].cin <= c.br[i].cin_off);
             int ps = 0;
-            for (size_t bi = 0; bi < c.br.size(); bi++) {
+            bool fused = disjoint;
+            for (int bi = 0; bi < nb; bi++) {
                 const Branch& b = c.br[bi];
                 ev_gc[n] = conv_wgrad(En, h, w, T1(n, r), nk, b.cin_off, b.cin, l2, dt2, gc, b.out_off, b.cout,
                                       rb.gc[bi], b.dil);
-                const bool last = bi + 1 == c.br.size();
-                ps = conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk, b.cin_off, 1,
-                                last && one_window ? &r2 : nullptr);
+                LnRed r2{T1(n, r), l2.gamma, l2.stats};
+                r2.base = ps;
+                const int np = conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk,
+                                          b.cin_off, 1, fused ? &r2 : nullptr);
+                fused = fused && np > 0;
+                ps += np;
             }
+            if (!fused) ps = 0;   // (k_lnb_reduce, over whatever partials were written)
             chain_wait(En, ev_ca[n]);
             ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b, ps);
         } else {   // conv_a

@@ -151,9 +151,9 @@ __device__ __forceinline__ void lnr_finish(const TConvArgs& a, double sg, double
             s0 += lred[2 * w];
             s1 += lred[2 * w + 1];
         }
-        const int tile = blockIdx.x + gridDim.x * blockIdx.z, np = gridDim.x * gridDim.z;
-        a.lnr_part[2 * ((size_t)b * np + tile)] = s0;
-        a.lnr_part[2 * ((size_t)b * np + tile) + 1] = s1;
+        const size_t k = (size_t)b * a.lnr_stride + a.lnr_base + blockIdx.x + gridDim.x * blockIdx.z;
+        a.lnr_part[2 * k] = s0;
+        a.lnr_part[2 * k + 1] = s1;
     }
 }
 #ifndef CNF_TW_U
@@ -549,7 +549,7 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
     const int npx = a.H * a.W;
     // a fused LN reduction writes one partial per workgroup of an image: drop it where there are too many
     auto lnr_ok = [&](const dim3& g) {
-        if (a.lnr_part != nullptr && (int)(g.x * g.z) > LNR_MAXPARTS) a.lnr_part = nullptr;
+        if (a.lnr_part != nullptr && a.lnr_base + (int)(g.x * g.z) > a.lnr_stride) a.lnr_part = nullptr;
         return a.lnr_part != nullptr ? (int)(g.x * g.z) : 0;
     };
     static const bool band_off = [] {   // A/B knob: no band-staged 3x3 kernel
@@ -1392,7 +1392,8 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
 // registers; k_lnb_gsum adds the slices in a fixed order (no atomics: deterministic)
 __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, const float* __restrict__ dxo,
                                                    const float* __restrict__ gamma, const float* __restrict__ stats,
-                                                   const double* __restrict__ sums, int rsl, long long n, int B, int act,
+                                                   const double* __restrict__ sums, int rsl, int rstride, long long n,
+                                                   int B, int act,
                                                    float* __restrict__ dx, int accumulate, float* __restrict__ gpart,
                                                    float* __restrict__ bpart) {
     const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -1432,8 +1433,8 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
                 rs = stats[2 * b + 1];
                 double s0 = 0.0, s1 = 0.0;   // the image's slice partials, in slice order
                 for (int k = 0; k < rsl; k++) {
-                    s0 += sums[2 * ((size_t)b * rsl + k)];
-                    s1 += sums[2 * ((size_t)b * rsl + k) + 1];
+                    s0 += sums[2 * ((size_t)b * rstride + k)];
+                    s1 += sums[2 * ((size_t)b * rstride + k) + 1];
                 }
                 mg = (float)(s0 * inv_n);
                 mgh = (float)(s1 * inv_n);
@@ -1484,22 +1485,24 @@ __global__ __launch_bounds__(256) void k_lnb_gsum(const float* __restrict__ gpar
 
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st, int presum) {
+                        float* scratch, hipStream_t st, int presum, int pstride) {
     // slices per image: at least two full passes of the workgroup each (64 images x 8 slices fill the
     // GPU where one workgroup per image used a quarter of it)
 #ifndef CNF_LNB_RS
 #define CNF_LNB_RS LNB_RS
 #endif
     int rsl = (int)std::min<long long>(CNF_LNB_RS, std::max<long long>(1, (n / 4) / (2LL * LNT)));
-    if (presum > 0)
+    int rstride = rsl;
+    if (presum > 0) {
         rsl = presum;
-    else if (stats)
+        rstride = pstride > 0 ? pstride : presum;
+    } else if (stats)
         hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
     const int S = B < LNB_SLICES ? B : LNB_SLICES;
     float* gpart = scratch;
     float* bpart = scratch + (size_t)LNB_SLICES * n;
     hipLaunchKernelGGL(k_lnb_apply, dim3((unsigned)((n + 1023) / 1024), S), dim3(256), 0, st, x, dxo, gamma, stats,
-                       sums, rsl, n, B, act, dx, accumulate, gpart, bpart);
+                       sums, rsl, rstride, n, B, act, dx, accumulate, gpart, bpart);
     if (stats)
         hipLaunchKernelGGL(k_lnb_gsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gpart, bpart, S, n, dgamma,
                            dbeta);
