@@ -185,7 +185,27 @@ __global__ __launch_bounds__(256) void k_tconv_mfma(TConvArgs a, int all_taps) {
     const int nw = G * 16 * NS;   // weight floats of one tap
     // (TW_U loads in flight per thread: the transposed weight reads are scattered 4-byte loads, and one
     // at a time they cost a memory round trip each)
+    const bool wvec = a.wk == 1 && (a.wn & 3) == 0 && (a.K & 3) == 0 && a.wt * a.taps < (1LL << 29);
+    const __amdgpu_buffer_rsrc_t rw = buf_rsrc(a.w, (uint32_t)((a.wt * a.taps) * 4));
     auto stage_w = [&](int tap, float* dst) {
+        if (wvec) {   // (as in k_tconv_band: one 16-byte load per (gq, j) of a data gradient's weights)
+            const int nw4 = nw >> 2;
+            for (int e0 = threadIdx.x; e0 < nw4; e0 += 256 * TW_U) {
+                f4 v[TW_U];
+#pragma unroll
+                for (int u = 0; u < TW_U; u++) {
+                    const int e = e0 + 256 * u;
+                    const int j = e % NS, gq = e / NS;
+                    const int k = 4 * gq, n = n0 + j;
+                    const bool ok = e < nw4 && k < a.K && n < a.N;
+                    v[u] = buf_load4(rw, ok ? (uint32_t)(tap * (int)a.wt + n * a.wn + k) * 4u : BUF_OOB);
+                }
+#pragma unroll
+                for (int u = 0; u < TW_U; u++)
+                    if (e0 + 256 * u < nw4) *reinterpret_cast<f4*>(dst + 4 * (e0 + 256 * u)) = v[u];
+            }
+            return;
+        }
         for (int e0 = threadIdx.x; e0 < nw; e0 += 256 * TW_U) {
             float v[TW_U];
 #pragma unroll
@@ -436,8 +456,32 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
         // time; a 2-channel K stages 4 gq rows per tap, not 16)
         const int GQ = 4 * ((KC + 15) >> 4);
         const uint32_t m_gq = udiv_magic(GQ);
+        // (buffer loads need 4-byte alignment only: the conv's offset in the dense image may be any float)
+        const bool wvec = a.wk == 1 && (a.wn & 3) == 0 && (a.K & 3) == 0 && (kc & 3) == 0 && a.wt * 9 < (1LL << 29);
+        const __amdgpu_buffer_rsrc_t rw = buf_rsrc(a.w, (uint32_t)((a.wt * 9) * 4));
         auto stage_w = [&](int t0, int nt) {
             const int nwc = nt * GQ * NS * 4;
+            if (wvec) {
+                // a data gradient's weights (wk == 1): the 4 k of an s-quad are consecutive in the dense
+                // image, one 16-byte buffer load per (tap, gq, j); out-of-range k / n read 0
+                const int nw4 = nwc >> 2;
+                for (int e0 = threadIdx.x; e0 < nw4; e0 += 256 * TW_U) {
+                    f4 v[TW_U];
+#pragma unroll
+                    for (int u = 0; u < TW_U; u++) {
+                        const int e = e0 + 256 * u;
+                        const int j = e % NS, rest = e / NS;
+                        const int tq = udiv(rest, m_gq), tap = t0 + tq, gq = rest - tq * GQ;
+                        const int k = kc + 4 * gq, n = n0 + j;
+                        const bool ok = e < nw4 && k < a.K && n < a.N;
+                        v[u] = buf_load4(rw, ok ? (uint32_t)(tap * (int)a.wt + n * a.wn + k) * 4u : BUF_OOB);
+                    }
+#pragma unroll
+                    for (int u = 0; u < TW_U; u++)
+                        if (e0 + 256 * u < nw4) *reinterpret_cast<f4*>(wl + 4 * (e0 + 256 * u)) = v[u];
+                }
+                return;
+            }
             for (int e0 = threadIdx.x; e0 < nwc; e0 += 256 * TW_U) {
                 float v[TW_U];
 #pragma unroll
@@ -1243,6 +1287,14 @@ __global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__
     __shared__ double red[16][64];
     const int t = threadIdx.x, el = t & 63, sl = t >> 6;
     const long long i = (long long)blockIdx.x * 64 + el;
+    // the destination and its current value are fetched first, behind the partial-row loads (only this
+    // launch writes these parameters' gradients)
+    int64_t dst = -1;
+    float old = 0.f;
+    if (sl == 0 && i < n) {
+        dst = map[i];
+        if (dst >= 0) old = dparams[dst];
+    }
     double s = 0.0;
     if (i < n) {
         for (int c0 = sl; c0 < chunks; c0 += 16 * 8) {
@@ -1262,8 +1314,7 @@ __global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__
         double tot = 0.0;
 #pragma unroll
         for (int k = 0; k < 16; k++) tot += red[k][el];
-        const int64_t dst = map[i];
-        if (dst >= 0) dparams[dst] += (float)tot;
+        if (dst >= 0) dparams[dst] = old + (float)tot;
     }
 }
 
@@ -1390,6 +1441,7 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
 // four consecutive elements per lane (one float4), over the images of batch slice blockIdx.y (four
 // at a time, their loads in flight together): dx, and the slice's dgamma / dbeta partials summed in
 // registers; k_lnb_gsum adds the slices in a fixed order (no atomics: deterministic)
+constexpr int LNA_MAXIMG = 256;   // images per batch slice whose sums k_lnb_apply shares through LDS
 __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, const float* __restrict__ dxo,
                                                    const float* __restrict__ gamma, const float* __restrict__ stats,
                                                    const double* __restrict__ sums, int rsl, int rstride, long long n,
@@ -1397,9 +1449,27 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
                                                    float* __restrict__ dx, int accumulate, float* __restrict__ gpart,
                                                    float* __restrict__ bpart) {
     const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (e0 >= n) return;
     const int S = gridDim.y, sl = blockIdx.y;
     const int bs = (B + S - 1) / S, b_lo = sl * bs, b_hi = min(B, b_lo + bs);
+    const float inv_n0 = 1.f / (float)n;
+    // the slice's per-image means of g and g * xhat, summed once per workgroup (one thread per image, its
+    // partials in order) instead of by every thread
+    __shared__ float smg[LNA_MAXIMG], smgh[LNA_MAXIMG];
+    const bool shared_sums = stats != nullptr && b_hi - b_lo <= LNA_MAXIMG;
+    if (shared_sums) {
+        const int b = b_lo + (int)threadIdx.x;
+        if (b < b_hi) {
+            double s0 = 0.0, s1 = 0.0;
+            for (int k = 0; k < rsl; k++) {
+                s0 += sums[2 * ((size_t)b * rstride + k)];
+                s1 += sums[2 * ((size_t)b * rstride + k) + 1];
+            }
+            smg[threadIdx.x] = (float)(s0 * inv_n0);
+            smgh[threadIdx.x] = (float)(s1 * inv_n0);
+        }
+        __syncthreads();
+    }
+    if (e0 >= n) return;
     const bool vec = (n & 3) == 0;
     const int ne = n - e0 < 4 ? (int)(n - e0) : 4;
     f4 gm = f4{1.f, 1.f, 1.f, 1.f}, dg = f4{0.f, 0.f, 0.f, 0.f}, dbt = f4{0.f, 0.f, 0.f, 0.f};
@@ -1431,13 +1501,18 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
             if (stats) {
                 mu = stats[2 * b];
                 rs = stats[2 * b + 1];
-                double s0 = 0.0, s1 = 0.0;   // the image's slice partials, in slice order
-                for (int k = 0; k < rsl; k++) {
-                    s0 += sums[2 * ((size_t)b * rstride + k)];
-                    s1 += sums[2 * ((size_t)b * rstride + k) + 1];
+                if (shared_sums) {
+                    mg = smg[b - b_lo];
+                    mgh = smgh[b - b_lo];
+                } else {
+                    double s0 = 0.0, s1 = 0.0;   // the image's slice partials, in slice order
+                    for (int k = 0; k < rsl; k++) {
+                        s0 += sums[2 * ((size_t)b * rstride + k)];
+                        s1 += sums[2 * ((size_t)b * rstride + k) + 1];
+                    }
+                    mg = (float)(s0 * inv_n);
+                    mgh = (float)(s1 * inv_n);
                 }
-                mg = (float)(s0 * inv_n);
-                mgh = (float)(s1 * inv_n);
             }
             f4 g4;
 #pragma unroll
