@@ -310,9 +310,16 @@ void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int
 // LN partial slots [B][part_stride][LNP] of one tensor (two nets: part0, part1 or null) merged into
 // slot 0 of each image (k_ln_merge): consumers then read nparts = 1
 void launch_ln_merge(float* part0, float* part1, int nparts, int part_stride, int B, hipStream_t st);
-// (mean, rstd) [B][2] per net of one LN tensor from its producer's partial slots (as in_ln)
-void launch_ln_final(const float* part0, const float* part1, int nparts, int part_stride, int B, float* st0, float* st1,
-                     hipStream_t st);
+// (mean, rstd) [B][2] per net of up to LNF_MAX LN tensors from their producers' partial slots (as in_ln),
+// one launch: tensor i's slots part[i][net] ([B][part_stride][LNP], nparts[i] used) -> st[i][net]
+constexpr int LNF_MAX = 4;
+struct LnFinalSet {
+    const float* part[LNF_MAX][2];
+    float* st[LNF_MAX][2];
+    int nparts[LNF_MAX];
+    int count, part_stride;
+};
+void launch_ln_final(const LnFinalSet& s, int B, hipStream_t st);
 void launch_map_gather(const float* src, float* dst, const int* idx, int n, int ss, int ds, int B, hipStream_t st);
 void launch_map_scatter(const float* src, float* dst, const int* sidx, const int* didx, int n, int ss, int ds,
                         int B, hipStream_t st);

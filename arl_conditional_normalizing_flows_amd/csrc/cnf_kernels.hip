@@ -875,25 +875,24 @@ void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
 // Training forward of a streamed layer: (mean, rstd) of one LN tensor per (image, net) from its
 // producer's partial slots, folded exactly as the consumer kernels fold them (in_ln): the statistics
 // the backward uses are bitwise the forward's. One wave per (image, net).
-__global__ __launch_bounds__(64) void k_ln_final(const float* __restrict__ part0, const float* __restrict__ part1,
-                                                 int nparts, int part_stride, float* __restrict__ st0,
-                                                 float* __restrict__ st1) {
-    const int img = blockIdx.x, net = blockIdx.y, lane = threadIdx.x;
-    const float* q = (net == 0 ? part0 : part1) + (size_t)img * part_stride * LNP;
+__global__ __launch_bounds__(64) void k_ln_final(LnFinalSet a) {
+    const int img = blockIdx.x, t = blockIdx.y >> 1, net = blockIdx.y & 1, lane = threadIdx.x;
+    const float* q = a.part[t][net] + (size_t)img * a.part_stride * LNP;
+    const int nparts = a.nparts[t];
     float n = 0.f, m = 0.f, M2 = 0.f;
     for (int i = lane; i < nparts; i += 64) ln_fold(*reinterpret_cast<const f4*>(q + (size_t)LNP * i), n, m, M2);
     float mu, rstd;
     ln_wave_final(n, m, M2, mu, rstd);
     if (lane == 0) {
-        float* s = net == 0 ? st0 : st1;
+        float* s = a.st[t][net];
         s[2 * img] = mu;
         s[2 * img + 1] = rstd;
     }
 }
 
-void launch_ln_final(const float* part0, const float* part1, int nparts, int part_stride, int B, float* st0, float* st1,
-                     hipStream_t st) {
-    CNF_LAUNCH(k_ln_final, dim3(B, 2), dim3(64), 0, st, part0, part1, nparts, part_stride, st0, st1);
+void launch_ln_final(const LnFinalSet& s, int B, hipStream_t st) {
+    if (s.count <= 0) return;
+    CNF_LAUNCH(k_ln_final, dim3(B, 2 * s.count), dim3(64), 0, st, s);
 }
 
 void launch_ln_merge(float* part0, float* part1, int nparts, int part_stride, int B, hipStream_t st) {

@@ -740,15 +740,28 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         }
         for (int n = 0; n < 2; n++) sl[n][k].nparts = nparts;
     };
-    // training save: the statistics of LN tensor i (see TrainLayout::StreamSave) from slab k's slots
+    // training save: the statistics of LN tensor i (see TrainLayout::StreamSave) from slab k's slots, folded
+    // by one k_ln_final per residual block (flush_stats before conv_b overwrites slab 0, and at the end):
+    // the three slabs hold y_r, t1_r and t2_r until then
+    LnFinalSet pend_stats{};
+    pend_stats.part_stride = L.st_parts;
+    auto flush_stats = [&]() {
+        if (pend_stats.count == 0) return;
+        const LnFinalSet fs = pend_stats;
+        double bytes = 0.0;
+        for (int q = 0; q < fs.count; q++) bytes += 16.0 * B * fs.nparts[q] * 2;
+        E.record("k_ln_final", 0, bytes, [=](void* st) { launch_ln_final(fs, B, (hipStream_t)st); });
+        pend_stats.count = 0;
+    };
     auto save_stats = [&](int k, int i) {
         if (ss == nullptr || !ln) return;
-        const float* p0 = sl[0][k].part;
-        const float* p1 = sl[1][k].part;
-        float* s0 = SST(0, i);
-        float* s1 = SST(1, i);
-        const int np = sl[0][k].nparts, ps = L.st_parts;
-        E.record("k_ln_final", 0, 16.0 * B * np * 2, [=](void* st) { launch_ln_final(p0, p1, np, ps, B, s0, s1, (hipStream_t)st); });
+        if (pend_stats.count == LNF_MAX) flush_stats();
+        const int q = pend_stats.count++;
+        pend_stats.part[q][0] = sl[0][k].part;
+        pend_stats.part[q][1] = sl[1][k].part;
+        pend_stats.st[q][0] = SST(0, i);
+        pend_stats.st[q][1] = SST(1, i);
+        pend_stats.nparts[q] = sl[0][k].nparts;
     };
     auto in_slab = [&](int n, int k) { return ln ? sl[n][k] : Slab{}; };
     const float* none = nullptr;
@@ -926,6 +939,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         }
         // conv_b: LN3(LReLU(t2)) -> 1x1 -> + shortcut -> y (in place)
         {
+            flush_stats();   // (conv_b writes slab 0's slots: y_r's statistics first)
             std::vector<ProbSpec> pr;
             for (int n = 0; n < 2; n++) {
                 const RBParams& rb = c.net[n].rb[r];
@@ -941,6 +955,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             save_stats(0, r + 1);
         }
     }
+    flush_stats();
     // conv_out: LN_out(LReLU(y)) -> 3x3 -> so (raw A pre-tanh / b); > 64 outputs in 64-channel chunks
     {
         std::vector<ProbSpec> pr;
