@@ -1221,6 +1221,14 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     }();
     CoupPend pend;
     bool have_pend = false;
+    // training: a layer whose output is the next coupling's input writes it straight into that coupling's
+    // save slot (no copy of every layer input; only the first coupling's, which reads xy)
+    auto save_slot_after = [&](size_t li) -> float* {
+        size_t nx = li + 1;
+        while (nx < p.layers.size() && p.layers[nx].kind == CNF_LAYER_SQUEEZE) nx++;
+        if (!save_inputs || nx >= p.layers.size() || p.layers[nx].kind != CNF_LAYER_COUPLING) return nullptr;
+        return E.at<float>(TL.save_u[p.couplings[p.layers[nx].ci].index]);
+    };
     for (size_t li = 0; li < p.layers.size(); li++) {
         const Layer& ly = p.layers[li];
         if (ly.kind == CNF_LAYER_COUPLING) {
@@ -1233,7 +1241,8 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             const bool next_maps = nx >= p.layers.size() || p.layers[nx].kind == CNF_LAYER_FACTOR;
             const bool defer = fuse && !save_inputs && c.use_lds && (next_lds || next_maps);
             float* nxt = buf[which];
-            if (save_inputs) {
+            if (float* slot = save_slot_after(li)) nxt = slot;
+            if (save_inputs && cur != E.at<float>(TL.save_u[c.index])) {
                 float* dst = E.at<float>(TL.save_u[c.index]);
                 const float* src = cur;
                 const size_t bytes = (size_t)B * c.H * c.W * c.D * 4;
@@ -1268,6 +1277,8 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
             // with a pending coupling the maps read u_k (the other buffer) on the fly, and v_k's
             // own buffer (cur, never written) takes the kept half
             float* nxt = have_pend ? const_cast<float*>(cur) : buf[which];
+            if (!have_pend)
+                if (float* slot = save_slot_after(li)) nxt = slot;
             const bool flip = !have_pend;
             const int* T = p.dtab(0);
             const float* src = cur;
