@@ -68,6 +68,8 @@ struct ConvProb {
     const int* st_map;                     // [64][2]: channel -> (offset of pixel 0 inside the image, pixel stride) in floats, offset < 0: not stored
     int in_mapped;                         // 1: A-operand quads through in_map (k_pw only; in_cs = floats per pixel of an image)
     const int* in_map;                     // [quad][2]: input channel quad -> (offset of pixel 0 inside the image, pixel stride)
+    float* out2;                           // k_pw only: also every output channel, plain [B][HW][cout] (null: none) —
+                                           // the training forward's full t1 next to conv_a's mapped stores
 };
 
 struct ConvArgs {

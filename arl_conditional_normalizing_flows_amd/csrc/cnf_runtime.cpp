@@ -243,6 +243,7 @@ struct ProbSpec {
     Slab out_st;              // .part == null: no output statistics
     int out_part_base;        // first partial slot of this problem
     int dil;
+    float* out2 = nullptr;    // k_pw only: every output channel also to a plain [B][HW][cout] tensor
 };
 
 static const char* role_name(int r) {
@@ -272,7 +273,7 @@ struct TapSrc {
 // returns the LN-partial slots per image each problem writes (4 per workgroup tile)
 static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vector<ProbSpec>& probs,
                        uint64_t store_mask = ~0ull, const TapSrc* tap = nullptr, const int* st_map = nullptr,
-                       const int* in_map = nullptr) {
+                       const int* in_map = nullptr, bool* dual_done = nullptr) {
     const bool st_compact = st_map != nullptr;
     if (probs.empty()) return 0;
     if ((int)probs.size() > MAXPROB) throw std::invalid_argument("too many problems in one conv launch");
@@ -327,6 +328,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         q.st_map = st_map;
         q.in_mapped = in_map != nullptr ? 1 : 0;
         q.in_map = in_map;
+        q.out2 = s.out2;
         if (in_map != nullptr && (ks != 1 || tap != nullptr || s.in_off != 0 || s.cin % 4 != 0))
             throw std::logic_error("mapped input: plain k_pw over whole quads only");
         if (st_compact && (s.res != nullptr || s.cout > 64)) throw std::logic_error("mapped stores: no residual, <= 64 outputs");
@@ -393,6 +395,9 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
                  (tap == nullptr || (double)tap->img * 4.0 < 2147483648.0);
     const bool pw_ok = ks == 1 && vec && pw_gm > 0 && ln_uniform && fits32 && E.p.use_pw;
     if ((st_compact || in_map != nullptr) && !pw_ok) throw std::logic_error("mapped loads / stores need the k_pw path");
+    if (dual_done != nullptr) *dual_done = pw_ok;   // (the other kernels ignore out2)
+    if (!pw_ok)
+        for (int i = 0; i < a.nprob; i++) a.p[i].out2 = nullptr;
     if (ks == 3) {
         const int grid_x = E.B * g.tiles;
         const int mr = g.MR;
@@ -806,12 +811,16 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + rb.ln1g : none,
                                       ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.t1_cs, 0, c.nk,
                                       none, out_slab(n, 1, 4 * nt1), 0, 1});
+                // training: the full t1_r for the backward's LN2 from the same launch (k_pw's second store)
+                if (ss != nullptr) pr.back().out2 = ST1(n, r);
             }
             // only the channels the branches read are stored (into their consumers' sub-tensors when
             // t1_compact); the LN2 statistics still cover all nk channels
             const int* t1map = c.t1_compact ? E.p.dtab(c.dev_t1_map) : nullptr;
-            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map));
-            if (ss != nullptr) {
+            bool dual = false;
+            set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map, nullptr, &dual));
+            if (ss != nullptr && dual) save_stats(1, c.R + 1 + r);
+            if (ss != nullptr && !dual) {
                 // the full t1_r for the backward's LN2 (the compact t1 above holds only the branch windows)
                 std::vector<ProbSpec> pf;
                 for (int n = 0; n < 2; n++) {

@@ -58,7 +58,9 @@ int read_pw_stamps(long long* host) {
 #endif
 constexpr int pw_depth(int gm, bool res) { return res ? 1 : gm <= 4 ? CNF_PW_DEPTH : (CNF_PW_DEPTH < 2 ? CNF_PW_DEPTH : 2); }
 
-template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false>
+// DUAL (generic non-tap instantiations of the training forward only): every output element is also
+// stored densely ([HW][cout]) to P.out2 -- conv_a's full t1 saved for the backward in the same launch
+template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false>
 __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
@@ -300,6 +302,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         }
         // epilogue: bias, residual, masked store, per-wave LN partial of LeakyReLU(out)
         const auto rout = img_rsrc(P.out, img, out_img);
+        const auto rout2 = img_rsrc(DUAL ? P.out2 : P.out, img, (uint32_t)HW * cout * 4u);
         constexpr uint32_t ob = 0;
         float vals[NR * 4];
         bool valid[NR * 4];
@@ -312,6 +315,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 #ifndef CNF_ABL_PW_NOSTORE
                 const uint32_t o = ooff(n, r);
                 buf_store1(rout, o == BUF_OOB ? BUF_OOB : ob + o, v);
+                if constexpr (DUAL)
+                    buf_store1(rout2, pv(r) && chv(n) ? (uint32_t)((po0 + r) * cout + 16 * n + i16) * 4u : BUF_OOB, v);
 #endif
                 vals[n * 4 + r] = lrelu(v);
                 valid[n * 4 + r] = pv(r) && chv(n);
@@ -351,6 +356,23 @@ int pw_num_shapes() { return CNF_PW_NSHAPES; }
 void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
     const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob (read per launch: tests switch it)
+    bool dual = false;
+    for (int i = 0; i < a.nprob; i++) dual |= a.p[i].out2 != nullptr;
+    if (dual) {   // training forward conv_a with the dense t1 copy: generic instantiations only
+        if (tap || res || !ln) throw std::invalid_argument("k_pw dual store: LN, no residual, no tap mode");
+        for (int i = 0; i < a.nprob; i++)
+            if (a.p[i].out2 == nullptr) throw std::invalid_argument("k_pw dual store: every problem needs out2");
+#define CNF_PW_DCASE(NR_, GM_)                                                         \
+        if (nr == NR_ && gm == GM_) {                                                  \
+            CNF_LAUNCH((k_pw<NR_, GM_, true, false, -1, false, true>), g, b, lds, st, a); \
+            return;                                                                    \
+        }
+#define CNF_PW_DNR(GM_) CNF_PW_DCASE(1, GM_) CNF_PW_DCASE(2, GM_) CNF_PW_DCASE(3, GM_) CNF_PW_DCASE(4, GM_)
+        CNF_PW_DNR(1) CNF_PW_DNR(2) CNF_PW_DNR(4) CNF_PW_DNR(8)
+#undef CNF_PW_DNR
+#undef CNF_PW_DCASE
+        throw std::invalid_argument("k_pw dual store: no instantiation for this shape");
+    }
     PwShape sh;
     if (!generic && pw_shape_of(nr, gm, ln, res, tap, a, sh))
         for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
