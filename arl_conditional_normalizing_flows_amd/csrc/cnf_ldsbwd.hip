@@ -10,7 +10,7 @@
 // v_mfma_f32_16x16x4_f32 over the transposed weights (3x3 taps mirrored through a k-table); weight
 // gradients contract over the image's pixels on MFMA. Every parameter gradient of the image goes to
 // its (net, image) row of the partial buffer in the net's canonical parameter order (convs through
-// the dense backward map), and k_grad_rows sums the rows over the batch in image order: the result is
+// the dense backward map), and k_grad_rows sums the rows over the batch in a fixed order: the result is
 // bitwise reproducible. This replaces the ~230 launches per layer of the multi-kernel backward
 // (cnf_train.cpp) — one launch per layer plus the row sum.
 //
@@ -861,35 +861,50 @@ void launch_lds_bwd(const LdsBwdArgs& a, int B, hipStream_t st) {
     hipLaunchKernelGGL(k_lds_bwd, dim3(B, 2), dim3(BWT), a.lds_bytes, st, a);
 }
 
-// dst[net][i] += sum over images b (in order) of part[net][b][i], i < row; lo[net]: the net's first
-// canonical parameter (deterministic: one thread per element, fp64 sum in image order)
-__global__ __launch_bounds__(256) void k_grad_rows(const float* __restrict__ part, int B, int row, int64_t lo0,
-                                                   int64_t lo1, int len0, int len1, float* __restrict__ dparams) {
+// dst[net][i] += sum over images b of part[net][b][i], i < row; lo[net]: the net's first canonical
+// parameter. 32 elements per workgroup, 8 image slices per element (slice s: images s, s + 8, ...,
+// all of them in flight at once up to B = 64), fp64 sums, then a fixed-order LDS sum over the
+// slices: deterministic
+constexpr int GR_EL = 32, GR_SL = 8, GR_U = 8;
+__global__ __launch_bounds__(GR_EL * GR_SL) void k_grad_rows(const float* __restrict__ part, int B, int row, int64_t lo0,
+                                                             int64_t lo1, int len0, int len1, float* __restrict__ dparams) {
+    __shared__ double red[GR_SL][GR_EL];
     const int net = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int el = threadIdx.x & (GR_EL - 1), sl = threadIdx.x / GR_EL;
+    const int i = blockIdx.x * GR_EL + el;
     const int len = net == 0 ? len0 : len1;
-    if (i >= len) return;
     const float* pr = part + (size_t)net * B * row + i;
-    double s = 0.0;
-    int b = 0;
-    for (; b + 4 <= B; b += 4) {
-        const float v0 = pr[(size_t)b * row], v1 = pr[(size_t)(b + 1) * row], v2 = pr[(size_t)(b + 2) * row],
-                    v3 = pr[(size_t)(b + 3) * row];
-        s += v0;
-        s += v1;
-        s += v2;
-        s += v3;
-    }
-    for (; b < B; b++) s += pr[(size_t)b * row];
+    float old = 0.f;
     float* d = dparams + (net == 0 ? lo0 : lo1) + i;
-    *d += (float)s;
+    if (sl == 0 && i < len) old = *d;
+    double s = 0.0;
+    if (i < len) {
+        for (int b0 = sl; b0 < B; b0 += GR_SL * GR_U) {
+            float v[GR_U];
+#pragma unroll
+            for (int u = 0; u < GR_U; u++) {
+                const int b = b0 + GR_SL * u;
+                v[u] = b < B ? pr[(size_t)b * row] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < GR_U; u++) s += (double)v[u];
+        }
+    }
+    red[sl][el] = s;
+    __syncthreads();
+    if (sl == 0 && i < len) {
+        double tot = 0.0;
+#pragma unroll
+        for (int k = 0; k < GR_SL; k++) tot += red[k][el];
+        *d = old + (float)tot;
+    }
 }
 
 void launch_grad_rows(const float* part, int B, int row, int64_t lo0, int64_t lo1, int len0, int len1, float* dparams,
                       hipStream_t st) {
     const int n = len0 > len1 ? len0 : len1;
-    hipLaunchKernelGGL(k_grad_rows, dim3((n + 255) / 256, 2), dim3(256), 0, st, part, B, row, lo0, lo1, len0, len1,
-                       dparams);
+    hipLaunchKernelGGL(k_grad_rows, dim3((n + GR_EL - 1) / GR_EL, 2), dim3(GR_EL * GR_SL), 0, st, part, B, row, lo0, lo1,
+                       len0, len1, dparams);
 }
 
 }  // namespace cnf

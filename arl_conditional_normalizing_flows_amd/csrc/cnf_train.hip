@@ -1280,13 +1280,15 @@ void launch_wgrad(const WGradArgs& a, hipStream_t st) {
         hipLaunchKernelGGL(k_wgrad_band<1>, g, blk, lds, st, a, RB, nunits, wg_abl());
 }
 
-// 64 elements per workgroup, 16 slices of the chunk rows per element (lane / slice), 8 loads in
-// flight per thread, then a fixed-order LDS sum over the slices: deterministic
-__global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__ part, int chunks, long long n,
-                                                       const int64_t* __restrict__ map, float* __restrict__ dparams) {
-    __shared__ double red[16][64];
-    const int t = threadIdx.x, el = t & 63, sl = t >> 6;
-    const long long i = (long long)blockIdx.x * 64 + el;
+// 32 elements per workgroup (one 128-byte line of a partial row per half-wave), 32 slices of the
+// chunk rows per element, every load of a slice in flight at once (<= 8 per thread up to 256 chunks),
+// then a fixed-order LDS sum over the slices: deterministic
+constexpr int GS_EL = 32, GS_SL = 32, GS_U = 8;
+__global__ __launch_bounds__(GS_EL * GS_SL) void k_grad_scatter(const float* __restrict__ part, int chunks, long long n,
+                                                                const int64_t* __restrict__ map, float* __restrict__ dparams) {
+    __shared__ double red[GS_SL][GS_EL];
+    const int t = threadIdx.x, el = t & (GS_EL - 1), sl = t / GS_EL;
+    const long long i = (long long)blockIdx.x * GS_EL + el;
     // the destination and its current value are fetched first, behind the partial-row loads (only this
     // launch writes these parameters' gradients)
     int64_t dst = -1;
@@ -1297,15 +1299,15 @@ __global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__
     }
     double s = 0.0;
     if (i < n) {
-        for (int c0 = sl; c0 < chunks; c0 += 16 * 8) {
-            float v[8];
+        for (int c0 = sl; c0 < chunks; c0 += GS_SL * GS_U) {
+            float v[GS_U];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int c = c0 + 16 * u;
+            for (int u = 0; u < GS_U; u++) {
+                const int c = c0 + GS_SL * u;
                 v[u] = c < chunks ? part[(size_t)c * n + i] : 0.f;
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) s += (double)v[u];
+            for (int u = 0; u < GS_U; u++) s += (double)v[u];
         }
     }
     red[sl][el] = s;
@@ -1313,14 +1315,15 @@ __global__ __launch_bounds__(1024) void k_grad_scatter(const float* __restrict__
     if (sl == 0 && i < n) {
         double tot = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) tot += red[k][el];
+        for (int k = 0; k < GS_SL; k++) tot += red[k][el];
         if (dst >= 0) dparams[dst] = old + (float)tot;
     }
 }
 
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_grad_scatter, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, part, chunks, n, map, dparams);
+    hipLaunchKernelGGL(k_grad_scatter, dim3((unsigned)((n + GS_EL - 1) / GS_EL)), dim3(GS_EL * GS_SL), 0, st, part, chunks, n, map,
+                       dparams);
 }
 
 // ------------------------------------------------------------------------------------------------
