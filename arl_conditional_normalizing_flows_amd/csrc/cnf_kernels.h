@@ -434,10 +434,12 @@ constexpr int LNB_SLICES = 8;
 // order where they are read)
 constexpr int LNB_RS = 8;
 // presum > 0: sums already holds presum partials per image at [b][k] of a [B][pstride][2] array (k_tconv_*
-// fused LN reductions), no k_lnb_reduce
+// fused LN reductions), no k_lnb_reduce. cmod > 0: dxo holds only the channels whose bit is set in
+// cmask (channel = element index % cmod, cmod <= 64); the others are read as 0 whatever dxo holds
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st, int presum = 0, int pstride = 0);
+                        float* scratch, hipStream_t st, int presum = 0, int pstride = 0,
+                        unsigned long long cmask = 0, int cmod = 0);
 // Fused training backward of a k_net_lds layer (cnf_ldsbwd.hip): grid (B, 2 nets), one workgroup per
 // (image, net). Offsets table per net (int32, `offs_per_net` entries): canonical parameter offsets
 // (LN gamma / beta, the net's first parameter, tanh scale or -1) and dense backward-image offsets

@@ -41,6 +41,13 @@ struct LnIn {
     int act = 0;
 };
 
+// CNF_LN2_MASK=0: zero dt1's gradient buffer before the grouped branches' data gradients instead of
+// masking the channels outside their windows in the LN2 backward (A/B; read per call: tests switch it)
+bool ln2_mask() {
+    const char* e = std::getenv("CNF_LN2_MASK");
+    return !(e && std::atoi(e) == 0);
+}
+
 bool fused_lnr() {   // A/B knob: the LN backward's reduction in the producing data-gradient kernel (per call)
     const char* e = std::getenv("CNF_LNR_FUSE");
     return !(e && std::atoi(e) == 0);
@@ -460,10 +467,10 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
 }
 
 void ln_bwd(TExec& E, const float* x, const float* dxo, const LnIn& ln, long long n, float* dx, int accumulate,
-            int64_t g_off, int64_t b_off, int presum = 0) {
+            int64_t g_off, int64_t b_off, int presum = 0, unsigned long long cmask = 0, int cmod = 0) {
     launch_ln_backward(x, dxo, ln.gamma, ln.stats, E.at<double>(E.T.lnsum[E.net]), n, E.B, 1, dx, accumulate,
                        ln.stats ? E.dparams + g_off : nullptr, ln.stats ? E.dparams + b_off : nullptr,
-                       E.at<float>(E.T.lnpart[E.net]), E.st, presum, LNR_MAXPARTS);
+                       E.at<float>(E.T.lnpart[E.net]), E.st, presum, LNR_MAXPARTS, cmask, cmod);
 }
 
 // the plan's side stream and fork / join events (created on first use on the current device)
@@ -727,17 +734,23 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
             ln_bwd(En, T2(n, r), dcb, l3, npx * gc, dt2, 0, rb.ln3g, rb.ln3b, ps);
         } else if (part == 1) {   // grouped dilated branches
             const LnIn l2 = lnin(n, R + 1 + r, rb.ln2g, rb.ln2b);
-            hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
             // the LN2 reduction rides on the branches' data gradients when their windows are pairwise disjoint
             // (the reference group mode's closure windows [(card - 1) w, card w) of each branch width w): each
             // element of dbuf is then final after the one launch that writes it, and each launch adds its
             // window's partials after the previous launches'
             const int nb = (int)c.br.size();
             bool disjoint = true;
-            for (int i = 0; i < nb; i++)
+            unsigned long long wmask = 0;
+            for (int i = 0; i < nb; i++) {
                 for (int j = i + 1; j < nb; j++)
                     disjoint = disjoint && (c.br[i].cin_off + c.br[i].cin <= c.br[j].cin_off ||
                                             c.br[j].cin_off + c.br[j].cin <= c.br[i].cin_off);
+                for (int ch = c.br[i].cin_off; ch < c.br[i].cin_off + c.br[i].cin && ch < 64; ch++) wmask |= 1ull << ch;
+            }
+            // disjoint windows over <= 64 channels: the branches store their windows (no accumulate) and the
+            // LN2 backward reads the channels outside them as 0 (channel mask), so dbuf is not zeroed first
+            const bool masked = disjoint && nk <= 64 && ln2_mask();
+            if (!masked) hchk(hipMemsetAsync(dbuf, 0, (size_t)B * npx * nk * 4, En.st), "hipMemsetAsync");
             int ps = 0;
             bool fused = disjoint;
             for (int bi = 0; bi < nb; bi++) {
@@ -747,13 +760,14 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
                 LnRed r2{T1(n, r), l2.gamma, l2.stats};
                 r2.base = ps;
                 const int np = conv_dgrad(En, h, w, dt2, gc, b.out_off, b.cout, rb.gc[bi], b.cin, b.dil, dbuf, nk,
-                                          b.cin_off, 1, fused ? &r2 : nullptr);
+                                          b.cin_off, masked ? 0 : 1, fused ? &r2 : nullptr);
                 fused = fused && np > 0;
                 ps += np;
             }
             if (!fused) ps = 0;   // (k_lnb_reduce, over whatever partials were written)
             chain_wait(En, ev_ca[n]);
-            ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b, ps);
+            ln_bwd(En, T1(n, r), dbuf, l2, npx * nk, dt1, 0, rb.ln2g, rb.ln2b, ps, masked ? wmask : 0ull,
+                   masked ? nk : 0);
         } else {   // conv_a
             const LnIn l1 = lnin(n, r, rb.ln1g, rb.ln1b);
             ev_ca[n] = conv_wgrad(En, h, w, Y(n, r), nk, 0, nk, l1, dt1, nk, 0, nk, rb.ca, 1);

@@ -1392,8 +1392,11 @@ void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, 
 // per image: sums[b] = (sum g, sum g*xhat), g = dxo * gamma
 __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x, const float* __restrict__ dxo,
                                                     const float* __restrict__ gamma, const float* __restrict__ stats,
-                                                    long long n, double* __restrict__ sums) {
+                                                    long long n, double* __restrict__ sums, unsigned long long cmask,
+                                                    int cmod) {
     __shared__ double red[LNT / 64];
+    // channel mask (cmod > 0): elements of unset channels count as dxo = 0
+    auto live = [&](long long e) { return cmod == 0 || ((cmask >> ((uint32_t)e % (uint32_t)cmod)) & 1ull) != 0; };
     const int b = blockIdx.x, sl = blockIdx.y, RS = gridDim.y;   // slice sl of image b's elements
     const float* xb = x + (size_t)b * n;
     const float* db = dxo + (size_t)b * n;
@@ -1413,6 +1416,10 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
                 xv[u] = ok ? x4[i] : f4{0.f, 0.f, 0.f, 0.f};
                 dv[u] = ok ? d4[i] : f4{0.f, 0.f, 0.f, 0.f};
                 gv[u] = ok ? g4[i] : f4{0.f, 0.f, 0.f, 0.f};
+                if (cmod != 0)
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (!live(4 * i + j)) dv[u][j] = 0.f;
             }
 #pragma unroll
             for (int u = 0; u < 2; u++)
@@ -1428,7 +1435,7 @@ __global__ __launch_bounds__(LNT) void k_lnb_reduce(const float* __restrict__ x,
         const long long q = (n + RS - 1) / RS, lo = sl * q, hi = min(n, lo + q);
         for (long long e = lo + threadIdx.x; e < hi; e += LNT) {
             const float xh = (lrelu(xb[e]) - mu) * rs;
-            const float g = db[e] * gamma[e];
+            const float g = (live(e) ? db[e] : 0.f) * gamma[e];
             sg += g;
             sgh += (double)g * xh;
         }
@@ -1450,7 +1457,7 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
                                                    const double* __restrict__ sums, int rsl, int rstride, long long n,
                                                    int B, int act,
                                                    float* __restrict__ dx, int accumulate, float* __restrict__ gpart,
-                                                   float* __restrict__ bpart) {
+                                                   float* __restrict__ bpart, unsigned long long cmask, int cmod) {
     const long long e0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
     const int S = gridDim.y, sl = blockIdx.y;
     const int bs = (B + S - 1) / S, b_lo = sl * bs, b_hi = min(B, b_lo + bs);
@@ -1485,6 +1492,11 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
         for (int j = 0; j < ne; j++) v[j] = p[i + j];
         return v;
     };
+    // channel mask (cmod > 0): the lane's elements of unset channels are dxo = 0 (not loaded)
+    f4 dm = f4{1.f, 1.f, 1.f, 1.f};
+    if (cmod != 0)
+        for (int j = 0; j < 4; j++) dm[j] = ((cmask >> ((uint32_t)(e0 + j) % (uint32_t)cmod)) & 1ull) ? 1.f : 0.f;
+    const bool dld = dm[0] != 0.f || dm[1] != 0.f || dm[2] != 0.f || dm[3] != 0.f;
     constexpr int U = 4;
     for (int b0 = b_lo; b0 < b_hi; b0 += U) {
         f4 xv[U], d[U], o[U];
@@ -1493,7 +1505,10 @@ __global__ __launch_bounds__(256) void k_lnb_apply(const float* __restrict__ x, 
             const int b = b0 + u;
             const size_t i = (size_t)b * n + e0;
             xv[u] = b < b_hi ? ld4(x, i) : f4{0.f, 0.f, 0.f, 0.f};
-            d[u] = b < b_hi ? ld4(dxo, i) : f4{0.f, 0.f, 0.f, 0.f};
+            d[u] = b < b_hi && dld ? ld4(dxo, i) : f4{0.f, 0.f, 0.f, 0.f};
+            if (cmod != 0)
+#pragma unroll
+                for (int j = 0; j < 4; j++) d[u][j] = dm[j] != 0.f ? d[u][j] : 0.f;
             o[u] = (accumulate && b < b_hi) ? ld4(dx, i) : f4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
@@ -1563,7 +1578,8 @@ __global__ __launch_bounds__(256) void k_lnb_gsum(const float* __restrict__ gpar
 
 void launch_ln_backward(const float* x, const float* dxo, const float* gamma, const float* stats, double* sums,
                         long long n, int B, int act, float* dx, int accumulate, float* dgamma, float* dbeta,
-                        float* scratch, hipStream_t st, int presum, int pstride) {
+                        float* scratch, hipStream_t st, int presum, int pstride, unsigned long long cmask, int cmod) {
+    if (cmod < 0 || cmod > 64) throw std::invalid_argument("launch_ln_backward: channel mask over <= 64 channels");
     // slices per image: at least two full passes of the workgroup each (64 images x 8 slices fill the
     // GPU where one workgroup per image used a quarter of it)
 #ifndef CNF_LNB_RS
@@ -1575,12 +1591,12 @@ void launch_ln_backward(const float* x, const float* dxo, const float* gamma, co
         rsl = presum;
         rstride = pstride > 0 ? pstride : presum;
     } else if (stats)
-        hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums);
+        hipLaunchKernelGGL(k_lnb_reduce, dim3(B, rsl), dim3(LNT), 0, st, x, dxo, gamma, stats, n, sums, cmask, cmod);
     const int S = B < LNB_SLICES ? B : LNB_SLICES;
     float* gpart = scratch;
     float* bpart = scratch + (size_t)LNB_SLICES * n;
     hipLaunchKernelGGL(k_lnb_apply, dim3((unsigned)((n + 1023) / 1024), S), dim3(256), 0, st, x, dxo, gamma, stats,
-                       sums, rsl, rstride, n, B, act, dx, accumulate, gpart, bpart);
+                       sums, rsl, rstride, n, B, act, dx, accumulate, gpart, bpart, cmask, cmod);
     if (stats)
         hipLaunchKernelGGL(k_lnb_gsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gpart, bpart, S, n, dgamma,
                            dbeta);

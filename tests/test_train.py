@@ -160,6 +160,9 @@ GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'in
               # the streamed layers' LN-backward reduction as its own kernel (k_lnb_reduce) instead of fused
               # into the producing data-gradient kernel (CNF_LNR_FUSE=0, read per call)
               ('cfg2', 2, {'_env': {'CNF_LNR_FUSE': '0'}}),
+              # dt1's gradient buffer zeroed before the grouped branches (CNF_LN2_MASK=0) instead of the LN2
+              # backward masking the channels outside the branch windows (read per call)
+              ('cfg2', 2, {'_env': {'CNF_LN2_MASK': '0'}}),
               # the benched training batch (bench.py --mode train): the batch-sliced LN backward (up to 8
               # workgroups per image), the multi-unit band weight gradients and the four-stream schedule
               # all see their full-size partitions only here
