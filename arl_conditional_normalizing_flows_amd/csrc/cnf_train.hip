@@ -613,17 +613,23 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
             const int TH = std::max(1, std::min(a.H, 64 * s / a.W));
             const long long wgs = (long long)((a.H + TH - 1) / TH) * a.B * ((a.N + NS - 1) / NS);
             const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
-            // (measured at cfg2 B=64, 32x32 branch dgrads: SUB=2 at 512 workgroups was slower than 1024
-            // workgroups of one subtile per wave, so wider tiles only when they still leave >= 1024)
+            // (measured at cfg2 B=64, train step, same box: minimum 1024 workgroups 12.17 ms, 512 12.10,
+            // 256 11.79 -- the 32x32 branch dgrads then run SUB=4, 256 workgroups of 8 rows, a quarter of
+            // the per-workgroup weight staging and halo rows)
             static const long long minwg = [] {   // A/B knob
                 const char* e = std::getenv("CNF_TBAND_MINWG");
-                return e ? std::atoll(e) : 1024LL;
+                return e ? std::atoll(e) : 256LL;
             }();
             if (64 * s <= a.H * a.W && wgs >= minwg && band + w1 <= 160 * 1024) sub = s;
         }
         const int TH = std::max(1, std::min(a.H, 64 * sub / a.W));
         const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
-        const int all_taps = band + 9 * w1 <= (sub > 1 ? 156 : 80) * 1024 ? 1 : 0;
+        static const long long at_kb = [] {   // A/B knob: LDS budget (KiB) for staging every tap's weights at once
+            const char* e = std::getenv("CNF_TBAND_ALLTAPS_KB");
+            return e ? std::atoll(e) : -1LL;
+        }();
+        const long long at_lim = at_kb >= 0 ? at_kb : (sub > 1 ? 156 : 80);
+        const int all_taps = (long long)(band + 9 * w1) <= at_lim * 1024 ? 1 : 0;
         const size_t lds = band + (all_taps ? 9 : 1) * w1;
         if (lds <= 160 * 1024) {
             const dim3 g((a.H + TH - 1) / TH, a.B, (a.N + NS - 1) / NS), blk(256);
