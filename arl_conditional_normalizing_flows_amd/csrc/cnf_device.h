@@ -17,8 +17,21 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // data never passes between the waves of a workgroup through these barriers.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops)
-__device__ __forceinline__ float lrelu(float x) { return fmaxf(x, LRELU_ALPHA * x); }
+// LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x (2 VALU ops;
+// fmaxf of a loaded x costs a third, the IEEE-mode canonicalisation v_max_f32 x, x, which the
+// CNF_LRELU_ASM form leaves out: it only quiets signalling NaNs)
+#ifndef CNF_LRELU_ASM
+#define CNF_LRELU_ASM 0
+#endif
+__device__ __forceinline__ float lrelu(float x) {
+#if CNF_LRELU_ASM
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(LRELU_ALPHA * x));
+    return r;
+#else
+    return fmaxf(x, LRELU_ALPHA * x);
+#endif
+}
 
 // n / d for n >= 0, n * d < 2^32 as one multiply-high: m = udiv_magic(d) = ceil(2^32 / d) (0 for d == 1)
 // — the runtime-shape training kernels divide flat indices per element, and the compiler's generic
@@ -179,42 +192,48 @@ __device__ __forceinline__ void ln_wave_final(float n, float m, float M2, float&
     mu = mean;
     rstd = __builtin_amdgcn_rsqf(fmaf(M, iN, LN_EPS));
 }
-// Split form of in_ln for prologues: in_ln_fetch issues the lane's partial-slot load early (with
-// the prologue's other global loads, so they share one memory round trip; valid when the producer
-// wrote at most 64 slots, lanes beyond read nothing), in_ln_finish folds it — the same arithmetic
-// as in_ln, bit for bit.
+// a lane's first partial: its (n, mean, M2) directly (no merge with the empty state, whose
+// n * rcp(n) need not be exactly 1)
+__device__ __forceinline__ void ln_fold_first(const f4 v, float& n, float& m, float& M2) {
+    n = 0.f;
+    m = 0.f;
+    M2 = 0.f;
+    if (v[3] > 0.f) {
+        const float r = v[1] * __builtin_amdgcn_rcpf(v[3]);
+        m = v[0] + r;
+        M2 = fmaxf(fmaf(-v[1], r, v[2]), 0.f);
+        n = v[3];
+    }
+}
+// Split form of in_ln for prologues: in_ln_fetch issues the lane's first partial-slot load early
+// (with the prologue's other global loads, so they share one memory round trip), in_ln_finish folds
+// it and any further slots. in_ln is in_ln_fetch + in_ln_finish, so an image's (mean, rstd) are the
+// same bits whichever form computes them: the form depends on the image's position in its
+// workgroup's image set, i.e. on the batch size (the round-4 batch dependence: ln_fold of the first
+// slot into the empty state and this path contracted differently).
 __device__ __forceinline__ f4 in_ln_fetch(const ConvProb& P, int img) {
     const int lane = threadIdx.x & 63;
     if (P.in_part == nullptr || lane >= P.in_nparts) return f4{0.f, 0.f, 0.f, 0.f};
     return *reinterpret_cast<const f4*>(P.in_part + ((size_t)img * P.part_stride + lane) * LNP);
 }
-__device__ __forceinline__ void in_ln_finish(const ConvProb& P, const f4 v, float& mu, float& rstd) {
+__device__ __forceinline__ void in_ln_finish(const ConvProb& P, int img, const f4 v, float& mu, float& rstd) {
     mu = 0.f;
     rstd = 1.f;
     if (P.in_part == nullptr) return;
 #ifdef CNF_ABL_NOINLN
     return;
 #endif
-    float n = 0.f, m = 0.f, M2 = 0.f;
-    ln_fold(v, n, m, M2);
-    ln_wave_final(n, m, M2, mu, rstd);
-}
-
-__device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
-    mu = 0.f;
-    rstd = 1.f;
-    if (P.in_part == nullptr) return;
-#ifdef CNF_ABL_NOINLN
-    return;
-#endif
-    const int lane = threadIdx.x & 63;
+    float n, m, M2;
+    ln_fold_first(v, n, m, M2);
     const float* __restrict__ q = P.in_part + (size_t)img * P.part_stride * LNP;
-    float n = 0.f, m = 0.f, M2 = 0.f;
-    for (int i = lane; i < P.in_nparts; i += 64) {
-        const f4 v = *reinterpret_cast<const f4*>(q + (size_t)LNP * i);
-        ln_fold(v, n, m, M2);
+    for (int i = (threadIdx.x & 63) + 64; i < P.in_nparts; i += 64) {
+        const f4 w = *reinterpret_cast<const f4*>(q + (size_t)LNP * i);
+        ln_fold(w, n, m, M2);
     }
     ln_wave_final(n, m, M2, mu, rstd);
+}
+__device__ __forceinline__ void in_ln(const ConvProb& P, int img, float& mu, float& rstd) {
+    in_ln_finish(P, img, in_ln_fetch(P, img), mu, rstd);
 }
 
 // Copy n floats (n % 4 == 0, both 16-byte aligned) global -> LDS; 8 float4 loads in flight per thread.

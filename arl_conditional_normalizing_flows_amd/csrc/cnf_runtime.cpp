@@ -811,14 +811,17 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + rb.ln1g : none,
                                       ln ? P + rb.ln1b : none, 1, X + rb.ca.w, X + rb.ca.b, t1[n], c.t1_cs, 0, c.nk,
                                       none, out_slab(n, 1, 4 * nt1), 0, 1});
-                // training: the full t1_r for the backward's LN2 from the same launch (k_pw's second store)
-                if (ss != nullptr) pr.back().out2 = ST1(n, r);
+                // training: the full t1_r for the backward's LN2 from the same launch (k_pw's second
+                // store; its dual-store instantiations exist for LN on only -- without LN the separate
+                // launch below writes it)
+                if (ss != nullptr && ln) pr.back().out2 = ST1(n, r);
             }
             // only the channels the branches read are stored (into their consumers' sub-tensors when
             // t1_compact); the LN2 statistics still cover all nk channels
             const int* t1map = c.t1_compact ? E.p.dtab(c.dev_t1_map) : nullptr;
             bool dual = false;
             set_parts(1, conv_launch(E, 1, ROLE_CONV_A, c.hc, c.wc, pr, c.t1_used, nullptr, t1map, nullptr, &dual));
+            dual = dual && ln;   // (out2 is set with LN only: without it k_pw made no second store)
             if (ss != nullptr && dual) save_stats(1, c.R + 1 + r);
             if (ss != nullptr && !dual) {
                 // the full t1_r for the backward's LN2 (the compact t1 above holds only the branch windows)

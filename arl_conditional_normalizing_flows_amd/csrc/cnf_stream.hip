@@ -56,6 +56,9 @@ int read_pw_stamps(long long* host) {
 #ifndef CNF_PW_EARLY
 #define CNF_PW_EARLY 0
 #endif
+#ifndef CNF_PW_BQD
+#define CNF_PW_BQD 1   // B-quad read distance in groups (specialised k_pw)
+#endif
 constexpr int pw_depth(int gm, bool res) { return res ? 1 : gm <= 4 ? CNF_PW_DEPTH : (CNF_PW_DEPTH < 2 ? CNF_PW_DEPTH : 2); }
 
 // DUAL (generic non-tap instantiations of the training forward only): every output element is also
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 
     // the first image of this wave's LN-statistics share: its partial slots fetched now, in the same
     // memory round trip as the loads above and the weights below (folded after the weight copy)
-    const bool lnpre = LN && wave < nimg && P.in_nparts <= 64;
+    const bool lnpre = LN && wave < nimg;
     const f4 slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
     // the rest of the ring's first images: in flight with the prologue's loads (CNF_PW_EARLY) or
     // issued once the weights are in LDS
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         for (int i = wave; i < nimg; i += NW) {
             float mu, rs;
             if (i == wave && lnpre)
-                in_ln_finish(P, slot0, mu, rs);
+                in_ln_finish(P, img0 + i, slot0, mu, rs);
             else
                 in_ln(P, img0 + i, mu, rs);
             if (lane == 0) {
@@ -273,9 +276,16 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         // compiler from hoisting every group's LDS reads (NR quads each) into live registers
         // (the generic instantiations keep the plain per-group loop: their runtime group bound already
         // limits the hoisting, and the extra buffer costs them registers)
-        f4 bq[2][NR];
+        // B quads of the specialised instantiations in a ring of BQD + 1 groups, read BQD groups ahead
+        // (the scheduler sinks a group's reads to the previous group's last MFMA: at distance 1 the LDS
+        // latency is exposed once per group)
+        constexpr int BQD = CNF_PW_BQD;
+        f4 bq[BQD + 1][NR];
 #pragma unroll
-        for (int n = 0; n < NR; n++) bq[0][n] = *reinterpret_cast<const f4*>(brow + n * 64);
+        for (int j = 0; j < BQD; j++)
+            if (j < GM && (SID >= 0 || j == 0))
+#pragma unroll
+                for (int n = 0; n < NR; n++) bq[j][n] = *reinterpret_cast<const f4*>(brow + (size_t)j * 4 * NSJ * 4 + n * 64);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
             if (SID < 0 && g < G) {
@@ -288,15 +298,16 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
                     for (int n = 0; n < NR; n++)
                         acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bp[n][s], acc[n], 0, 0, 0);
             } else if (SID >= 0 && g < G) {
-                if (g + 1 < GM && g + 1 < G)
+                if (g + BQD < GM && g + BQD < G)
 #pragma unroll
                     for (int n = 0; n < NR; n++)
-                        bq[(g + 1) & 1][n] = *reinterpret_cast<const f4*>(brow + (size_t)(g + 1) * 4 * NSJ * 4 + n * 64);
+                        bq[(g + BQD) % (BQD + 1)][n] =
+                            *reinterpret_cast<const f4*>(brow + (size_t)(g + BQD) * 4 * NSJ * 4 + n * 64);
 #pragma unroll
                 for (int s = 0; s < 4; s++)
 #pragma unroll
                     for (int n = 0; n < NR; n++)
-                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bq[g & 1][n][s], acc[n], 0, 0, 0);
+                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bq[g % (BQD + 1)][n][s], acc[n], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -698,7 +709,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     lnP.in_part = a.in_part[net];
     lnP.in_nparts = a.in_nparts;
     lnP.part_stride = a.part_stride;
-    const bool lnpre = ln && wave < nimg && a.in_nparts <= 64;
+    const bool lnpre = ln && wave < nimg;
     const f4 slot0 = lnpre ? in_ln_fetch(lnP, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
     // packed weights and quad-offset tables of every branch (once per workgroup)
     for (int bi = 0; bi < GS(nbr); bi++) {
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
         for (int i = wave; i < nimg; i += GC_NW) {
             float mu, rs;
             if (i == wave && lnpre)
-                in_ln_finish(lnP, slot0, mu, rs);
+                in_ln_finish(lnP, img0 + i, slot0, mu, rs);
             else
                 in_ln(lnP, img0 + i, mu, rs);
             if (lane == 0) {

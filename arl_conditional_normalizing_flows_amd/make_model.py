@@ -578,18 +578,33 @@ class cFlow:
         default = '1' if dist is not None and dist.get_backend(grp) == 'nccl' else '0'
         overlap = dist is not None and os.environ.get('CNF_GRAD_OVERLAP', default) != '0'
         works = []
+        errors = []
+        reported = []
         if overlap:
             ranges = self._coupling_param_ranges()
             grads = self._grads
 
             def done(_user, ci):
-                lo, hi = ranges[ci]
-                works.append(dist.all_reduce(grads[lo:hi], group=grp, async_op=True))
+                # an exception must not escape into C (ctypes would print it and return, and this rank
+                # would silently skip the layer's all-reduce while the other ranks pair it with the next)
+                try:
+                    reported.append(ci)
+                    lo, hi = ranges[ci]
+                    works.append(dist.all_reduce(grads[lo:hi], group=grp, async_op=True))
+                except BaseException as e:   # noqa: BLE001 -- re-raised below
+                    errors.append(e)
             cb = _lib.LAYER_DONE_FN(done)
         else:
             cb = _lib.LAYER_DONE_FN()
         check(lib.cnf_flow_backward_ex(self._plan, ptr(self.params), ptr(xy), ptr(zy), ptr(ws), B, ptr(buf) + 16,
                                        ptr(self._grads), cb, None, _stream()), 'cnf_flow_backward_ex')
+        if overlap and not errors and sorted(reported) != sorted(self._coupling_param_ranges()):
+            errors.append(RuntimeError(f'layer_done reported couplings {sorted(reported)}, expected each of '
+                                       f'{sorted(self._coupling_param_ranges())} once'))
+        if errors:
+            # this rank's collective sequence no longer matches the other ranks': raised before any wait
+            # (a wait could hang); the caller decides whether to abort the process group
+            raise RuntimeError('per-layer gradient all-reduce failed') from errors[0]
         for w in works:
             w.wait()
         if dist is not None and not overlap:

@@ -1,6 +1,6 @@
 """Diagnostic (not a test): per-phase clock stamps of the fused LDS backward (k_lds_bwd) of the last
 launched LDS layer (coupling 0 of cfg2) at the bench batch. Run on a GPU box:
-    CNF_LDSBWD_STAMPS=1 python tests/diag_bwd_stamps.py"""
+    CNF_LDSBWD_STAMPS=1 python profiles/diag/diag_bwd_stamps.py"""
 import ctypes as C
 import os
 import sys
@@ -8,7 +8,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
 from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 from arl_conditional_normalizing_flows_amd.make_model import cFlow  # noqa: E402

@@ -1,6 +1,6 @@
 """Diagnostic (not a test): phase stamps of workgroup (0, 0) of every k_gc launch of one forward
 (s_memrealtime, 100 MHz), from a CNF_EXTRA_FLAGS=-DCNF_GC_STAMPS build loaded through CNF_LIB.
-Run on a GPU box: CNF_LIB=.../var_gcst.so python tests/diag_gc_stamps.py [config] [batch]"""
+Run on a GPU box: CNF_LIB=.../var_gcst.so python profiles/diag/diag_gc_stamps.py [config] [batch]"""
 import ctypes as C
 import os
 import sys
@@ -8,7 +8,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
 from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 from arl_conditional_normalizing_flows_amd.make_model import cFlow  # noqa: E402

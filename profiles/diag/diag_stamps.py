@@ -1,5 +1,5 @@
 """Diagnostic (not a test): per-phase timing of k_net_lds from barrier-free shader-clock stamps
-(wave 0 of workgroup (0, 0)). Run on a GPU box: CNF_STAMPS=1 python tests/diag_stamps.py"""
+(wave 0 of workgroup (0, 0)). Run on a GPU box: CNF_STAMPS=1 python profiles/diag/diag_stamps.py"""
 import ctypes as C
 import os
 import sys
@@ -7,7 +7,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from arl_conditional_normalizing_flows_amd import _lib  # noqa: E402
 from arl_conditional_normalizing_flows_amd.config import PRESETS  # noqa: E402
 from arl_conditional_normalizing_flows_amd.make_model import cFlow  # noqa: E402

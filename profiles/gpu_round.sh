@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box session: parity tests, bench line, rocprofv3 kernel-trace summary of the same bench.
-# usage (from repo root, on the GPU box): bash tests/gpu_round.sh TAG [pytest -k expr]
+# usage (from repo root, on the GPU box): bash profiles/gpu_round.sh TAG [pytest -k expr]
 set -o pipefail
 tag=${1:-run}
 out=gpurun_out/$tag

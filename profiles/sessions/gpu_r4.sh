@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4 GPU session: risky new shapes first (own short limit), then the whole GPU suite, then the bench
-# usage (repo root, GPU box): bash tests/gpu_r4.sh TAG [pytest -k expr for the first step]
+# usage (repo root, GPU box): bash profiles/sessions/gpu_r4.sh TAG [pytest -k expr for the first step]
 set -o pipefail
 tag=${1:-r4}
 out=gpurun_out/$tag

@@ -1,5 +1,5 @@
 #!/bin/bash
-# per-kernel stats of the training step under environment variants:  bash tests/gpu_r4_abl.sh TAG "ENV=.." ...
+# per-kernel stats of the training step under environment variants:  bash profiles/sessions/gpu_r4_abl.sh TAG "ENV=.." ...
 set -o pipefail
 tag=$1; shift
 root=$PWD

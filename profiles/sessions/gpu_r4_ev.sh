@@ -1,6 +1,6 @@
 #!/bin/bash
 # training-step stream check: train bench, the per-layer step profile (queue overlap per layer), and the
-# 2-rank gloo rehearsal with and without the overlapped all-reduce.   bash tests/gpu_r4_ev.sh TAG
+# 2-rank gloo rehearsal with and without the overlapped all-reduce.   bash profiles/sessions/gpu_r4_ev.sh TAG
 set -o pipefail
 tag=${1:-r4ev}
 out=gpurun_out/$tag

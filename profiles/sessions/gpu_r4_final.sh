@@ -1,9 +1,9 @@
 #!/bin/bash
 # round-4 closing call: the GPU suite, the three bench lines, the training step's kernel stats and per-layer
-# fold.   bash tests/gpu_r4_final.sh TAG
+# fold.   bash profiles/sessions/gpu_r4_final.sh TAG
 set -o pipefail
 tag=${1:-r4f}
-bash tests/gpu_r4.sh $tag || exit 1
+bash profiles/sessions/gpu_r4.sh $tag || exit 1
 root=$PWD
 out=$root/gpurun_out/${tag}_prof
 mkdir -p $out

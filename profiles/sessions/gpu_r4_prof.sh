@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 profile call: kernel stats + PMC passes + training stats (profiles/collect.sh), the
 # per-GPU-batch anchors with their rocprof stats, then a 2-rank rehearsal of the training bench on
-# one GPU (gloo).   bash tests/gpu_r4_prof.sh TAG
+# one GPU (gloo).   bash profiles/sessions/gpu_r4_prof.sh TAG
 set -o pipefail
 tag=${1:-r04}
 root=$PWD

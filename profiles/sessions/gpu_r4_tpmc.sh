@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the training step (each its own run, --kernel-trace only):  bash tests/gpu_r4_tpmc.sh TAG
+# PMC passes over the training step (each its own run, --kernel-trace only):  bash profiles/sessions/gpu_r4_tpmc.sh TAG
 set -o pipefail
 tag=${1:-r4tpmc}
 root=$PWD

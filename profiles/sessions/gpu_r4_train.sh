@@ -1,6 +1,6 @@
 #!/bin/bash
 # training-path GPU session: gradient parity (fused LDS backward and the multi-kernel one), the
-# training bench, the host-enqueue diagnostic.   bash tests/gpu_r4_train.sh TAG
+# training bench, the host-enqueue diagnostic.   bash profiles/sessions/gpu_r4_train.sh TAG
 set -o pipefail
 tag=${1:-r4tr}
 out=gpurun_out/$tag

@@ -168,3 +168,64 @@ def test_gloo_world2_overlapped_gradient_allreduce(gpu, tmp_path, G):
     print(f'G={G}: sharded vs whole-batch gradient max abs diff {err:.2e} (max |g| {np.max(np.abs(g1)):.2e})')
     assert err <= 1e-5 * np.max(np.abs(g1))
     assert np.allclose(t[0, 1], torch.stack(t1).cpu().numpy(), rtol=1e-5, atol=1e-4)
+
+
+def test_layer_done_orders_every_gradient_write(gpu):
+    """cnf_flow_backward_ex's layer_done contract (include/cnf.h): when coupling c is reported,
+    every kernel writing c's gradient range is ordered on the caller's stream before that point.
+    The callback records an event on the caller's stream and, on a side stream ordered ONLY by
+    that event, snapshots the range and then poisons it with NaN. If a kernel writing the range
+    were still unordered, its result would be missing from the snapshot (snapshot != the plain
+    backward's gradient) or would land after the poison (a non-NaN left in the range). This is the
+    ordering the RCCL overlap (cFlow.gradients on 'nccl') relies on; one GPU suffices. cfg2 B=8
+    covers the streamed layers (four streams), the split LDS backward (weight gradients on a side
+    stream, reported two layers late) and the LDS layers."""
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow, _stream
+    from arl_conditional_normalizing_flows_amd.distributed import pack_nll_sums
+    cfg = PRESETS['cfg2']
+    kw = cfg.kwargs()
+    flow = cFlow(**kw, device=gpu)
+    flow.set_weights(OracleCFlow(**kw).init_params(4))
+    H, W, _ = cfg.io_shape
+    B = 8
+    x = torch.from_numpy(synthetic_class_batch(B, H, W, cfg.x_d, seed=12)).to(gpu)
+    g_ref = flow.gradients(x)[0].clone()
+    torch.cuda.synchronize()
+
+    lib = _lib.load()
+    ranges = flow._coupling_param_ranges()
+    ws = flow._train_workspace(B)
+    zy = torch.empty_like(x)
+    ld = torch.empty(B, device=gpu, dtype=torch.float32)
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream(device=gpu)
+    _lib.check(lib.cnf_flow_forward_train(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(), x.data_ptr(),
+                                          zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, _stream()), 'forward_train')
+    sums, _ = flow.nll_sums(x, zy, ld)
+    buf = pack_nll_sums(sums, B)
+    grads = torch.full((flow.num_params,), 7.0, device=gpu)
+    snap = torch.full_like(grads, 3.0)
+    reported, errors, events = [], [], []
+
+    def done(_user, ci):
+        try:
+            reported.append(ci)
+            lo, hi = ranges[ci]
+            ev = torch.cuda.Event()
+            ev.record(main)
+            events.append(ev)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                snap[lo:hi].copy_(grads[lo:hi])
+                grads[lo:hi].fill_(float('nan'))
+        except BaseException as e:   # noqa: BLE001
+            errors.append(e)
+    cb = _lib.LAYER_DONE_FN(done)
+    _lib.check(lib.cnf_flow_backward_ex(flow._plan, flow.params.data_ptr(), x.data_ptr(), zy.data_ptr(),
+                                        ws.data_ptr(), B, buf.data_ptr() + 16, grads.data_ptr(), cb, None,
+                                        _stream()), 'backward_ex')
+    torch.cuda.synchronize()
+    assert not errors, errors
+    assert sorted(reported) == sorted(ranges), reported
+    assert torch.equal(snap, g_ref), 'a gradient write was not ordered before its layer_done'
+    assert torch.isnan(grads).all(), 'a gradient write landed after its layer_done'

@@ -144,6 +144,8 @@ def _gpu_flow(kw, P, gpu):
 
 GRAD_CASES = [('tiny', 2, {}), ('small', 3, {}), ('small', 2, {'group_mode': 'intended'}),
               ('tiny', 2, {'LAYER_NORM': False}), ('cfg2', 2, {}),
+              # no LayerNorm on streamed (not LDS-resident) layers: conv_a's saved t1 by its own launch
+              ('cfg2', 2, {'LAYER_NORM': False}),
               # couplings 2 and 1 pixels wide: the weight gradients fall back to the VALU k_wgrad
               ('narrow', 3, {}),
               # every training convolution on the VALU kernels (k_tconv, k_wgrad; CNF_TRAIN_VALU=1, read per call)
@@ -210,8 +212,11 @@ def test_gradients_match_oracle(gpu, name, B, extra):
         for k in env:
             os.environ.pop(k, None)
     terms = [float(t) for t in terms]
+    # the north-star bound of the forward parity tests (test_gpu_parity.test_nll_matches_oracle): 1e-5 of
+    # max(|ref|, mean over images of sum|s|) -- the log-det terms' conditioning scale
+    _, _, abs_s = ora.forward(np.asarray(xy, np.float64), P, abs_s=True)
     for r, t in zip(terms_ref, terms):
-        assert abs(r - t) <= 1e-5 * max(1.0, abs(r)) * 10, (terms_ref, terms)
+        assert abs(r - t) <= 1e-5 * max(abs(r), float(np.mean(abs_s))), (terms_ref, terms)
     gmax = max(float(np.max(np.abs(v))) for v in G_ref.values())
     worst = (0.0, '')
     bad = []
