@@ -84,6 +84,9 @@ struct ConvArgs {
     // umask < 0: the source is a plain NHWC tensor of the conv's own H x W (uD channels per pixel,
     // taps from channel uoff, dilation udil; LN / LeakyReLU on load as the problem says)
     int udil, uoff;
+    // k_pw shared-tile mode (CNF_PW_SH builds): PW_NS image streams of 4 waves share one workgroup, its
+    // weights and the tile's LN gamma/beta (in LDS at byte gb_off); 0: plain
+    int sh, gb_off;
 };
 
 struct CoupArgs {
@@ -303,7 +306,9 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvA
 }
 void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 int pw_num_shapes();
-int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS): [4 workgroups][16]   // shape-specialised k_pw instantiations compiled in
+bool pw_shared_tile();   // built with the shared-tile k_pw mode (CNF_PW_SH)
+int pw_streams();        // its image streams per workgroup
+int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS=SID): [2048 workgroups][12]   // shape-specialised k_pw instantiations compiled in
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);

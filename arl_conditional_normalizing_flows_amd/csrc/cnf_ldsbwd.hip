@@ -31,7 +31,7 @@ namespace {
 constexpr int BWN = 8;          // waves per workgroup
 constexpr int BWT = BWN * 64;   // threads
 
-__device__ __forceinline__ float lrelu_b(float x) { return fmaxf(x, LRELU_ALPHA * x); }
+__device__ __forceinline__ float lrelu_b(float x) { return lrelu(x); }   // (cnf_device.h)
 __device__ __forceinline__ float lrelu_d(float x) { return x > 0.f ? 1.f : LRELU_ALPHA; }
 
 // k-table entry of a flat reduction index k = tap * cpt + c: (dr + 64) | (dc + 64) << 7 | c << 14,

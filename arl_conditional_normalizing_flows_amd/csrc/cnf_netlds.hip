@@ -43,7 +43,7 @@ constexpr int NT = NW * 64;         // threads
 #endif
 
 // LeakyReLU(0.3) as max(x, 0.3x) (2 VALU ops; equal to the select form for every finite x)
-__device__ __forceinline__ float lrelu_(float x) { return __builtin_fmaxf(x, LRELU_ALPHA * x); }
+__device__ __forceinline__ float lrelu_(float x) { return lrelu(x); }   // (cnf_device.h)
 
 __device__ __forceinline__ float wsum_f(float v) { return wave_sum_f(v); }   // DPP (cnf_device.h)
 __device__ __forceinline__ double wsum_d(double v) {

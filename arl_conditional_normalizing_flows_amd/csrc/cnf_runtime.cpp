@@ -415,12 +415,27 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         a.tiles_per_img = tiles;
         for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = probs[i].out_part_base;
         const int64_t units = (int64_t)tiles * a.nprob * E.B;
-        a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+        const bool lnf = probs[0].in_st.part != nullptr;
+        // shared-tile mode (CNF_PW_SH builds; CNF_PW_SH=0 at run time: off): one workgroup per CU,
+        // pw_streams() images of the tile at a time, gamma / beta staged once in LDS behind the weights
+        a.sh = pw_shared_tile() && lnf && tap == nullptr && a.p[0].out2 == nullptr && !(std::getenv("CNF_PW_SH") &&
+               std::atoi(std::getenv("CNF_PW_SH")) == 0) ? 1 : 0;
+        int ilds_pw = ilds;
+        if (a.sh) {
+            const int ns = pw_streams();
+            a.ipw = (int)std::min<int64_t>(32, std::max<int64_t>(ns, (units + 255) / 256));
+            a.gb_off = (int)align_up(lds, 16);
+            ilds_pw = a.gb_off + pw_gm * 4 * 64 * 16 * 2;
+            if (ilds_pw > 160 * 1024) {   // gamma / beta do not fit beside the weights: plain mode
+                a.sh = 0;
+                ilds_pw = ilds;
+            }
+        }
+        if (!a.sh) a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
         if (const char* e = std::getenv(resf ? "CNF_PW_IPW_RES" : "CNF_PW_IPW"))   // tuning override
-            a.ipw = std::max(1, std::min(16, std::atoi(e)));
+            a.ipw = std::max(1, std::min(a.sh ? 32 : 16, std::atoi(e)));
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
-        const bool lnf = probs[0].in_st.part != nullptr;
         const bool tapf = tap != nullptr;
         if (tap) {
             a.umask = tap->mask;
@@ -441,8 +456,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         }
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
                            role_name(role) + ">";
-        E.record(name, flops, bytes, [nr, gm, lnf, resf, tapf, a, grid_x, ilds](void* st) {
-            launch_pw(nr, gm, lnf, resf, tapf, a, grid_x, ilds, (hipStream_t)st);
+        E.record(name, flops, bytes, [nr, gm, lnf, resf, tapf, a, grid_x, ilds_pw](void* st) {
+            launch_pw(nr, gm, lnf, resf, tapf, a, grid_x, ilds_pw, (hipStream_t)st);
         });
         return nw * tiles;
     } else {

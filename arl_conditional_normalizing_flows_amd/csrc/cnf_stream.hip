@@ -30,14 +30,17 @@ constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
 #define PP(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : P.f)
 #define PA(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : a.f)
-__device__ long long g_pw_stamps[4][16];
+// diagnostic per-workgroup stamps (CNF_PW_STAMPS=SID builds only; never in timed runs): thread 0 of
+// every workgroup of the instantiation SID records s_memrealtime at its start (0), before (1) and
+// after (2) the prologue barrier and after each of its images (3 + i)
+constexpr int PW_ST_WG = 2048, PW_ST_N = 12;
+__device__ long long g_pw_stamps[PW_ST_WG][PW_ST_N];
 #ifdef CNF_PW_STAMPS
 #define PWSTAMP(i)                                                                                       \
     do {                                                                                                 \
-        if (SID >= 0 && SID < 2 && threadIdx.x == 0 && blockIdx.y == 0 &&                                \
-            (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))                                            \
-            g_pw_stamps[2 * (SID >= 0 ? SID : 0) + (blockIdx.x == 0 ? 0 : 1)][(i)] =                     \
-                (long long)__builtin_amdgcn_s_memrealtime();                                             \
+        if (SID == CNF_PW_STAMPS && threadIdx.x == 0 && (i) < PW_ST_N &&                                 \
+            blockIdx.y * gridDim.x + blockIdx.x < PW_ST_WG)                                              \
+            g_pw_stamps[blockIdx.y * gridDim.x + blockIdx.x][(i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define PWSTAMP(i) do { } while (0)
@@ -63,10 +66,22 @@ constexpr int pw_depth(int gm, bool res) { return res ? 1 : gm <= 4 ? CNF_PW_DEP
 
 // DUAL (generic non-tap instantiations of the training forward only): every output element is also
 // stored densely ([HW][cout]) to P.out2 -- conv_a's full t1 saved for the backward in the same launch
-template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false>
-__global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
+//
+// SH (shared-tile mode, CNF_PW_SH builds, LN on load, not tap mode): NS = PW_NS image streams of NW
+// waves share the workgroup -- wave w computes pixel subtile w % NW of images ii = w / NW, + NS, ...
+// -- and the tile's LN gamma / beta live once in LDS instead of in every wave's registers: half the
+// prologue bytes per CU (one workgroup per CU loads the weights and gamma/beta once for NS x the
+// images) and 56 fewer VGPRs at conv_b. The LN partial slots stay per (tile, subtile): bitwise the
+// plain mode's partition.
+#ifndef PW_NS
+#define PW_NS 2
+#endif
+template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false, bool SH = false>
+__global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
+    constexpr int NS = SH ? PW_NS : 1;
+    static_assert(!SH || (LN && !TAP && !DUAL), "shared-tile k_pw: LN on load, no tap mode, no dual store");
     PWSTAMP(0);
     const ConvProb P = a.p[blockIdx.y];
     const int HW = PA(H) * PA(W);
@@ -74,9 +89,11 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     const int img0 = (blockIdx.x / PA(tiles_per_img)) * a.ipw;
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = SH ? wave % NW : wave, strm = SH ? wave / NW : 0;   // pixel subtile, image stream
     const int i16 = lane & 15, kq = lane >> 4;
     const int cin = PP(cin), G = (cin + 15) >> 4, cout = PP(cout);
     constexpr int NSJ = 16 * NR;
+    f4* lgb = reinterpret_cast<f4*>(smem + a.gb_off);   // SH: gamma [GM][NW][64] then beta
     float* lw = reinterpret_cast<float*>(smem + PP(lds_w_off));
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
@@ -92,7 +109,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // are evaluated per element from shape fields (folded to constants in the specialised
     // instantiations, whose offsets then become lane base + immediate)
     const bool full_px = HW % (16 * NW) == 0;
-    const int pa = tile * (16 * NW) + wave * 16 + i16;
+    const int pa = tile * (16 * NW) + sub * 16 + i16;
     const bool pav = full_px || pa < HW;
     const uint32_t aoff = ((uint32_t)pa * PP(in_cs) + PP(in_off) + 4 * kq) * 4u;
     // mapped input (conv_b over a t2 split into its producers' sub-tensors): quad 4g + kq of the
@@ -106,7 +123,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     auto aoffg = [&](int g) -> uint32_t { return PP(in_mapped) ? amap[g] : aoff + 64u * g; };
     auto gok = [&](int g) { return pav && g < G && (cin % 16 == 0 || 16 * g + 4 * kq < cin); };
     // output: acc[n][r] = out[pixel po0 + r][channel 16n + i16]
-    const int po0 = tile * (16 * NW) + wave * 16 + kq * 4;
+    const int po0 = tile * (16 * NW) + sub * 16 + kq * 4;
     const uint32_t obase = ((uint32_t)po0 * PP(out_cs) + PP(out_off) + i16) * 4u;
     const bool all_st = PP(st_mask_lo) == ~0u && PP(st_mask_hi) == ~0u;
     auto chv = [&](int n) { return cout % 16 == 0 || n * 16 + i16 < cout; };
@@ -177,9 +194,15 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
                 }
         }
     };
-    load_img(0, x[0], rv[0]);
+    if (strm < nimg) load_img(strm, x[0], rv[0]);
     f4 gm[GM], bt[GM];
-    if (LN) {
+    if (SH) {   // stream 0 stages gamma, stream 1 beta (NS >= 2), each for its subtile's lanes
+        if (strm < 2) {
+            const auto rg = buf_rsrc(strm == 0 ? P.gamma : P.beta, in_img);
+#pragma unroll
+            for (int g = 0; g < GM; g++) gm[g] = buf_load4(rg, gok(g) ? aoffg(g) : BUF_OOB);
+        }
+    } else if (LN) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
@@ -209,7 +232,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 
     // the first image of this wave's LN-statistics share: its partial slots fetched now, in the same
     // memory round trip as the loads above and the weights below (folded after the weight copy)
-    const bool lnpre = LN && wave < nimg;
+    const bool lnpre = LN && wave < nimg;   // (image wave: the LN table below is per workgroup)
     const f4 slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
     // the rest of the ring's first images: in flight with the prologue's loads (CNF_PW_EARLY) or
     // issued once the weights are in LDS
@@ -221,9 +244,13 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
     int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
     asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
-    copy_to_lds<64 * NW>(P.wt, lw, nwf);
+    copy_to_lds<64 * NW * NS>(P.wt, lw, nwf);
+    if (SH && strm < 2) {
+#pragma unroll
+        for (int g = 0; g < GM; g++) lgb[((strm * GM + g) * NW + sub) * 64 + lane] = gm[g];
+    }
     if (LN) {
-        for (int i = wave; i < nimg; i += NW) {
+        for (int i = wave; i < nimg; i += NW * NS) {
             float mu, rs;
             if (i == wave && lnpre)
                 in_ln_finish(P, img0 + i, slot0, mu, rs);
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     if (!CNF_PW_EARLY) {
 #pragma unroll
         for (int j = 1; j < D; j++)
-            if (j < nimg) load_img(j, x[j], rv[j]);
+            if (strm + j * NS < nimg) load_img(strm + j * NS, x[j], rv[j]);
     }
 
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
@@ -253,6 +280,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         float av[GM][4];
 #pragma unroll
         for (int g = 0; g < GM; g++) {
+            if (SH) {
+                gm[g] = lgb[(g * NW + sub) * 64 + lane];
+                bt[g] = lgb[((GM + g) * NW + sub) * 64 + lane];
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float v = !TAP || P.act ? lrelu(xc[g][j]) : xc[g][j];   // conv_in reads raw u
@@ -334,14 +365,16 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
             }
         if (P.out_part != nullptr)
             ln_partial(vals, valid,
-                       P.out_part + ((size_t)img * PP(part_stride) + P.out_part_base + tile * NW + wave) * LNP);
+                       P.out_part + ((size_t)img * PP(part_stride) + P.out_part_base + tile * NW + sub) * LNP);
     };
-    for (int i0 = 0; i0 < nimg; i0 += D) {
+    // this wave's images strm, strm + NS, ... in a ring of D buffers
+    for (int i0 = strm; i0 < nimg; i0 += D * NS) {
 #pragma unroll
         for (int j = 0; j < D; j++) {
-            if (i0 + j >= nimg) break;
-            step(i0 + j, x[j], rv[j], i0 + j + D);   // buffer j then receives image i0 + j + D
-            PWSTAMP(3 + i0 + j);
+            const int ii = i0 + j * NS;
+            if (ii >= nimg) break;
+            step(ii, x[j], rv[j], ii + D * NS);   // buffer j then receives image ii + D * NS
+            PWSTAMP(3 + ii);
         }
     }
 }
@@ -349,11 +382,26 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 #undef PP
 #undef PA
 
+#ifndef CNF_PW_SH
+#define CNF_PW_SH 0
+#endif
+bool pw_shared_tile() { return CNF_PW_SH != 0; }
+int pw_streams() { return PW_NS; }
+
 template <int S>
 bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStream_t st) {
     if constexpr (S < CNF_PW_NSHAPES) {
         if (sid == S) {
             constexpr PwShape k = kPwShapes[S];
+#if CNF_PW_SH
+            if constexpr (k.ln != 0 && k.tap == 0) {
+                if (a.sh) {
+                    CNF_LAUNCH((k_pw<k.nr, k.gm, true, k.res != 0, S, false, false, true>), g, dim3(64 * PW_NW * PW_NS),
+                               lds, st, a);
+                    return true;
+                }
+            }
+#endif
             CNF_LAUNCH((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S, k.tap != 0>), g, b, lds, st, a);
             return true;
         }
@@ -402,6 +450,22 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
 #undef CNF_PW_TCASE
         throw std::invalid_argument("k_pw tap mode: no instantiation for this shape");
     }
+#if CNF_PW_SH
+    if (a.sh) {   // shared-tile generic instantiations
+        if (!ln || tap) throw std::invalid_argument("k_pw shared tile: LN on load, no tap mode");
+#define CNF_PW_SCASE(NR_, GM_, RES_)                                                                  \
+        if (nr == NR_ && gm == GM_ && res == RES_) {                                                  \
+            CNF_LAUNCH((k_pw<NR_, GM_, true, RES_, -1, false, false, true>), g, dim3(64 * PW_NW * PW_NS), lds, st, a); \
+            return;                                                                                   \
+        }
+#define CNF_PW_SNR(GM_, RES_) CNF_PW_SCASE(1, GM_, RES_) CNF_PW_SCASE(2, GM_, RES_) CNF_PW_SCASE(3, GM_, RES_) CNF_PW_SCASE(4, GM_, RES_)
+        CNF_PW_SNR(1, false) CNF_PW_SNR(2, false) CNF_PW_SNR(4, false) CNF_PW_SNR(8, false)
+        CNF_PW_SNR(1, true) CNF_PW_SNR(2, true) CNF_PW_SNR(4, true) CNF_PW_SNR(8, true)
+#undef CNF_PW_SNR
+#undef CNF_PW_SCASE
+        throw std::invalid_argument("k_pw shared tile: no instantiation for this shape");
+    }
+#endif
 #define CNF_PW_CASE(NR_, GM_, LN_, RES_)                                              \
     if (nr == NR_ && gm == GM_ && ln == LN_ && res == RES_) {                          \
         CNF_LAUNCH((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
@@ -496,11 +560,11 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             const int tr = rem / GS(TW), tc = rem - tr * GS(TW);
             base[h] = band + ((blk * (GS(TH) + 2 * br.dil) + tr) * br.BW + tc) * br.S;
         }
-        f4 acc0[NR], acc1[NR];
+        f4 acc0[NR], acc1[NR];   // start at the bias
 #pragma unroll
         for (int n = 0; n < NR; n++) {
-            acc0[n] = f4{0.f, 0.f, 0.f, 0.f};
-            acc1[n] = f4{0.f, 0.f, 0.f, 0.f};
+            acc0[n] = bz[n];
+            acc1[n] = bz[n];
         }
         for (int g0 = 0; g0 < G; g0 += GQ) {
             int qv[GQ];
@@ -529,7 +593,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             }
         }
         if (stats && first) {
-            st.set_shift(lrelu(acc0[0][0] + bz[0][0]));
+            st.set_shift(lrelu(acc0[0][0]));
             first = false;
         }
 #pragma unroll
@@ -540,7 +604,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             float* orow = outp + (size_t)gc_out_pixel<SID>(a, pv ? po : 0, px0, r0, ph0) * br.opcs + br.out_off + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NR; n++) {
-                f4 v = (h ? acc1[n] : acc0[n]) + bz[n];
+                const f4 v = h ? acc1[n] : acc0[n];
 #ifdef CNF_ABL_GC_NOSTORE_POLY   // ablation (diagnostic builds only): no t2 stores from polyphase tiles
                 if (GS(ps) > 1) {
                 } else
@@ -591,6 +655,17 @@ __device__ long long g_gc_stamps[64];
 #else
 #define GSTAMP(i) do { } while (0)
 #endif
+// per-workgroup stamps (CNF_GC_WGSTAMPS builds only): thread 0 of every workgroup, at its start (0),
+// after the prologue (1) and after each image (2 + i); read through cnf_debug_read_pw_stamps
+#ifdef CNF_GC_WGSTAMPS
+#define GWSTAMP(i)                                                                                       \
+    do {                                                                                                 \
+        if (threadIdx.x == 0 && (i) < PW_ST_N && blockIdx.y * gridDim.x + blockIdx.x < PW_ST_WG)         \
+            g_pw_stamps[blockIdx.y * gridDim.x + blockIdx.x][(i)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define GWSTAMP(i) do { } while (0)
+#endif
 
 // One workgroup per CU: a tile of TH rows of one net, looping over `ipw` images. The bands are
 // double-buffered: the next image's t1 quads are loaded into registers before the current image's
@@ -620,6 +695,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     float* lds_f = reinterpret_cast<float*>(smem);
     int gs = 0;
     GSTAMP(gs++);
+    GWSTAMP(0);
 
     // image-independent staging plan of this thread: quad e = tid + GC_NT*u of the concatenated branch
     // bands -> source offset inside one image, LDS float index, valid channels (0 = zero quad)
@@ -747,6 +823,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     store_img(0, xq[0]);
     __syncthreads();
     GSTAMP(gs++);
+    GWSTAMP(1);
 
     // the ring's other images (PD > 1)
 #pragma unroll
@@ -786,6 +863,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
         if (ii + 1 < nimg) store_img(ii + 1, xq[(jj + 1) % PD]);   // the other buffer: nobody reads it this iteration
         __syncthreads();
         GSTAMP(gs++);
+        GWSTAMP(2 + ii);
     }
 #ifdef CNF_GC_STAMPS
     if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_gc_stamps[63] = gs;
