@@ -77,6 +77,40 @@ __device__ __forceinline__ int pend_index(const CoupPend& q, int pos, int W, int
 }
 
 
+// Philox4x32-10 (Salmon et al. 2011): counter (c0..c3), key (k0, k1), 10 rounds in place
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+// instance_noise (conv_cINN_base_functions.py:635-654) of element g of the stream (g = offset + flat
+// index): alpha x + (1 - alpha) z, z ~ N(0, 1) by Box-Muller on the Philox words of counter g / 4
+// (4 normals per counter value, element g taking normal g % 4). One expression for k_noise and the
+// forward's fused first-layer gather (cnf_flow_forward_noise), so the two agree bit for bit.
+// x_or_null == false: renew_noise (:660-676), z alone.
+__device__ __forceinline__ float instance_noise_value(float x, bool has_x, float alpha, uint64_t seed, uint64_t g) {
+    uint32_t c[4] = {(uint32_t)(g >> 2), (uint32_t)(g >> 34), 0u, 0u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const int w = (int)(g & 3);
+    const int pair = w >> 1;
+    // uniform in (0, 1] and [0, 1)
+    const float u1 = ((float)(c[2 * pair] >> 8) + 1.f) * (1.f / 16777216.f);
+    const float u2 = (float)(c[2 * pair + 1] >> 8) * (1.f / 16777216.f);
+    const float rad = sqrtf(-2.f * logf(u1));
+    const float th = 6.283185307179586f * u2;
+    const float z = (w & 1) ? rad * sinf(th) : rad * cosf(th);
+    return has_x ? fmaf(alpha, x, (1.f - alpha) * z) : z;
+}
+
 // Wave-wide fp32 sum by DPP lane moves (quad_perm, row_shr, row_bcast: a few cycles each instead
 // of an LDS-routed ds_bpermute per step); lane 63 ends with the total, broadcast by readlane.
 // Out-of-range source lanes read 0 (update_dpp with old = 0). Fixed order: bitwise reproducible.

@@ -167,6 +167,13 @@ struct NetLdsArgs {
     // (null: inference)
     float* save;
     int save_img, save_t1, save_t2, save_st;
+    // fused input noise (cnf_flow_forward_noise, first coupling only): the u1c gather reads nz_src and
+    // applies instance_noise_value (stream element nz_off + flat batch index), and u (then the noisy
+    // xy, written here) receives every element of the image: net A's workgroup the gathered half,
+    // net b's the transformed half. null: u is read as is
+    const float* nz_src;
+    float nz_alpha;
+    unsigned long long nz_seed, nz_off;
 };
 
 // Block of one (net, image) in a k_net_lds layer's training save area (all float offsets):

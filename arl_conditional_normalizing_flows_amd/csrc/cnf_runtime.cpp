@@ -639,10 +639,19 @@ static double net_flops(const Coupling& c) {
 // layer of the same forward).
 // save / so_save (training forward of a layer with the fused LDS backward): k_net_lds also writes the
 // raw activations and LN statistics to save (LdsSave blocks) and its s / t outputs to so_save[2]
+// input noise of cnf_flow_forward_noise (instance_noise, conv_cINN_base_functions.py:635-654)
+struct NoiseIn {
+    const float* src;   // the clean input xy
+    float alpha;
+    uint64_t seed, off;
+};
+
+// nz (first coupling of cnf_flow_forward_noise, k_net_lds layers only): u is the noisy-input buffer,
+// written by this layer's k_net_lds from nz->src (the fused gather)
 static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir,
                          const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr,
                          float* save = nullptr, float* const* so_save = nullptr,
-                         const TrainLayout::StreamSave* ss = nullptr) {
+                         const TrainLayout::StreamSave* ss = nullptr, const NoiseIn* nz = nullptr) {
     const int B = E.B;
     const WsLayout& L = E.L;
     const float* P = E.params;
@@ -683,6 +692,13 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             na.save_t2 = s.t2;
             na.save_st = s.st;
         }
+        if (nz != nullptr) {
+            if (pend != nullptr || save != nullptr) throw std::logic_error("fused input noise: first inference layer only");
+            na.nz_src = nz->src;
+            na.nz_alpha = nz->alpha;
+            na.nz_seed = nz->seed;
+            na.nz_off = nz->off;
+        }
         if (pend != nullptr) {
             // buffer discipline of the deferred law (dry runs carry no real pointers): this layer's
             // input is the pending layer's output v_k, which must not be the u_k it is computed
@@ -706,6 +722,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         const double by = 4.0 * (B * HWc * (c.dc1 + c.dc2) * 2 + 2 * (ln_floats + w_floats));
         E.record("k_net_lds", fl, by, [na, B, ilds](void* st) { launch_net_lds(na, B, ilds, (hipStream_t)st); });
     } else {
+    if (nz != nullptr) throw std::logic_error("fused input noise: k_net_lds layers only");
     float* u1c = E.at<float>(L.u1c);
     // conv_in straight from u (k_pw tap mode: the mask gather inside the im2col loads) when packed
     const bool cin_tap = E.p.use_pw && c.net[0].ci_pw.size > 0;
@@ -1226,8 +1243,12 @@ size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
 
 // the forward schedule; save_inputs: also copy every coupling layer's input into the training
 // workspace (cnf_flow_forward_train)
+// nz (cnf_flow_forward_noise): xy is the caller's buffer for the noisy input, which the first coupling's
+// k_net_lds writes while gathering from nz->src with the noise applied (a k_noise pass into it first when
+// that layer is streamed)
 static void flow_forward(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
-                         float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs) {
+                         float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs,
+                         const NoiseIn* nz = nullptr) {
     if (!p.dry) ensure_tables(p);
     p.recorded.clear();
     Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
@@ -1240,6 +1261,17 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     int which = 0;
     size_t bi = 0;
     const int nuv = (int)L.n_uv;
+    const bool nz_fused = nz != nullptr && !save_inputs && !p.layers.empty() &&
+                          p.layers[0].kind == CNF_LAYER_COUPLING && p.couplings[p.layers[0].ci].use_lds;
+    if (nz != nullptr && !nz_fused) {
+        const NoiseIn q = *nz;
+        float* dst = const_cast<float*>(xy);
+        const int64_t n = (int64_t)B * p.desc.io_h * p.desc.io_w * p.desc.io_d;
+        E.record("k_noise", 0, 8.0 * n, [=](void* st) {
+            if (cnf_instance_noise(q.src, dst, n, q.alpha, q.seed, q.off, st) != CNF_OK)
+                throw std::runtime_error(cnf_last_error());
+        });
+    }
     // a k_net_lds layer followed directly by another one leaves its coupling law to that layer's
     // kernel (CoupPend): no k_coupling launch for it. Not when saving layer inputs (training).
     static const bool fuse = [] {   // A/B knob
@@ -1292,7 +1324,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
                 so_save[1] = so_save[0] + (size_t)B * c.hc * c.wc * c.dc2;
             }
             run_coupling(E, c, cur, nxt, ld + (size_t)c.index * B * L.ld_parts, +1, have_pend ? &pend : nullptr,
-                         defer, &next, save, (save || ss) ? so_save : nullptr, ss);
+                         defer, &next, save, (save || ss) ? so_save : nullptr, ss, nz_fused && li == 0 ? nz : nullptr);
             pend = next;
             have_pend = defer;
             cur = nxt;
@@ -1352,6 +1384,20 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
     if (xy == zy) return fail(CNF_E_INVALID, "xy and zy must not alias (out-of-place only)");
     CNF_TRY
     flow_forward(*plan->p, params, aux, xy, zy, logdet_per_image, workspace, B, (hipStream_t)stream, false);
+    return CNF_OK;
+    CNF_CATCH
+}
+
+int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux, const float* xy, float alpha,
+                           uint64_t seed, uint64_t offset, float* xy_noisy, float* zy, float* logdet_per_image,
+                           void* workspace, int B, void* stream) {
+    if (!plan || !params || !aux || !xy || !xy_noisy || !zy || !logdet_per_image || !workspace || B <= 0)
+        return fail(CNF_E_INVALID, "null argument or B <= 0");
+    if (xy == zy || xy_noisy == zy || xy_noisy == xy)
+        return fail(CNF_E_INVALID, "xy, xy_noisy and zy must not alias (out-of-place only)");
+    CNF_TRY
+    const NoiseIn nz{xy, alpha, seed, offset};
+    flow_forward(*plan->p, params, aux, xy_noisy, zy, logdet_per_image, workspace, B, (hipStream_t)stream, false, &nz);
     return CNF_OK;
     CNF_CATCH
 }

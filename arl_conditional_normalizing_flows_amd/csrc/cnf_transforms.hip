@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../../include/cnf.h"
+#include "cnf_device.h"
 
 namespace cnf {
 
@@ -117,40 +118,12 @@ __global__ __launch_bounds__(256) void k_up(const float* __restrict__ in, float*
     }
 }
 
-// Philox4x32-10 (Salmon et al. 2011): counter (offset + i / 4 as 64 bits, 0, 0), key = seed
-__device__ inline void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; r++) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
-        c[0] = n0;
-        c[1] = n1;
-        c[2] = n2;
-        c[3] = n3;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
-// instance_noise (:635-654) / renew_noise (:660-676); Box-Muller on Philox words, 4 normals per
-// counter value (element i uses normal i % 4 of counter (offset + i) / 4)
+// instance_noise (:635-654) / renew_noise (:660-676): element i of the stream offset + i
+// (instance_noise_value, cnf_device.h)
 __global__ __launch_bounds__(256) void k_noise(const float* __restrict__ x, float* __restrict__ out, long long n,
                                                float alpha, uint64_t seed, uint64_t offset) {
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const uint64_t g = offset + (uint64_t)i;
-        uint32_t c[4] = {(uint32_t)(g >> 2), (uint32_t)(g >> 34), 0u, 0u};
-        philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const int w = (int)(g & 3);
-        const int pair = w >> 1;
-        // uniform in (0, 1] and [0, 1)
-        const float u1 = ((float)(c[2 * pair] >> 8) + 1.f) * (1.f / 16777216.f);
-        const float u2 = (float)(c[2 * pair + 1] >> 8) * (1.f / 16777216.f);
-        const float rad = sqrtf(-2.f * logf(u1));
-        const float th = 6.283185307179586f * u2;
-        const float z = (w & 1) ? rad * sinf(th) : rad * cosf(th);
-        out[i] = x != nullptr ? alpha * x[i] + (1.f - alpha) * z : z;
-    }
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+        out[i] = instance_noise_value(x != nullptr ? x[i] : 0.f, x != nullptr, alpha, seed, offset + (uint64_t)i);
 }
 
 int grid_for(long long n) {

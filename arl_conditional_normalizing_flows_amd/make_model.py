@@ -426,15 +426,38 @@ class cFlow:
         return [self.loss_tracker, self.z_loss_tracker, self.y_loss_tracker, self.detJ_loss_tracker]
 
     # -- the hot path ---------------------------------------------------------------------------
-    def call(self, uv, direction=-1, per_image_logdet=False, layerwise=False):
+    def call(self, uv, direction=-1, per_image_logdet=False, layerwise=False, noise=None):
         """cFlow.call (:1723-1798). direction=+1: xy -> (zy, log_detJ) with log_detJ the batch-mean
         scalar (a (B,) tensor with per_image_logdet=True); direction=-1: zy -> xy.
         layerwise=True walks layers_list through the per-layer entry points exactly as the
-        reference loop does; the default runs the whole schedule in one native call."""
+        reference loop does; the default runs the whole schedule in one native call.
+        noise=(alpha, seed, offset) (direction=+1): the training pipeline's instance noise
+        (conv_cINN.py:312-315, conv_cINN_base_functions.py:635-654) applied to xy first -- inside
+        the first coupling layer's gather (cnf_flow_forward_noise) -- returning (zy, log_detJ,
+        xy_noisy); xy_noisy equals base_functions.instance_noise(xy, alpha, seed, offset) bit for
+        bit and is the xy of the loss."""
         uv = _as_input(uv, 'uv')
         if tuple(uv.shape[1:]) != tuple(self.io_shape):
             raise ValueError(f'input shape {tuple(uv.shape)} != [None, {self.io_shape}]')
         B = uv.shape[0]
+        if noise is not None:
+            if direction != 1:
+                raise ValueError('noise applies to the forward direction only')
+            alpha, seed, offset = (tuple(noise) + (0, 0))[:3]
+            if layerwise:
+                from .base_functions import instance_noise
+                xn = instance_noise(uv, alpha, seed, offset)
+                zy, ld = self._call_layerwise_forward(xn)
+            else:
+                xn = torch.empty_like(uv)
+                zy = torch.empty_like(uv)
+                ld = torch.empty(B, device=uv.device, dtype=torch.float32)
+                ws = self._workspace(B)
+                check(_lib.load().cnf_flow_forward_noise(self._plan, ptr(self.params), ptr(self._aux), ptr(uv),
+                                                         float(alpha), int(seed) & (2 ** 64 - 1),
+                                                         int(offset) & (2 ** 64 - 1), ptr(xn), ptr(zy), ptr(ld),
+                                                         ptr(ws), B, _stream()), 'cnf_flow_forward_noise')
+            return zy, (ld if per_image_logdet else ld.mean()), xn
         if direction == 1:
             if layerwise:
                 zy, ld = self._call_layerwise_forward(uv)
@@ -495,15 +518,20 @@ class cFlow:
                                   _stream()), 'cnf_nll')
         return sums, per
 
-    def log_loss(self, xy, process_group=None):
+    def log_loss(self, xy, process_group=None, noise=None):
         """cFlow.log_loss (:1800-1848): (loss, z_loss, y_loss, detJ_loss), batch means.
         With process_group given (True = the default group) and torch.distributed initialised,
         this rank's 4 sums and its image count are all-reduced (one collective of 5 fp32,
         distributed.reduce_nll_sums) so the means are over the global batch; shards may be
-        ragged."""
+        ragged. noise=(alpha, seed, offset): the loss of the instance-noised input (call(noise=...):
+        the noise applied inside the forward's first kernel, y' taken from the noisy input)."""
         from .distributed import reduce_nll_sums
         xy = _as_input(xy, 'xy')
-        sums, _ = self.nll_sums(xy)
+        if noise is not None:
+            zy, ld, xn = self.call(xy, 1, per_image_logdet=True, noise=noise)
+            sums, _ = self.nll_sums(xn, zy, ld)
+        else:
+            sums, _ = self.nll_sums(xy)
         grp = None if process_group is True else process_group
         return reduce_nll_sums(sums, xy.shape[0], group=grp, all_reduce=process_group is not None)
 

@@ -28,6 +28,7 @@ Extra fields of the JSON line (rank 0):
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import math
 import os
@@ -362,6 +363,10 @@ def main():
                          'fwd+logdet metric step; prints its own JSON line. inverse: sampling, '
                          'cFlow.call(zy, -1) (conv_cINN_make_model.py:1774-1798) on the forward\'s zy of the '
                          'bench batch (no collective: the inverse has no cross-image term)')
+    ap.add_argument('--noise', type=float, default=None, metavar='ALPHA',
+                    help='forward mode: the training pipeline\'s instance noise alpha xy + (1 - alpha) N(0,1) '
+                         '(conv_cINN.py:312-315, e.g. 0.98) applied inside the first coupling kernel '
+                         '(cnf_flow_forward_noise), the NLL taken on the noisy input')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -415,6 +420,8 @@ def main():
     lib = _lib.load()
 
     inverse = args.mode == 'inverse'
+    noisy = args.noise is not None and not inverse
+    xn = torch.empty_like(xy) if noisy else xy   # the noisy input (cnf_flow_forward_noise writes it)
     if inverse:
         # sampling input: the forward's zy of the bench batch (a valid latent of this flow)
         zy_in, _ = flow(xy, 1)
@@ -427,9 +434,15 @@ def main():
             _lib.check(lib.cnf_flow_inverse(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
                                             zy_in.data_ptr(), x_out.data_ptr(), ws.data_ptr(), B, st), 'inverse')
             return
-        _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(), xy.data_ptr(),
-                                        zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
-        _lib.check(lib.cnf_nll(flow._plan, xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
+        if noisy:
+            _lib.check(lib.cnf_flow_forward_noise(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
+                                                  xy.data_ptr(), float(args.noise), 1000 + rank, 0, xn.data_ptr(),
+                                                  zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
+        else:
+            _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
+                                            xy.data_ptr(), zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st),
+                       'forward')
+        _lib.check(lib.cnf_nll(flow._plan, xn.data_ptr(), zy.data_ptr(), ld.data_ptr(), per.data_ptr(),
                                sums.data_ptr(), B, st), 'nll')
 
     def exchange():
@@ -451,6 +464,15 @@ def main():
     step()
     note('first step done')
     torch.cuda.synchronize()
+    noise_pass = None
+    if noisy:   # is the noise applied by a launch of its own (first layer streamed) or inside k_net_lds?
+        nm = C.create_string_buffer(256)
+        fl, by = C.c_double(), C.c_double()
+        names = []
+        for i in range(lib.cnf_plan_num_recorded_launches(flow._plan)):
+            _lib.check(lib.cnf_plan_recorded_launch_info(flow._plan, i, nm, 256, C.byref(fl), C.byref(by)), 'info')
+            names.append(nm.value.decode())
+        noise_pass = 'k_noise' in names
     graph = None
     if not args.no_graph:
         try:
@@ -536,7 +558,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = (cpu_baseline_inverse(cfg, flow, zy_in.cpu().numpy(), B) if inverse
-                   else cpu_baseline(cfg, flow, xy_np, B))
+                   else cpu_baseline(cfg, flow, xn.cpu().numpy() if noisy else xy_np, B))
         H, W, _ = cfg.io_shape
         bpd = float(loss_mean / (np.log(2) * H * W * cfg.x_d)) if not inverse else None
         if inverse:
@@ -560,7 +582,9 @@ def main():
                        'model': f'cFlow {cfg.name}', 'global_batch': G,
                        'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world} (batch shards, '
                                                                           f'1 all-reduce of 5 fp32)',
-                       'graph': graph is not None},
+                       'graph': graph is not None,
+                       'input_noise': ({'alpha': args.noise, 'separate_noise_pass': noise_pass}
+                                       if noisy else None)},
             'step_ms_median': round(float(np.median(st_ms)), 4) if st_ms else None,
             'bits_per_dim': round(bpd, 6) if bpd is not None else None,
             'logdet_mean': ld_mean,

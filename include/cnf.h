@@ -117,6 +117,19 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux,
                      const float* xy, float* zy, float* logdet_per_image,
                      void* workspace, int B, void* stream);
 
+/* cnf_flow_forward of the training pipeline's noisy input (conv_cINN.py:312-315:
+ * instance_noise(xy, alpha) per element, conv_cINN_base_functions.py:635-654):
+ * xy_noisy[B,H,W,D] receives alpha xy + (1 - alpha) N(0, 1) -- the Philox stream
+ * of cnf_instance_noise(xy, xy_noisy, B*H*W*D, alpha, seed, offset), bit for bit --
+ * and zy / logdet_per_image are cnf_flow_forward of it. The noise is applied
+ * inside the first coupling layer's gather (no separate pass over xy) when that
+ * layer is LDS-resident; otherwise by a cnf_instance_noise pass first. xy_noisy
+ * is the xy of the matching cnf_nll call. No two of xy, xy_noisy, zy may alias. */
+int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux,
+                           const float* xy, float alpha, uint64_t seed, uint64_t offset,
+                           float* xy_noisy, float* zy, float* logdet_per_image,
+                           void* workspace, int B, void* stream);
+
 /* cFlow.call(zy, direction=-1) (:1774-1798): zy -> xy (must not alias). */
 int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux,
                      const float* zy, float* xy, void* workspace, int B, void* stream);

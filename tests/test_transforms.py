@@ -122,3 +122,41 @@ def test_instance_noise_formula_and_moments(gpu):
     tail = F.renew_noise(x[:1000], seed=7, offset=n - 1000).cpu().numpy().astype(np.float64)
     assert np.array_equal(tail, z[-1000:])
     assert not np.array_equal(F.renew_noise(x, seed=8).cpu().numpy()[:64], z[:64].astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,B', [('cfg2', 3), ('small', 2), ('cfg4', 1)])
+def test_noise_fused_into_the_forward(gpu, name, B):
+    """cnf_flow_forward_noise (cFlow.call(noise=...)): the training pipeline's 2 % instance noise
+    (conv_cINN.py:312-315; conv_cINN_base_functions.py:635-654) applied inside the first coupling
+    layer's k_net_lds gather (cfg2, small: no separate pass over xy; cfg4's first layer is streamed:
+    a cnf_instance_noise pass first). The noisy input equals the standalone cnf_instance_noise stream
+    bit for bit, zy / log-det equal cnf_flow_forward of it bit for bit, the loss is that of the noisy
+    input, and zy matches the float64 oracle composed with the oracle-side noisy input."""
+    from arl_conditional_normalizing_flows_amd.base_functions import instance_noise
+    from arl_conditional_normalizing_flows_amd.config import PRESETS
+    from arl_conditional_normalizing_flows_amd.make_model import cFlow
+    from oracle.cflow_np import OracleCFlow, synthetic_class_batch
+    cfg = PRESETS[name]
+    kw = cfg.kwargs()
+    flow = cFlow(**kw, device=gpu)
+    ora = OracleCFlow(**kw)
+    P = ora.init_params(2)
+    flow.set_weights(P)
+    H, W, _ = cfg.io_shape
+    x = torch.from_numpy(synthetic_class_batch(B, H, W, cfg.x_d, seed=4)).to(gpu)
+    noise = (0.98, 1234567, 99)
+    zy, ld, xn = flow(x, 1, per_image_logdet=True, noise=noise)
+    xn_ref = instance_noise(x, *noise)
+    zy_ref, ld_ref = flow(xn_ref, 1, per_image_logdet=True)
+    lf = flow.log_loss(x, noise=noise)
+    lr = flow.log_loss(xn_ref)
+    torch.cuda.synchronize()
+    assert torch.equal(xn, xn_ref)
+    assert torch.equal(zy, zy_ref) and torch.equal(ld, ld_ref)
+    assert all(torch.equal(a, b) for a, b in zip(lf, lr))
+    assert not torch.equal(xn, x)
+    z64, l64, abs_s = ora.forward(xn.cpu().double().numpy(), P, abs_s=True)
+    e = np.max(np.abs(zy.cpu().numpy() - z64)) / np.max(np.abs(z64))
+    assert e < 1e-5, e
+    assert np.all(np.abs(ld.cpu().numpy() - l64) <= 1e-5 * np.maximum(np.abs(l64), abs_s))
