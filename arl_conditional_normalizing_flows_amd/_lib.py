@@ -60,8 +60,8 @@ _SIGS = [
     ('cnf_pack_params', C.c_int, [_P, _F, _F, _P]),
     ('cnf_plan_workspace_bytes', C.c_size_t, [_P, C.c_int]),
     ('cnf_flow_forward', C.c_int, [_P, _F, _F, _F, _F, _F, _P, C.c_int, _P]),
-    ('cnf_flow_forward_noise', C.c_int, [_P, _F, _F, _F, C.c_float, C.c_uint64, C.c_uint64, _F, _F, _F, _P, C.c_int,
-                                         _P]),
+    ('cnf_flow_forward_noise', C.c_int, [_P, _F, _F, _F, C.c_float, C.c_float, C.c_uint64, C.c_uint64, _F, _F, _F, _P,
+                                         C.c_int, _P]),
     ('cnf_flow_inverse', C.c_int, [_P, _F, _F, _F, _F, _P, C.c_int, _P]),
     ('cnf_coupling_forward', C.c_int, [_P, C.c_int, _F, _F, _F, _F, _F, _P, C.c_int, _P]),
     ('cnf_coupling_inverse', C.c_int, [_P, C.c_int, _F, _F, _F, _F, _P, C.c_int, _P]),

@@ -111,6 +111,20 @@ __device__ __forceinline__ float instance_noise_value(float x, bool has_x, float
     return has_x ? fmaf(alpha, x, (1.f - alpha) * z) : z;
 }
 
+// the reference's logit preprocess of x (preprocess_dataset_class(LOGITS=True), :174-231):
+// v -> (logit(a + (1 - a) b v) - logit(a)) / (logit(1 - a) - logit(a)); k_logit and the fused
+// input preparation share this expression
+__device__ __forceinline__ float logit_value(float v, const LogitK& k) {
+    const float e = fmaf(k.c1, v, k.a);
+    return (logf(e / (1.f - e)) - k.lo) / k.span;
+}
+// InputPrepArgs (cnf_kernels.h) of element g of the batch stream, channel ch: cnf_flow_forward_noise's
+// fused gather and its k_prep fallback use this one expression, bit for bit the k_logit + k_noise passes
+__device__ __forceinline__ float input_prep_value(float x, int ch, const InputPrepArgs& q, uint64_t g) {
+    if (q.logit && ch < q.x_d) x = logit_value(x, q.lk);
+    return instance_noise_value(x, true, q.alpha, q.seed, g);
+}
+
 // Wave-wide fp32 sum by DPP lane moves (quad_perm, row_shr, row_bcast: a few cycles each instead
 // of an LDS-routed ds_bpermute per step); lane 63 ends with the total, broadcast by readlane.
 // Out-of-range source lanes read 0 (update_dpp with old = 0). Fixed order: bitwise reproducible.

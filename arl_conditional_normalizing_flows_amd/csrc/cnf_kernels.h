@@ -141,6 +141,26 @@ struct CoupPend {
     int dir = 1;
 };
 
+// fp32 constants of the reference's logit map (preprocess_dataset_class, conv_cINN_base_functions.py
+// :174-231; TF evaluates the Python-float constants in fp32): c1 = (1-a) b, lo = logit(a),
+// span = logit(1-a) - logit(a), inv_bc = 1 / (b (1 - a)) (cnf_transforms.hip logit_consts)
+struct LogitK {
+    float a, c1, lo, span, inv_bc;
+};
+// the flow's input as the reference pipeline builds it from the raw xy (conv_cINN.py:246-315): the
+// logit map on the x channels (ch < x_d, logit != 0), then instance noise alpha v + (1 - alpha) N(0,1)
+// on every channel (cnf_device.h input_prep_value)
+struct InputPrepArgs {
+    const float* src;   // the raw xy (null: no preparation)
+    float alpha;
+    unsigned long long seed, off;
+    int logit, x_d, D;
+    LogitK lk;
+};
+
+LogitK logit_consts(float a);   // cnf_transforms.hip
+void launch_input_prep(float* out, long long n, const InputPrepArgs& q, hipStream_t st);   // k_prep
+
 struct NetLdsArgs {
     const float* u;           // layer input [B][H][W][D]
     float* so[2];             // outputs: raw conv_out of net A (pre-tanh) / net b, [B][hc][wc][dc2]
@@ -167,13 +187,12 @@ struct NetLdsArgs {
     // (null: inference)
     float* save;
     int save_img, save_t1, save_t2, save_st;
-    // fused input noise (cnf_flow_forward_noise, first coupling only): the u1c gather reads nz_src and
-    // applies instance_noise_value (stream element nz_off + flat batch index), and u (then the noisy
-    // xy, written here) receives every element of the image: net A's workgroup the gathered half,
-    // net b's the transformed half. null: u is read as is
-    const float* nz_src;
-    float nz_alpha;
-    unsigned long long nz_seed, nz_off;
+    // fused input preparation (cnf_flow_forward_noise, first coupling only): the u1c gather reads
+    // nz.src and applies input_prep_value (logit on the x channels, instance noise of stream element
+    // nz.off + flat batch index), and u (then the prepared xy, written here) receives every element
+    // of the image: net A's workgroup the gathered half, net b's the transformed half. nz.src null:
+    // u is read as is
+    InputPrepArgs nz;
 };
 
 // Block of one (net, image) in a k_net_lds layer's training save area (all float offsets):

@@ -917,17 +917,18 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
         return o[11 + 2 * l] + ((SA(br_cout)[l] + 3) & ~3) - o[10];
     };
     // gather u1c (mask compress) into T2 (stride SU)
-    if (a.pend.on == 0 && a.nz_src != nullptr) {
-        // fused instance noise on the layer input (the first coupling of cnf_flow_forward_noise): the
-        // gathered half with noise, and the noisy input written out (net b: the transformed half too)
+    if (a.pend.on == 0 && a.nz.src != nullptr) {
+        // fused input preparation of the layer input (the first coupling of cnf_flow_forward_noise:
+        // logit on the x channels, instance noise): the gathered half prepared, and the prepared input
+        // written out (net b: the transformed half too)
         const size_t n_img = (size_t)SA(H) * SA(W) * SA(D), ib = (size_t)img * n_img;
-        const float* xb = a.nz_src + ib;
+        const float* xb = a.nz.src + ib;
         float* ub = const_cast<float*>(a.u) + ib;
         const int n = HW * SA(dc1);
         for (int e = threadIdx.x; e < n; e += NT) {
             const int p = e / SA(dc1), c = e - p * SA(dc1);
             const int pos = mask_pos_(a.mask, p, c, W, SA(W), SA(D));
-            const float val = instance_noise_value(xb[pos], true, a.nz_alpha, a.nz_seed, a.nz_off + ib + pos);
+            const float val = input_prep_value(xb[pos], pos % SA(D), a.nz, a.nz.off + ib + pos);
             T2[p * SU + c] = val;
             if (net == 0) ub[pos] = val;
         }
@@ -936,7 +937,7 @@ __global__ __launch_bounds__(NT) void k_net_lds(NetLdsArgs a) {
             for (int e = threadIdx.x; e < n2; e += NT) {
                 const int p = e / SA(dc2), c = e - p * SA(dc2);
                 const int pos = mask_pos_(a.mask ^ 1, p, c, W, SA(W), SA(D));   // the complement mask
-                ub[pos] = instance_noise_value(xb[pos], true, a.nz_alpha, a.nz_seed, a.nz_off + ib + pos);
+                ub[pos] = input_prep_value(xb[pos], pos % SA(D), a.nz, a.nz.off + ib + pos);
             }
         }
     } else if (a.pend.on == 0) {

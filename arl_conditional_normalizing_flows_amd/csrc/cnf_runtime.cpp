@@ -639,19 +639,12 @@ static double net_flops(const Coupling& c) {
 // layer of the same forward).
 // save / so_save (training forward of a layer with the fused LDS backward): k_net_lds also writes the
 // raw activations and LN statistics to save (LdsSave blocks) and its s / t outputs to so_save[2]
-// input noise of cnf_flow_forward_noise (instance_noise, conv_cINN_base_functions.py:635-654)
-struct NoiseIn {
-    const float* src;   // the clean input xy
-    float alpha;
-    uint64_t seed, off;
-};
-
 // nz (first coupling of cnf_flow_forward_noise, k_net_lds layers only): u is the noisy-input buffer,
 // written by this layer's k_net_lds from nz->src (the fused gather)
 static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, double* ld_part, int dir,
                          const CoupPend* pend = nullptr, bool defer = false, CoupPend* out_pend = nullptr,
                          float* save = nullptr, float* const* so_save = nullptr,
-                         const TrainLayout::StreamSave* ss = nullptr, const NoiseIn* nz = nullptr) {
+                         const TrainLayout::StreamSave* ss = nullptr, const InputPrepArgs* nz = nullptr) {
     const int B = E.B;
     const WsLayout& L = E.L;
     const float* P = E.params;
@@ -694,10 +687,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         }
         if (nz != nullptr) {
             if (pend != nullptr || save != nullptr) throw std::logic_error("fused input noise: first inference layer only");
-            na.nz_src = nz->src;
-            na.nz_alpha = nz->alpha;
-            na.nz_seed = nz->seed;
-            na.nz_off = nz->off;
+            na.nz = *nz;
         }
         if (pend != nullptr) {
             // buffer discipline of the deferred law (dry runs carry no real pointers): this layer's
@@ -1248,7 +1238,7 @@ size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
 // that layer is streamed)
 static void flow_forward(Plan& p, const float* params, const float* aux, const float* xy, float* zy,
                          float* logdet_per_image, void* workspace, int B, hipStream_t stream, bool save_inputs,
-                         const NoiseIn* nz = nullptr) {
+                         const InputPrepArgs* nz = nullptr) {
     if (!p.dry) ensure_tables(p);
     p.recorded.clear();
     Exec E{p, params, aux, (char*)workspace, p.layout(B), B, stream};
@@ -1264,13 +1254,10 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     const bool nz_fused = nz != nullptr && !save_inputs && !p.layers.empty() &&
                           p.layers[0].kind == CNF_LAYER_COUPLING && p.couplings[p.layers[0].ci].use_lds;
     if (nz != nullptr && !nz_fused) {
-        const NoiseIn q = *nz;
+        const InputPrepArgs q = *nz;
         float* dst = const_cast<float*>(xy);
-        const int64_t n = (int64_t)B * p.desc.io_h * p.desc.io_w * p.desc.io_d;
-        E.record("k_noise", 0, 8.0 * n, [=](void* st) {
-            if (cnf_instance_noise(q.src, dst, n, q.alpha, q.seed, q.off, st) != CNF_OK)
-                throw std::runtime_error(cnf_last_error());
-        });
+        const long long n = (long long)B * p.desc.io_h * p.desc.io_w * p.desc.io_d;
+        E.record("k_prep", 0, 8.0 * n, [=](void* st) { launch_input_prep(dst, n, q, (hipStream_t)st); });
     }
     // a k_net_lds layer followed directly by another one leaves its coupling law to that layer's
     // kernel (CoupPend): no k_coupling launch for it. Not when saving layer inputs (training).
@@ -1388,15 +1375,26 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
     CNF_CATCH
 }
 
-int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux, const float* xy, float alpha,
-                           uint64_t seed, uint64_t offset, float* xy_noisy, float* zy, float* logdet_per_image,
-                           void* workspace, int B, void* stream) {
+int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux, const float* xy, float logit_a,
+                           float alpha, uint64_t seed, uint64_t offset, float* xy_noisy, float* zy,
+                           float* logdet_per_image, void* workspace, int B, void* stream) {
     if (!plan || !params || !aux || !xy || !xy_noisy || !zy || !logdet_per_image || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy || xy_noisy == zy || xy_noisy == xy)
         return fail(CNF_E_INVALID, "xy, xy_noisy and zy must not alias (out-of-place only)");
+    if (logit_a != 0.f && !(logit_a > 0.f && logit_a < 0.5f))
+        return fail(CNF_E_INVALID, "logit_a must be 0 (no logit map) or in (0, 0.5)");
     CNF_TRY
-    const NoiseIn nz{xy, alpha, seed, offset};
+    InputPrepArgs nz;
+    std::memset(&nz, 0, sizeof(nz));
+    nz.src = xy;
+    nz.alpha = alpha;
+    nz.seed = seed;
+    nz.off = offset;
+    nz.logit = logit_a != 0.f ? 1 : 0;
+    nz.x_d = plan->p->desc.x_d;
+    nz.D = plan->p->desc.io_d;
+    if (nz.logit) nz.lk = logit_consts(logit_a);
     flow_forward(*plan->p, params, aux, xy_noisy, zy, logdet_per_image, workspace, B, (hipStream_t)stream, false, &nz);
     return CNF_OK;
     CNF_CATCH

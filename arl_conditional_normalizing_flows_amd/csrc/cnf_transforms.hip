@@ -15,13 +15,7 @@ namespace cnf {
 
 int set_error(int code, const char* msg);   // cnf_runtime.cpp (cnf_last_error)
 
-namespace {
-
-// fp32 constants of the reference's logit map (TF evaluates the Python-float constants in fp32):
-// c1 = (1-a) b, lo = logit(a), span = logit(1-a) - logit(a)
-struct LogitK {
-    float a, c1, lo, span, inv_bc;
-};
+// LogitK (cnf_kernels.h) of the fudge factor a
 LogitK logit_consts(float a) {
     const double ad = a;
     const double b = (1.0 - 2.0 * ad) / (1.0 - ad);
@@ -35,6 +29,8 @@ LogitK logit_consts(float a) {
     return k;
 }
 
+namespace {
+
 // preprocess_dataset_class._preprocess_for_logit / _logit / _scale_logit (:198-212)
 __global__ __launch_bounds__(256) void k_logit(const float* __restrict__ x, float* __restrict__ out, long long n,
                                                LogitK k, int inverse) {
@@ -42,8 +38,7 @@ __global__ __launch_bounds__(256) void k_logit(const float* __restrict__ x, floa
         const float v = x[i];
         float r;
         if (!inverse) {
-            const float e = k.a + k.c1 * v;
-            r = (logf(e / (1.f - e)) - k.lo) / k.span;
+            r = logit_value(v, k);
         } else {   // de_logitify (:306-318): (logistic(v span + lo) - a) / (b (1 - a))
             const float z = v * k.span + k.lo;
             r = (1.f / (1.f + expf(-z)) - k.a) * k.inv_bc;
@@ -126,6 +121,13 @@ __global__ __launch_bounds__(256) void k_noise(const float* __restrict__ x, floa
         out[i] = instance_noise_value(x != nullptr ? x[i] : 0.f, x != nullptr, alpha, seed, offset + (uint64_t)i);
 }
 
+// cnf_flow_forward_noise's input preparation as a pass of its own (the first coupling layer is
+// streamed): out[i] = input_prep_value of element i
+__global__ __launch_bounds__(256) void k_prep(float* __restrict__ out, long long n, InputPrepArgs q) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+        out[i] = input_prep_value(q.src[i], (int)(i % q.D), q, q.off + (uint64_t)i);
+}
+
 int grid_for(long long n) {
     long long g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > 65536 ? 65536 : g));
@@ -138,6 +140,12 @@ int finish(const char* what) {
 }
 
 }  // namespace
+
+void launch_input_prep(float* out, long long n, const InputPrepArgs& q, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_prep, dim3(grid_for(n)), dim3(256), 0, st, out, n, q);
+}
+
 }  // namespace cnf
 
 extern "C" {

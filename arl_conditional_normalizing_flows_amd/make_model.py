@@ -431,11 +431,14 @@ class cFlow:
         scalar (a (B,) tensor with per_image_logdet=True); direction=-1: zy -> xy.
         layerwise=True walks layers_list through the per-layer entry points exactly as the
         reference loop does; the default runs the whole schedule in one native call.
-        noise=(alpha, seed, offset) (direction=+1): the training pipeline's instance noise
-        (conv_cINN.py:312-315, conv_cINN_base_functions.py:635-654) applied to xy first -- inside
-        the first coupling layer's gather (cnf_flow_forward_noise) -- returning (zy, log_detJ,
-        xy_noisy); xy_noisy equals base_functions.instance_noise(xy, alpha, seed, offset) bit for
-        bit and is the xy of the loss."""
+        noise=(alpha, seed, offset[, logit_a]) (direction=+1): the input prepared as the reference's
+        training pipeline does (conv_cINN.py:246-315) -- the logit map of
+        preprocess_dataset_class(LOGITS=True, a=logit_a) on the x channels when logit_a is given
+        (conv_cINN_base_functions.py:174-231), then instance_noise(., alpha) (:635-654) -- inside
+        the first coupling layer's gather (cnf_flow_forward_noise), returning (zy, log_detJ,
+        xy_noisy); xy_noisy equals base_functions.instance_noise(xy', alpha, seed, offset) bit for
+        bit (xy' = xy with its x channels through preprocess_dataset_class) and is the xy of the
+        loss."""
         uv = _as_input(uv, 'uv')
         if tuple(uv.shape[1:]) != tuple(self.io_shape):
             raise ValueError(f'input shape {tuple(uv.shape)} != [None, {self.io_shape}]')
@@ -443,10 +446,14 @@ class cFlow:
         if noise is not None:
             if direction != 1:
                 raise ValueError('noise applies to the forward direction only')
-            alpha, seed, offset = (tuple(noise) + (0, 0))[:3]
+            alpha, seed, offset, logit_a = (tuple(noise) + (0, 0, 0.0))[:4]
             if layerwise:
-                from .base_functions import instance_noise
-                xn = instance_noise(uv, alpha, seed, offset)
+                from .base_functions import instance_noise, preprocess_dataset_class
+                xp = uv
+                if logit_a:
+                    xp = torch.cat([preprocess_dataset_class(uv[..., :self.x_d], LOGITS=True, a=logit_a),
+                                    uv[..., self.x_d:]], dim=-1).contiguous()
+                xn = instance_noise(xp, alpha, seed, offset)
                 zy, ld = self._call_layerwise_forward(xn)
             else:
                 xn = torch.empty_like(uv)
@@ -454,7 +461,7 @@ class cFlow:
                 ld = torch.empty(B, device=uv.device, dtype=torch.float32)
                 ws = self._workspace(B)
                 check(_lib.load().cnf_flow_forward_noise(self._plan, ptr(self.params), ptr(self._aux), ptr(uv),
-                                                         float(alpha), int(seed) & (2 ** 64 - 1),
+                                                         float(logit_a), float(alpha), int(seed) & (2 ** 64 - 1),
                                                          int(offset) & (2 ** 64 - 1), ptr(xn), ptr(zy), ptr(ld),
                                                          ptr(ws), B, _stream()), 'cnf_flow_forward_noise')
             return zy, (ld if per_image_logdet else ld.mean()), xn

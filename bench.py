@@ -49,12 +49,13 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_16x16x4_f32) dense peak
 
 
-def synth(cfg, B, seed):
+def synth(cfg, B, seed, noise_alpha=0.98):
+    """noise_alpha=1: the clean batch (--noise applies the pipeline's noise inside the forward)"""
     from arl_conditional_normalizing_flows_amd.synthetic import class_batch, sr_batch
     H, W, D = cfg.io_shape
     if cfg.data == 'class':
-        return class_batch(B, H, W, cfg.x_d, seed=seed)
-    return sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=seed)
+        return class_batch(B, H, W, cfg.x_d, seed=seed, noise_alpha=noise_alpha)
+    return sr_batch(B, H, W, cfg.x_d, cfg.sr_pow, seed=seed, noise_alpha=noise_alpha)
 
 
 def kernel_symbol(name):
@@ -367,6 +368,9 @@ def main():
                     help='forward mode: the training pipeline\'s instance noise alpha xy + (1 - alpha) N(0,1) '
                          '(conv_cINN.py:312-315, e.g. 0.98) applied inside the first coupling kernel '
                          '(cnf_flow_forward_noise), the NLL taken on the noisy input')
+    ap.add_argument('--logit', type=float, default=0.0, metavar='A',
+                    help='with --noise: the logit preprocess (preprocess_dataset_class(LOGITS=True, a=A), '
+                         'conv_cINN_base_functions.py:174-231) on the x channels first, fused likewise')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -407,7 +411,7 @@ def main():
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
     flow = cFlow(**cfg.kwargs(), device=dev, seed=0)
     # one seeded global batch, sliced per rank
-    xy_np = synth(cfg, G, 1000)[lo:hi].copy()
+    xy_np = synth(cfg, G, 1000, 1.0 if (args.noise is not None and args.mode == 'forward') else 0.98)[lo:hi].copy()
     xy = torch.from_numpy(xy_np).to(dev)
     if args.mode == 'train':
         return train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling)
@@ -436,7 +440,8 @@ def main():
             return
         if noisy:
             _lib.check(lib.cnf_flow_forward_noise(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
-                                                  xy.data_ptr(), float(args.noise), 1000 + rank, 0, xn.data_ptr(),
+                                                  xy.data_ptr(), float(args.logit), float(args.noise), 1000 + rank, 0,
+                                                  xn.data_ptr(),
                                                   zy.data_ptr(), ld.data_ptr(), ws.data_ptr(), B, st), 'forward')
         else:
             _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
@@ -472,7 +477,7 @@ def main():
         for i in range(lib.cnf_plan_num_recorded_launches(flow._plan)):
             _lib.check(lib.cnf_plan_recorded_launch_info(flow._plan, i, nm, 256, C.byref(fl), C.byref(by)), 'info')
             names.append(nm.value.decode())
-        noise_pass = 'k_noise' in names
+        noise_pass = 'k_prep' in names
     graph = None
     if not args.no_graph:
         try:
@@ -571,10 +576,12 @@ def main():
             'metric': metric,
             'value': round(value, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms, 4), 'higher_is_better': True, 'scaling': scaling,
-            'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded class-conditional batch, 2% noise), '
-                                                        'seeded orthogonal-init weights'
-            if cfg.data == 'class' else 'synthetic (seeded SR batch: residual x, down/up y, 2% noise), '
-                                        'seeded orthogonal-init weights',
+            'vs_baseline': None, 'dtype': 'f32',
+            'data': ('synthetic (seeded class-conditional batch, ' if cfg.data == 'class' else
+                     'synthetic (seeded SR batch: residual x, down/up y, ')
+                    + ('clean; logit + 2% noise applied in the forward' if noisy and args.logit else
+                       'clean; 2% noise applied in the forward' if noisy else '2% noise')
+                    + '), seeded orthogonal-init weights',
             'config': {'workload': (f'{cfg.name}: cFlow.call(zy,-1), zy {list(cfg.io_shape)}, ' if inverse else
                                     f'{cfg.name}: cFlow.call(xy,+1) + log-det + NLL sums, xy {list(cfg.io_shape)}, ')
                                    + (f'{G} images global over {world} GPUs' if scaling == 'strong'
@@ -583,7 +590,8 @@ def main():
                        'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world} (batch shards, '
                                                                           f'1 all-reduce of 5 fp32)',
                        'graph': graph is not None,
-                       'input_noise': ({'alpha': args.noise, 'separate_noise_pass': noise_pass}
+                       'input_noise': ({'alpha': args.noise, 'logit_a': args.logit or None,
+                                        'separate_noise_pass': noise_pass}
                                        if noisy else None)},
             'step_ms_median': round(float(np.median(st_ms)), 4) if st_ms else None,
             'bits_per_dim': round(bpd, 6) if bpd is not None else None,

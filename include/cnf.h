@@ -117,17 +117,19 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux,
                      const float* xy, float* zy, float* logdet_per_image,
                      void* workspace, int B, void* stream);
 
-/* cnf_flow_forward of the training pipeline's noisy input (conv_cINN.py:312-315:
- * instance_noise(xy, alpha) per element, conv_cINN_base_functions.py:635-654):
- * xy_noisy[B,H,W,D] receives alpha xy + (1 - alpha) N(0, 1) -- the Philox stream
- * of cnf_instance_noise(xy, xy_noisy, B*H*W*D, alpha, seed, offset), bit for bit --
- * and zy / logdet_per_image are cnf_flow_forward of it. The noise is applied
- * inside the first coupling layer's gather (no separate pass over xy) when that
- * layer is LDS-resident; otherwise by a cnf_instance_noise pass first. xy_noisy
- * is the xy of the matching cnf_nll call. No two of xy, xy_noisy, zy may alias. */
+/* cnf_flow_forward of the input as the reference's training pipeline prepares it
+ * (conv_cINN.py:246-315): with logit_a in (0, 0.5) the logit map of
+ * preprocess_dataset_class(LOGITS=True, a=logit_a) on the x channels
+ * (conv_cINN_base_functions.py:174-231; 0: none), then instance_noise(., alpha) on every
+ * channel (:635-654, the pipeline's 2 % noise: alpha = 0.98). xy_noisy[B,H,W,D] receives the
+ * prepared input -- bit for bit cnf_logit (x channels) followed by cnf_instance_noise(.,
+ * xy_noisy, B*H*W*D, alpha, seed, offset) -- and zy / logdet_per_image are cnf_flow_forward
+ * of it. The preparation runs inside the first coupling layer's gather (no pass over xy)
+ * when that layer is LDS-resident, otherwise as one pass first. xy_noisy is the xy of the
+ * matching cnf_nll call. No two of xy, xy_noisy, zy may alias. */
 int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux,
-                           const float* xy, float alpha, uint64_t seed, uint64_t offset,
-                           float* xy_noisy, float* zy, float* logdet_per_image,
+                           const float* xy, float logit_a, float alpha, uint64_t seed,
+                           uint64_t offset, float* xy_noisy, float* zy, float* logdet_per_image,
                            void* workspace, int B, void* stream);
 
 /* cFlow.call(zy, direction=-1) (:1774-1798): zy -> xy (must not alias). */

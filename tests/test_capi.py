@@ -252,10 +252,13 @@ def test_forward_rejects_aliased_xy_zy(lib):
         assert lib.cnf_flow_forward_train(p, a, a, b, b, a, a, 2, None) == -1
         c = 3 << 40
         # the noisy-input forward: xy, xy_noisy and zy pairwise distinct
-        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.98, 1, 0, b, c, a, a, 2, None) == -1
-        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.98, 1, 0, c, c, a, a, 2, None) == -1
-        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.98, 1, 0, c, b, a, a, 2, None) == -1
+        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.0, 0.98, 1, 0, b, c, a, a, 2, None) == -1
+        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.0, 0.98, 1, 0, c, c, a, a, 2, None) == -1
+        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.0, 0.98, 1, 0, c, b, a, a, 2, None) == -1
         assert b'alias' in lib.cnf_last_error()
+        d = 4 << 40
+        assert lib.cnf_flow_forward_noise(p, a, a, b, 0.7, 0.98, 1, 0, c, d, a, a, 2, None) == -1   # logit_a
+        assert b'logit_a' in lib.cnf_last_error()
     finally:
         lib.cnf_plan_destroy(p)
 

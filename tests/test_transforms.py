@@ -125,15 +125,18 @@ def test_instance_noise_formula_and_moments(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('name,B', [('cfg2', 3), ('small', 2), ('cfg4', 1)])
-def test_noise_fused_into_the_forward(gpu, name, B):
-    """cnf_flow_forward_noise (cFlow.call(noise=...)): the training pipeline's 2 % instance noise
-    (conv_cINN.py:312-315; conv_cINN_base_functions.py:635-654) applied inside the first coupling
-    layer's k_net_lds gather (cfg2, small: no separate pass over xy; cfg4's first layer is streamed:
-    a cnf_instance_noise pass first). The noisy input equals the standalone cnf_instance_noise stream
-    bit for bit, zy / log-det equal cnf_flow_forward of it bit for bit, the loss is that of the noisy
-    input, and zy matches the float64 oracle composed with the oracle-side noisy input."""
-    from arl_conditional_normalizing_flows_amd.base_functions import instance_noise
+@pytest.mark.parametrize('name,B,logit_a', [('cfg2', 3, 0.0), ('cfg2', 2, 0.01), ('small', 2, 0.05), ('cfg4', 1, 0.0),
+                                            ('cfg4', 1, 0.01)])
+def test_noise_fused_into_the_forward(gpu, name, B, logit_a):
+    """cnf_flow_forward_noise (cFlow.call(noise=...)): the input as the reference's training pipeline
+    prepares it (conv_cINN.py:246-315) -- the logit map on the x channels (logit_a > 0,
+    conv_cINN_base_functions.py:174-231), then the 2 % instance noise (:635-654) -- applied inside the
+    first coupling layer's k_net_lds gather (cfg2, small: no pass over xy; cfg4's first layer is
+    streamed: one k_prep pass first). The prepared input equals cnf_logit (x channels) followed by the
+    standalone cnf_instance_noise stream bit for bit, zy / log-det equal cnf_flow_forward of it bit for
+    bit, the loss is that of the prepared input, the logit map matches the numpy oracle, and zy matches
+    the float64 oracle composed with the prepared input."""
+    from arl_conditional_normalizing_flows_amd.base_functions import instance_noise, preprocess_dataset_class
     from arl_conditional_normalizing_flows_amd.config import PRESETS
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
     from oracle.cflow_np import OracleCFlow, synthetic_class_batch
@@ -144,10 +147,19 @@ def test_noise_fused_into_the_forward(gpu, name, B):
     P = ora.init_params(2)
     flow.set_weights(P)
     H, W, _ = cfg.io_shape
-    x = torch.from_numpy(synthetic_class_batch(B, H, W, cfg.x_d, seed=4)).to(gpu)
-    noise = (0.98, 1234567, 99)
+    xy = synthetic_class_batch(B, H, W, cfg.x_d, seed=4)
+    if logit_a:   # the logit map takes the raw images in [0, 1] (the pipeline's noise comes after it)
+        xy[..., :cfg.x_d] = np.clip(xy[..., :cfg.x_d], 0.0, 1.0)
+    x = torch.from_numpy(xy).to(gpu)
+    noise = (0.98, 1234567, 99, logit_a)
     zy, ld, xn = flow(x, 1, per_image_logdet=True, noise=noise)
-    xn_ref = instance_noise(x, *noise)
+    xp = x
+    if logit_a:
+        xl = preprocess_dataset_class(x[..., :cfg.x_d], LOGITS=True, a=logit_a)
+        xl_np = T.logit_preprocess(x[..., :cfg.x_d].cpu().double().numpy(), logit_a)
+        assert np.max(np.abs(xl.cpu().numpy() - xl_np)) < 2e-6
+        xp = torch.cat([xl, x[..., cfg.x_d:]], dim=-1).contiguous()
+    xn_ref = instance_noise(xp, *noise[:3])
     zy_ref, ld_ref = flow(xn_ref, 1, per_image_logdet=True)
     lf = flow.log_loss(x, noise=noise)
     lr = flow.log_loss(xn_ref)
