@@ -254,18 +254,30 @@ __device__ __forceinline__ void ln_fold_first(const f4 v, float& n, float& m, fl
         n = v[3];
     }
 }
-// Split form of in_ln for prologues: in_ln_fetch issues the lane's first partial-slot load early
-// (with the prologue's other global loads, so they share one memory round trip), in_ln_finish folds
-// it and any further slots. in_ln is in_ln_fetch + in_ln_finish, so an image's (mean, rstd) are the
-// same bits whichever form computes them: the form depends on the image's position in its
-// workgroup's image set, i.e. on the batch size (the round-4 batch dependence: ln_fold of the first
-// slot into the empty state and this path contracted differently).
-__device__ __forceinline__ f4 in_ln_fetch(const ConvProb& P, int img) {
+// Split form of in_ln for prologues: in_ln_fetch issues the lane's first LN_FETCH partial-slot loads
+// early (slots lane, lane + 64, ...: with the prologue's other global loads, so they share one memory
+// round trip), in_ln_finish folds them and any further slots. in_ln is in_ln_fetch + in_ln_finish, so
+// an image's (mean, rstd) are the same bits whichever form computes them: the form depends on the
+// image's position in its workgroup's image set, i.e. on the batch size (the round-4 batch
+// dependence: ln_fold of the first slot into the empty state and this path contracted differently).
+// Producers of up to 64 * LN_FETCH slots per image (the 64x64 layers' 256) need no k_ln_merge launch.
+constexpr int LN_FETCH = 4;
+struct LnSlots {
+    f4 v[LN_FETCH];
+};
+__device__ __forceinline__ LnSlots in_ln_fetch(const ConvProb& P, int img) {
     const int lane = threadIdx.x & 63;
-    if (P.in_part == nullptr || lane >= P.in_nparts) return f4{0.f, 0.f, 0.f, 0.f};
-    return *reinterpret_cast<const f4*>(P.in_part + ((size_t)img * P.part_stride + lane) * LNP);
+    LnSlots s;
+#pragma unroll
+    for (int k = 0; k < LN_FETCH; k++) {
+        const int i = lane + 64 * k;
+        s.v[k] = P.in_part != nullptr && i < P.in_nparts
+                     ? *reinterpret_cast<const f4*>(P.in_part + ((size_t)img * P.part_stride + i) * LNP)
+                     : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    return s;
 }
-__device__ __forceinline__ void in_ln_finish(const ConvProb& P, int img, const f4 v, float& mu, float& rstd) {
+__device__ __forceinline__ void in_ln_finish(const ConvProb& P, int img, const LnSlots& s, float& mu, float& rstd) {
     mu = 0.f;
     rstd = 1.f;
     if (P.in_part == nullptr) return;
@@ -273,9 +285,11 @@ __device__ __forceinline__ void in_ln_finish(const ConvProb& P, int img, const f
     return;
 #endif
     float n, m, M2;
-    ln_fold_first(v, n, m, M2);
+    ln_fold_first(s.v[0], n, m, M2);
+#pragma unroll
+    for (int k = 1; k < LN_FETCH; k++) ln_fold(s.v[k], n, m, M2);   // (empty slots: v[3] == 0, skipped)
     const float* __restrict__ q = P.in_part + (size_t)img * P.part_stride * LNP;
-    for (int i = (threadIdx.x & 63) + 64; i < P.in_nparts; i += 64) {
+    for (int i = (threadIdx.x & 63) + 64 * LN_FETCH; i < P.in_nparts; i += 64) {
         const f4 w = *reinterpret_cast<const f4*>(q + (size_t)LNP * i);
         ln_fold(w, n, m, M2);
     }

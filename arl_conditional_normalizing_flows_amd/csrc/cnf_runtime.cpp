@@ -750,14 +750,15 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // a producing launch reports the partial slots it wrote per image (set_parts); in_slab hands
     // that count on to the consumer
     auto out_slab = [&](int n, int k, int) { return ln ? sl[n][k] : Slab{}; };
-    // more slots than one consumer wave folds in a pass (the 64x64 and 128x128 layers): merged once
-    // per image by k_ln_merge instead of by every consumer workgroup for each of its images
-    static const bool ln_merge = [] {   // A/B knob
+    // more slots than a consumer wave fetches in its prologue (64 x LN_FETCH = 256: the 128x128 layers):
+    // merged once per image by k_ln_merge instead of by every consumer workgroup for each of its images
+    // (the 64x64 layers' 256 slots are folded by the consumers: 58 fewer launches per cfg4 step)
+    static const int ln_merge_over = [] {   // A/B knob: CNF_LN_MERGE=0 never merges, =64 the round-4 rule
         const char* e = std::getenv("CNF_LN_MERGE");
-        return !(e && std::atoi(e) == 0);
+        return e ? (std::atoi(e) == 0 ? 1 << 30 : std::atoi(e)) : 256;
     }();
     auto set_parts = [&](int k, int nparts) {
-        if (ln && ln_merge && nparts > 64) {
+        if (ln && nparts > ln_merge_over) {
             float* p0 = sl[0][k].part;
             float* p1 = sl[1][k].part;
             const int np = nparts, ps = L.st_parts;

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
     // the first image of this wave's LN-statistics share: its partial slots fetched now, in the same
     // memory round trip as the loads above and the weights below (folded after the weight copy)
     const bool lnpre = LN && wave < nimg;   // (image wave: the LN table below is per workgroup)
-    const f4 slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
+    const LnSlots slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : LnSlots{};
     // the rest of the ring's first images: in flight with the prologue's loads (CNF_PW_EARLY) or
     // issued once the weights are in LDS
     if (CNF_PW_EARLY) {
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     lnP.in_nparts = a.in_nparts;
     lnP.part_stride = a.part_stride;
     const bool lnpre = ln && wave < nimg;
-    const f4 slot0 = lnpre ? in_ln_fetch(lnP, img0 + wave) : f4{0.f, 0.f, 0.f, 0.f};
+    const LnSlots slot0 = lnpre ? in_ln_fetch(lnP, img0 + wave) : LnSlots{};
     // packed weights and quad-offset tables of every branch (once per workgroup)
     for (int bi = 0; bi < GS(nbr); bi++) {
         const GcBranch& br = GS(br)[bi];
