@@ -348,6 +348,78 @@ def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
         dist.destroy_process_group()
 
 
+def serving_inflight(flow, lib, xy, B, nl, steps, dev, noise=None, logit=0.0):
+    """Serving throughput with nl batches in flight: nl lanes (own workspace, input copy, outputs,
+    HIP stream and captured graph of one step: forward + log-det + NLL sums of B images), steps
+    issued round-robin over the lanes, K steps timed between two synchronisations. One batch's
+    k_net_lds layers (128 workgroups at B=64: half the CUs) and kernel prologues / tails then overlap
+    another batch's kernels. Per-batch latency: the median event time of one lane's step while the
+    other lanes run."""
+    lanes = []
+    for i in range(nl):
+        L = {'xy': xy.clone(), 'zy': torch.empty_like(xy), 'ld': torch.empty(B, device=dev),
+             'per': torch.empty((B, 3), device=dev), 'sums': torch.empty(4, device=dev),
+             'ws': torch.empty(int(lib.cnf_plan_workspace_bytes(flow._plan, B)), device=dev, dtype=torch.uint8),
+             's': torch.cuda.Stream(device=dev)}
+        L['xn'] = torch.empty_like(xy) if noise is not None else L['xy']
+
+        def step(L=L):
+            st = torch.cuda.current_stream().cuda_stream
+            if noise is not None:
+                _lib.check(lib.cnf_flow_forward_noise(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
+                                                      L['xy'].data_ptr(), float(logit), float(noise), 2000 + i, 0,
+                                                      L['xn'].data_ptr(), L['zy'].data_ptr(), L['ld'].data_ptr(),
+                                                      L['ws'].data_ptr(), B, st), 'forward')
+            else:
+                _lib.check(lib.cnf_flow_forward(flow._plan, flow.params.data_ptr(), flow._aux.data_ptr(),
+                                                L['xy'].data_ptr(), L['zy'].data_ptr(), L['ld'].data_ptr(),
+                                                L['ws'].data_ptr(), B, st), 'forward')
+            _lib.check(lib.cnf_nll(flow._plan, L['xn'].data_ptr(), L['zy'].data_ptr(), L['ld'].data_ptr(),
+                                   L['per'].data_ptr(), L['sums'].data_ptr(), B, st), 'nll')
+        with torch.cuda.stream(L['s']):
+            step()
+        torch.cuda.synchronize()
+        L['g'] = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(L['g'], stream=L['s']):
+            step()
+        lanes.append(L)
+    torch.cuda.synchronize()
+
+    def issue(k):
+        L = lanes[k % nl]
+        with torch.cuda.stream(L['s']):
+            L['g'].replay()
+    for k in range(4 * nl):
+        issue(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        issue(k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # latency of one batch with the others in flight: events around lane 0's steps
+    evs = []
+    for k in range(nl * 20):
+        L = lanes[k % nl]
+        with torch.cuda.stream(L['s']):
+            if k % nl == 0:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                L['g'].replay()
+                b.record()
+                evs.append((a, b))
+            else:
+                L['g'].replay()
+    torch.cuda.synchronize()
+    lat = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    ok = all(torch.equal(L['sums'], lanes[0]['sums']) for L in lanes[1:]) if noise is None else True
+    return {'batches_in_flight': nl, 'value': round(B * steps / el, 2), 'unit': 'images/s', 'steps': steps,
+            'ms_per_step': round(el / steps * 1e3, 4), 'batch_latency_ms_median': round(lat, 4),
+            'lanes_bitwise_equal': ok,
+            'note': 'each step = one batch of B images (fwd + log-det + NLL sums), steps round-robin over '
+                    'nl HIP streams with their own workspaces and captured graphs'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -371,6 +443,10 @@ def main():
     ap.add_argument('--logit', type=float, default=0.0, metavar='A',
                     help='with --noise: the logit preprocess (preprocess_dataset_class(LOGITS=True, a=A), '
                          'conv_cINN_base_functions.py:174-231) on the x channels first, fused likewise')
+    ap.add_argument('--inflight', type=int, default=2,
+                    help='also measure serving throughput with this many batches (of the same size) in flight on '
+                         'as many HIP streams, each its own captured step (reported as "serving"; `value` is one '
+                         'batch in flight); 1: skip')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
@@ -465,6 +541,12 @@ def main():
         if os.environ.get('CNF_BENCH_VERBOSE'):
             print(f'# rank {rank}: {msg}', file=sys.stderr, flush=True)
 
+    serving = None
+    if world == 1 and not inverse and args.inflight > 1:
+        # first, on a fresh runtime: after hipExtLaunchKernelGGL with events (measure_in_stream), or
+        # once the step graph has run on the default stream, the runtime serialises the lanes'
+        # streams (measured in profiles/diag/diag_serving.py: 59.1k -> 43.3k images/s)
+        serving = serving_inflight(flow, lib, xy, B, args.inflight, max(args.steps, 50), dev, args.noise, args.logit)
     note('first step')
     step()
     note('first step done')
@@ -600,6 +682,7 @@ def main():
             'roofline': roof,
             'step_roofline': step_roof,
             'cpu_baseline': cpu,
+            'serving': serving,
         }
         if cpu and cpu.get('bits_per_dim_ref') is not None and world == 1:
             out['bits_per_dim_ref'] = round(cpu['bits_per_dim_ref'], 6)
