@@ -260,8 +260,8 @@ __device__ __forceinline__ void ln_fold_first(const f4 v, float& n, float& m, fl
 // an image's (mean, rstd) are the same bits whichever form computes them: the form depends on the
 // image's position in its workgroup's image set, i.e. on the batch size (the round-4 batch
 // dependence: ln_fold of the first slot into the empty state and this path contracted differently).
-// Producers of up to 64 * LN_FETCH slots per image (the 64x64 layers' 256) need no k_ln_merge launch.
-constexpr int LN_FETCH = 4;
+// Producers of up to 64 * LN_FETCH slots per image (the 64x64 layers' k_gc groups) need no k_ln_merge
+// (LN_FETCH: cnf_kernels.h).
 struct LnSlots {
     f4 v[LN_FETCH];
 };

@@ -16,6 +16,9 @@ constexpr double LOG_2PI_D = 1.8378770664093453;
 // LayerNorm statistics partial of one producing wave: (K, S1, S2, n) with S1 = sum(x - K),
 // S2 = sum((x - K)^2) over its n values of LeakyReLU(out), K a sample of them (fp32, 16 bytes)
 constexpr int LNP = 4;
+// LN partial slots per image a consumer wave folds from its prologue loads, per lane (cnf_device.h
+// in_ln_fetch); producers of more than 64 * LN_FETCH slots get a k_ln_merge launch (cnf_runtime.cpp)
+constexpr int LN_FETCH = 8;
 
 constexpr int MAXPROB = 12;
 

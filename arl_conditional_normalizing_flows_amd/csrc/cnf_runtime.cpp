@@ -750,12 +750,12 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // a producing launch reports the partial slots it wrote per image (set_parts); in_slab hands
     // that count on to the consumer
     auto out_slab = [&](int n, int k, int) { return ln ? sl[n][k] : Slab{}; };
-    // more slots than a consumer wave fetches in its prologue (64 x LN_FETCH = 256: the 128x128 layers):
+    // more slots than a consumer wave fetches in its prologue (64 x LN_FETCH = 512: the 128x128 layers):
     // merged once per image by k_ln_merge instead of by every consumer workgroup for each of its images
-    // (the 64x64 layers' 256 slots are folded by the consumers: 58 fewer launches per cfg4 step)
+    // (the 64x64 layers' slots are folded by the consumers: 70 fewer launches per cfg4 step)
     static const int ln_merge_over = [] {   // A/B knob: CNF_LN_MERGE=0 never merges, =64 the round-4 rule
         const char* e = std::getenv("CNF_LN_MERGE");
-        return e ? (std::atoi(e) == 0 ? 1 << 30 : std::atoi(e)) : 256;
+        return e ? (std::atoi(e) == 0 ? 1 << 30 : std::atoi(e)) : 64 * LN_FETCH;
     }();
     auto set_parts = [&](int k, int nparts) {
         if (ln && nparts > ln_merge_over) {

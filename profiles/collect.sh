@@ -13,7 +13,7 @@ root=$PWD
 out=$root/gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
-B="$root/bench.py --no-cpu-baseline --no-roofline"
+B="$root/bench.py --no-cpu-baseline --no-roofline --inflight 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o run -- python3 $B --steps 20 --warmup 5 > $out/stats.log 2>&1 || { echo "stats pass failed"; tail $out/stats.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $out/fetch -o run -- python3 $B --steps 3 --warmup 1 --no-graph > $out/fetch.log 2>&1 || { echo "fetch pass failed"; tail $out/fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $out/write -o run -- python3 $B --steps 3 --warmup 1 --no-graph > $out/write.log 2>&1 || { echo "write pass failed"; tail $out/write.log; exit 1; }
