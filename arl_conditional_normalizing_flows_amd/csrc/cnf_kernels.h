@@ -108,6 +108,27 @@ struct CoupArgs {
     float* so_w[2];
 };
 
+// Streamed conv_out and the coupling law in one launch (k_out_law, cnf_kernels.hip): one workgroup
+// per (image, TR x TW tile of compressed pixels) stages LN_out(LReLU(y)) of both nets over the tile
+// and its 1-pixel halo in LDS, runs the two 3x3 convs (nk -> dc2) on the vector ALUs and applies the
+// affine law to the tile's pixels (the tile is the log-det slot). Replaces the tap-GEMM k_pw + k_coupling
+// pair of the streamed layers whose conv_out is in tap format — opt-in (CNF_OUT_LAW=1): measured
+// slower (cfg2: 28 us against 12.3 + 7.2 us; every workgroup re-reads the per-element LN gamma / beta
+// and the halo rows through its CU's L1, 3x the pair's bytes into the CUs).
+struct OutLawArgs {
+    ConvProb p[2];             // per net: in = y, in_part / in_nparts / part_stride (LN_out), gamma, beta
+    const float* w[2];         // raw conv_out kernels [3][3][nk][dc2] (params)
+    const float* b[2];         // [dc2]
+    float* so_w[2];            // raw conv_out of each net, [B][hc][wc][dc2] (s pre-tanh / t)
+    const float* u;
+    float* v;
+    const float* tanh_w;
+    double* ld_part;           // [B][np] or null
+    int H, W, D, mask, mask_c, hc, wc, dc1, dc2, dir;
+    int TR, TW, tiles_r, tiles_c, np;
+    uint32_t tw_mag, twp_mag;  // magic divisors (cnf_device.h udiv) for TW and TW + 2
+};
+
 // Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).
 constexpr int NETLDS_MAXBR = 8;
 #ifndef CNF_NETLDS_OTAB
@@ -342,6 +363,11 @@ void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hi
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st);
+// k_out_law over B * tiles_r * tiles_c workgroups: nk == 64, dc2 <= 3 (the tap-format layers of the presets), ks = 128 / (TR * TW) in {1, 2}
+// (K split over ks waves per net); returns false for a shape it has no instantiation for
+bool out_law_supported(int nk, int dc2, int TR, int TW);
+size_t out_law_lds_bytes(int dc2, int TR, int TW);
+void launch_out_law(const OutLawArgs& a, int B, hipStream_t st);
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st);
 // LN partial slots [B][part_stride][LNP] of one tensor (two nets: part0, part1 or null) merged into
 // slot 0 of each image (k_ln_merge): consumers then read nparts = 1

@@ -107,6 +107,38 @@ static ConvGeom1 conv1_geo(int h, int w) {
 // largest layers run one element per thread (latency-bound otherwise)
 static int ld_parts_for(int npx) { return std::max(1, std::min(16, (npx + 63) / 64)); }
 
+static uint32_t udiv_magic_host(uint32_t d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }   // cnf_device.h udiv
+
+// k_out_law tile (TR rows x TW columns of compressed pixels) of a streamed layer with a tap-format
+// conv_out, or false (tap GEMM + k_coupling): 64-pixel tiles (K split over two waves per net) first,
+// then 128-pixel tiles, as long as the image's tiles fit its np log-det slots. Opt-in, CNF_OUT_LAW=1
+// (measured slower than the pair, see cnf_kernels.h OutLawArgs); CNF_OUT_LAW_KS=1 / 2: only 128- /
+// 64-pixel tiles
+static bool out_law_tiles(const Coupling& c, int np, int& TR, int& TW) {
+    static const int mode = [] {
+        const char* e = std::getenv("CNF_OUT_LAW");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const int force_ks = [] {
+        const char* e = std::getenv("CNF_OUT_LAW_KS");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (mode == 0) return false;
+    for (int ks = 2; ks >= 1; ks--) {
+        if (force_ks != 0 && ks != force_ks) continue;
+        const int cap = 128 / ks;
+        const int tw = std::min(c.wc, 32);
+        const int tr = std::max(1, cap / tw);
+        if (tr * tw > cap) continue;
+        const int tiles = ((c.hc + tr - 1) / tr) * ((c.wc + tw - 1) / tw);
+        if (tiles > np || !out_law_supported(c.nk, c.dc2, tr, tw)) continue;
+        TR = tr;
+        TW = tw;
+        return true;
+    }
+    return false;
+}
+
 WsLayout Plan::layout(int B) const {
     WsLayout L;
     int64_t n_uv = (int64_t)desc.io_h * desc.io_w * desc.io_d;
@@ -1007,6 +1039,54 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + np.ln_out_g : none,
                                   ln ? P + np.ln_out_b : none, 1, X + np.co.w, X + np.co.b, so[n], c.dc2, 0, c.dc2,
                                   none, Slab{}, 0, 1});
+        }
+        int otr = 0, otw = 0;
+        if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2 && !defer &&
+            out_law_tiles(c, L.ld_parts, otr, otw)) {
+            // conv_out and the law in one k_out_law launch (no tap planes, no k_coupling)
+            OutLawArgs oa;
+            std::memset(&oa, 0, sizeof(oa));
+            for (int n = 0; n < 2; n++) {
+                const NetParams& np = c.net[n];
+                ConvProb& q = oa.p[n];
+                const Slab s = in_slab(n, 0);
+                q.in = y[n];
+                q.in_part = s.part;
+                q.in_nparts = s.nparts;
+                q.part_stride = L.st_parts;
+                q.gamma = ln ? P + np.ln_out_g : none;
+                q.beta = ln ? P + np.ln_out_b : none;
+                oa.w[n] = P + np.conv_out_k;
+                oa.b[n] = P + np.conv_out_b;
+                oa.so_w[n] = n == 0 ? so0 : so1;
+            }
+            oa.u = u;
+            oa.v = v;
+            oa.tanh_w = P + c.net[0].tanh_w;
+            oa.ld_part = ld_part;
+            oa.H = c.H;
+            oa.W = c.W;
+            oa.D = c.D;
+            oa.mask = c.mask;
+            oa.mask_c = c.mask_c;
+            oa.hc = c.hc;
+            oa.wc = c.wc;
+            oa.dc1 = c.dc1;
+            oa.dc2 = c.dc2;
+            oa.dir = dir;
+            oa.TR = otr;
+            oa.TW = otw;
+            oa.tiles_r = (c.hc + otr - 1) / otr;
+            oa.tiles_c = (c.wc + otw - 1) / otw;
+            oa.np = L.ld_parts;
+            oa.tw_mag = udiv_magic_host((uint32_t)otw);
+            oa.twp_mag = udiv_magic_host((uint32_t)otw + 2);
+            const double npx = (double)c.hc * c.wc;
+            const double fl = 2.0 * B * npx * 9.0 * c.nk * c.dc2 * 2;
+            const double by = 4.0 * (B * (npx * c.nk * 2 + 2.0 * c.H * c.W * c.D + 2 * npx * c.dc2) +
+                                     (ln ? 4.0 * npx * c.nk : 0.0));
+            E.record("k_out_law", fl, by, [oa, B](void* st) { launch_out_law(oa, B, (hipStream_t)st); });
+            return;
         }
         if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2) {
             // tap GEMM C = LN_out(LReLU(y)) . W_tap as a streamed 1x1 conv into the dead t1 buffer;

@@ -48,7 +48,7 @@ def make_lane(seed):
     with torch.cuda.graph(g, stream=s):
         step()
     torch.cuda.synchronize()
-    return g, s, sums
+    return g, s, step
 
 
 # CNF_DIAG_DUMMY_STREAMS=n: create n streams first (HIP maps streams onto GPU_MAX_HW_QUEUES hardware
@@ -76,6 +76,37 @@ def run(nl, iters, offset_us=0):
     torch.cuda.synchronize()
     return time.perf_counter() - t0
 
+
+def round_graph(nl):
+    """one captured graph of a whole round: the capture stream forks to the nl lane streams and
+    joins them (does graph replay keep the branches concurrent?)"""
+    s0 = torch.cuda.Stream(device=dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s0):
+        for _, s, step in lanes[:nl]:
+            s.wait_stream(s0)
+            with torch.cuda.stream(s):
+                step()
+        for _, s, _ in lanes[:nl]:
+            s0.wait_stream(s)
+    torch.cuda.synchronize()
+    return g, s0
+
+
+if os.environ.get('CNF_DIAG_ROUND_GRAPH') == '1':
+    for nl in (1, 2, 3):
+        g, s0 = round_graph(nl)
+        for it in (10, K):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            with torch.cuda.stream(s0):
+                for _ in range(it):
+                    g.replay()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+        print(f'{name} B={B}: round graph of {nl} lane(s): {nl * B * K / el:9.1f} images/s, '
+              f'{el / K * 1e3:.3f} ms per round', flush=True)
+    sys.exit(0)
 
 offsets = [int(v) for v in os.environ.get('CNF_DIAG_OFFSETS', '0').split(',')]
 for nl in (1, 2, 3):
