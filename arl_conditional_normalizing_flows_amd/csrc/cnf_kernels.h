@@ -483,6 +483,11 @@ bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO);
 // taps 1 / 9; its partial-row count (<= WGRAD_MAX_CHUNKS) for a batch of B images of H rows
 bool wgrad_direct_ok(int H, int W, int taps);
 int wgrad_direct_chunks(int B, int H);
+// k_wgrad_thin (3x3, dilation 1, CO <= 4, CI <= 64, CI % 4 == 0: the streamed conv_out's weight
+// gradient): one partial row [taps][CI][CO] + [CO] per workgroup, wgrad_thin_chunks of them
+bool wgrad_thin_ok(int H, int W, int taps, int dil, int CI, int CO);
+int wgrad_thin_chunks(int B, int H, int W);
+void launch_wgrad_thin(const WGradArgs& a, hipStream_t st);
 // dparams[map[i]] += sum_c part[c][i] for i < n (map[i] >= 0)
 void launch_grad_scatter(const float* part, int chunks, long long n, const int64_t* map, float* dparams, hipStream_t st);
 void launch_ln_stats(const float* x, long long n, int B, int act, float* stats, hipStream_t st);

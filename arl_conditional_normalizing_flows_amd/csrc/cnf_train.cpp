@@ -446,6 +446,13 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
         launch_grad_scatter(a.bpart, a.chunks, cout, map + pc.db, E.dparams, E.st);
         return nullptr;
     }
+    // thin outputs (the streamed conv_out, CO = dc2): k_wgrad_thin, rows of [weights | bias] as below
+    if ((long long)h * w * x_cs * 4 < (1LL << 31) && wgrad_thin_ok(h, w, pc.taps, dil, cin, cout) && pc.db == pc.dw + nw) {
+        a.chunks = wgrad_thin_chunks(E.B, h, w);
+        launch_wgrad_thin(a, E.st);
+        launch_grad_scatter(a.part, a.chunks, nw + cout, map + pc.dw, E.dparams, E.st);
+        return nullptr;
+    }
     // k_wgrad_direct (k_wgrad_band with CNF_WGRAD_DIRECT=0): rows of [weights | bias]; the dense image
     // keeps the bias right after the weights (pc.db == pc.dw + taps * cin * cout), so one scatter
     // reduces both

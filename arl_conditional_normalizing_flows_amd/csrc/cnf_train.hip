@@ -582,6 +582,117 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
     if (lnr) lnr_finish(a, sg, sgh, b);
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_tconv_thin: a 3x3 (dilation 1) convolution with K <= 4 input channels, forward or transposed, no
+// LN on load: the streamed conv_out's data gradient (K = dc2 -> N = nk, with the fused LN_out
+// reduction) and conv_in's forward recompute (K = dc1). The MFMA kernels pad such a K to a 16-wide
+// group and stage per-tap weights for 2 useful channels; here a workgroup owns TR full rows
+// (TR * W <= 64 pixels at N = 64) of one image, stages the K-channel band (1-pixel halo, zeros
+// outside) and the 9 * K * N weights in LDS; each thread computes up to 4 pixels x 4 channels on the
+// vector ALUs (tap outer: one weight quad read per tap and k), then issues every epilogue load (residual / previous
+// output / the LN reduction's raw input and gamma) before its float4 stores.
+// ------------------------------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256, 2) void k_tconv_thin(TConvArgs a, int TR) {
+    extern __shared__ __attribute__((aligned(16))) float tsm[];
+    constexpr int PX = 4;   // pixels per thread (TR * W <= 4 * 256 / (N / 4))
+    const int H = a.H, W = a.W, npx = H * W, b = blockIdx.y, N = a.N;
+    const int r0 = blockIdx.x * TR, BW = W + 2, BH = TR + 2;
+    const int nb = (BH * BW * K + 3) & ~3;
+    float* ws = tsm + nb;   // [tap][k][N] weights
+    const float* inb = a.in + (size_t)b * npx * a.in_cs + a.in_off;
+    for (int e = threadIdx.x; e < BH * BW * K; e += 256) {
+        const int pb = e / K, k = e - pb * K;
+        const int br = pb / BW, bc = pb - br * BW;
+        const int r = r0 - 1 + br, c = bc - 1;
+        float v = 0.f;
+        if (r >= 0 && r < H && c >= 0 && c < W) {
+            v = inb[(size_t)(r * W + c) * a.in_cs + k];
+            if (a.act) v = lrelu(v);
+        }
+        tsm[e] = v;
+    }
+    for (int e = threadIdx.x; e < 9 * K * N; e += 256) {
+        const int tk = e / N, n = e - tk * N, tap = tk / K, k = tk - tap * K;
+        ws[e] = a.w[tap * a.wt + (long long)k * a.wk + (long long)n * a.wn];
+    }
+    const int NQ = N >> 2, PS = 256 / NQ;
+    const int qd = threadIdx.x % NQ, ps = threadIdx.x / NQ, n0 = 4 * qd;
+    f4 bias = f4{0.f, 0.f, 0.f, 0.f};
+    if (a.bias)
+#pragma unroll
+        for (int j = 0; j < 4; j++) bias[j] = a.bias[n0 + j];
+    const int ntp = min(TR, H - r0) * W;   // this tile's pixels
+    int xo[PX], ob[PX];   // band float offset of the pixel (tap (1, 1)); output float offset
+    f4 acc[PX];
+#pragma unroll
+    for (int i = 0; i < PX; i++) {
+        const int px = min(ps + PS * i, ntp - 1);
+        const int pr = px / W, pc = px - pr * W;
+        xo[i] = ((pr + 1) * BW + pc + 1) * K;
+        ob[i] = ((b * npx + (r0 + pr) * W + pc) * a.out_cs + a.out_off + n0);
+        acc[i] = bias;
+    }
+    __syncthreads();
+    // tap outer, pixels inner: each weight quad is read from LDS once per thread
+#pragma unroll
+    for (int tap = 0; tap < 9; tap++) {
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        const int toff = (a.sgn * dr * BW + a.sgn * dc) * K;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const f4 wq = *reinterpret_cast<const f4*>(ws + (tap * K + k) * N + n0);
+#pragma unroll
+            for (int i = 0; i < PX; i++) {
+                const float x = tsm[xo[i] + toff + k];
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[i][j] = fmaf(x, wq[j], acc[i][j]);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one tap's LDS reads live at a time (else all 9 are hoisted)
+    }
+    const bool lnr = a.lnr_part != nullptr;
+    // (gamma lives in the parameter vector at any float offset: a 16-byte buffer load needs 4-byte
+    // alignment only)
+    const __amdgpu_buffer_rsrc_t rlg = buf_rsrc(lnr ? a.lnr_gamma : a.out, (uint32_t)(npx * a.out_cs) * 4u);
+    // (out-of-tile slots were clamped to the tile's last pixel above: every load is in range, only the
+    // stores and the sums are predicated — no control flow around the per-pixel arrays)
+    f4 lx[PX], lg[PX];
+#pragma unroll
+    for (int i = 0; i < PX; i++) {
+        if (a.res) acc[i] += *reinterpret_cast<const f4*>(a.res + ob[i]);
+        if (a.accumulate) acc[i] += *reinterpret_cast<const f4*>(a.out + ob[i]);
+        if (lnr) {
+            lx[i] = *reinterpret_cast<const f4*>(a.lnr_x + ob[i]);
+            lg[i] = buf_load4(rlg, (uint32_t)(ob[i] - b * npx * a.out_cs) * 4u);
+        }
+    }
+    const float lmu = lnr ? a.lnr_stats[2 * b] : 0.f, lrs = lnr ? a.lnr_stats[2 * b + 1] : 0.f;
+    double sg = 0.0, sgh = 0.0;
+#pragma unroll
+    for (int i = 0; i < PX; i++) {
+        const bool ok = ps + PS * i < ntp;
+        const f4 v = acc[i];
+        if (ok) *reinterpret_cast<f4*>(a.out + ob[i]) = v;
+        if (lnr)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float g = ok ? v[j] * lg[i][j] : 0.f, xh = (lrelu(lx[i][j]) - lmu) * lrs;
+                sg += g;
+                sgh += (double)g * xh;
+            }
+    }
+    if (lnr) lnr_finish(a, sg, sgh, b);
+}
+
+static bool tconv_thin_on() {   // A/B knob: CNF_TCONV_THIN=0 sends the thin-K convolutions to the MFMA kernels
+    static const bool v = [] {
+        const char* e = std::getenv("CNF_TCONV_THIN");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (read per call: tests switch it)
     const char* e = std::getenv("CNF_TRAIN_VALU");
     return e && std::atoi(e) != 0;
@@ -600,6 +711,26 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
         const char* e = std::getenv("CNF_TCONV_BAND");
         return e && std::atoi(e) == 0;
     }();
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!train_valu() && tconv_thin_on() && a.taps == 9 && a.dil == 1 && a.K >= 1 && a.K <= 4 &&
+        a.stats == nullptr && (a.N == 64 || a.N == 32 || a.N == 16) && a.W >= 1 && (a.out_cs & 3) == 0 &&
+        (a.out_off & 3) == 0 && al16(a.out) && (a.res == nullptr || al16(a.res)) &&
+        (a.lnr_part == nullptr || al16(a.lnr_x)) && (long long)a.B * a.H * a.W * a.out_cs < (1LL << 31)) {
+        const int PS = 256 / (a.N / 4);
+        const int TR = std::max(1, std::min(a.H, PS * 4 / a.W));
+        if (TR * a.W <= PS * 4) {
+            const dim3 g((a.H + TR - 1) / TR, a.B, 1), blk(256);
+            const int np = lnr_ok(g);
+            const size_t lds = (((size_t)(TR + 2) * (a.W + 2) * a.K + 3) / 4 * 4 + (size_t)9 * a.K * a.N) * 4;
+            switch (a.K) {
+                case 1: hipLaunchKernelGGL((k_tconv_thin<1>), g, blk, lds, st, a, TR); break;
+                case 2: hipLaunchKernelGGL((k_tconv_thin<2>), g, blk, lds, st, a, TR); break;
+                case 3: hipLaunchKernelGGL((k_tconv_thin<3>), g, blk, lds, st, a, TR); break;
+                default: hipLaunchKernelGGL((k_tconv_thin<4>), g, blk, lds, st, a, TR); break;
+            }
+            return np;
+        }
+    }
     if (!train_valu() && !band_off && a.taps == 9 && a.dil <= 2 && a.W <= 64 && a.W >= 1) {
         const int nr = a.N <= 16 ? 1 : a.N <= 32 ? 2 : a.N <= 48 ? 3 : 4;
         const int NS = 16 * nr;
@@ -1213,6 +1344,152 @@ static void launch_wgrad_direct(const WGradArgs& a, hipStream_t st) {
 #undef CNF_WD_N
 #undef CNF_WD
     throw std::logic_error("k_wgrad_direct: no instantiation for this tiling");
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_wgrad_thin: the weight gradient of a 3x3 (dilation 1) convolution with CO <= 4 outputs and
+// CI <= 64 inputs (the streamed conv_out: LN_out(LeakyReLU(y)), nk channels -> dc2), where the MFMA
+// kernel's 16-wide output tiles are 2/16 used. A workgroup owns TR full rows (<= 128 pixels) of ipw
+// images: per image it stages X over the rows and their 1-pixel halo (LN on load, zeros outside) and
+// dY in LDS; thread (kh, ci) sums the three taps (kh, 0..2) of input channel ci for every output
+// with a sliding window along the row (one LDS read per pixel), CO more threads the bias. One partial
+// row [taps][CI][CO] + [CO] per workgroup (<= WGRAD_MAX_CHUNKS), reduced by k_grad_scatter.
+// ------------------------------------------------------------------------------------------------
+template <int CO>
+__global__ __launch_bounds__(256) void k_wgrad_thin(WGradArgs a, int TR, int ipw, int ntile) {
+    extern __shared__ __attribute__((aligned(16))) float wsm[];
+    const int H = a.H, W = a.W, npx = H * W, CI = a.CI, BW = W + 2, BH = TR + 2, CQ = CI >> 2;
+    float* xs = wsm;                          // [BH * BW][CI]
+    float* ds = wsm + (size_t)BH * BW * CI;   // [TR * W][CO]
+    const int tile = blockIdx.x % ntile, grp = blockIdx.x / ntile;
+    const int r0 = tile * TR, nr = min(TR, H - r0);
+    const int b0 = grp * ipw, b1 = min(a.B, b0 + ipw);
+    const int t = threadIdx.x, ci = t % CI, kh = t / CI;
+    const bool wt = t < 3 * CI, bt = t >= 3 * CI && t < 3 * CI + CO;
+    float acc[3][CO];
+#pragma unroll
+    for (int kw = 0; kw < 3; kw++)
+#pragma unroll
+        for (int co = 0; co < CO; co++) acc[kw][co] = 0.f;
+    float bacc = 0.f;
+    const bool ln = a.stats != nullptr;
+    const int nq = BH * BW * CQ;
+    for (int b = b0; b < b1; b++) {
+        __syncthreads();   // the previous image's reads are done
+        const float mu = ln ? a.stats[2 * b] : 0.f, rs = ln ? a.stats[2 * b + 1] : 1.f;
+        // buffer loads (4-byte alignment: x / gamma / beta windows at any float offset; 0 out of range)
+        const uint32_t xbytes = (uint32_t)(npx * a.x_cs - a.x_off) * 4u;
+        const __amdgpu_buffer_rsrc_t rx = buf_rsrc(a.x + (size_t)b * npx * a.x_cs + a.x_off, xbytes);
+        const __amdgpu_buffer_rsrc_t rg = buf_rsrc(ln ? a.gamma + a.x_off : a.x, xbytes);
+        const __amdgpu_buffer_rsrc_t rb = buf_rsrc(ln ? a.beta + a.x_off : a.x, xbytes);
+        constexpr int U = 8;   // quads per thread and batch (the 32-wide tiles' 3264 quads in two batches)
+        for (int e0 = t; e0 < nq; e0 += 256 * U) {
+            f4 v[U], g[U], bb[U];
+            bool ok[U];
+            uint32_t off[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int e = e0 + 256 * u;
+                const int pb = e / CQ, q = e - pb * CQ;
+                const int br = pb / BW, bc = pb - br * BW;
+                const int r = r0 - 1 + br, c = bc - 1;
+                ok[u] = e < nq && r >= 0 && r < H && c >= 0 && c < W;
+                off[u] = ok[u] ? (uint32_t)((r * W + c) * a.x_cs + 4 * q) * 4u : BUF_OOB;
+                v[u] = buf_load4(rx, off[u]);
+                if (ln) {
+                    g[u] = buf_load4(rg, off[u]);
+                    bb[u] = buf_load4(rb, off[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int e = e0 + 256 * u;
+                if (e >= nq) break;
+                f4 o;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float x = v[u][j];
+                    const float y = ln ? (lrelu(x) - mu) * rs * g[u][j] + bb[u][j] : (a.act ? lrelu(x) : x);
+                    o[j] = ok[u] ? y : 0.f;   // zero padding of the conv input (LN of 0 is not 0)
+                }
+                *reinterpret_cast<f4*>(xs + 4 * e) = o;
+            }
+        }
+        for (int e = t; e < nr * W * CO; e += 256) {
+            const int p = e / CO, co = e - p * CO;
+            ds[e] = a.dy[((size_t)b * npx + (size_t)r0 * W + p) * a.dy_cs + a.dy_off + co];
+        }
+        __syncthreads();
+        if (wt) {
+            for (int pr = 0; pr < nr; pr++) {
+                const float* xr = xs + (size_t)(pr + kh) * BW * CI + ci;
+                const float* dr = ds + (size_t)pr * W * CO;
+                float x0 = xr[0], x1 = xr[CI];
+                for (int pc = 0; pc < W; pc++) {
+                    const float x2 = xr[(pc + 2) * CI];
+#pragma unroll
+                    for (int co = 0; co < CO; co++) {
+                        const float d = dr[pc * CO + co];
+                        acc[0][co] = fmaf(x0, d, acc[0][co]);
+                        acc[1][co] = fmaf(x1, d, acc[1][co]);
+                        acc[2][co] = fmaf(x2, d, acc[2][co]);
+                    }
+                    x0 = x1;
+                    x1 = x2;
+                }
+            }
+        } else if (bt) {
+            const int co = t - 3 * CI;
+            for (int p = 0; p < nr * W; p++) bacc += ds[p * CO + co];
+        }
+    }
+    float* part = a.part + (size_t)blockIdx.x * (9 * CI * CO + CO);
+    if (wt)
+#pragma unroll
+        for (int kw = 0; kw < 3; kw++)
+#pragma unroll
+            for (int co = 0; co < CO; co++) part[((kh * 3 + kw) * CI + ci) * CO + co] = acc[kw][co];
+    if (bt) part[9 * CI * CO + (t - 3 * CI)] = bacc;
+}
+
+static void wgrad_thin_shape(int B, int H, int W, int& TR, int& ipw, int& ntile) {
+    TR = std::max(1, std::min(H, 128 / std::max(1, W)));
+    ntile = (H + TR - 1) / TR;
+    ipw = (B * ntile + WGRAD_MAX_CHUNKS - 1) / WGRAD_MAX_CHUNKS;
+    if (ipw < 1) ipw = 1;
+}
+
+bool wgrad_thin_ok(int H, int W, int taps, int dil, int CI, int CO) {
+    static const bool on = [] {   // A/B knob: CNF_WGRAD_THIN=0 sends them to k_wgrad_direct / k_wgrad_band
+        const char* e = std::getenv("CNF_WGRAD_THIN");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (!on || taps != 9 || dil != 1 || CO < 1 || CO > 4 || CI < 4 || CI > 64 || (CI & 3) != 0 || W < 1 || W > 128)
+        return false;
+    int TR, ipw, ntile;
+    wgrad_thin_shape(1, H, W, TR, ipw, ntile);
+    return ((size_t)(TR + 2) * (W + 2) * CI + (size_t)TR * W * CO) * 4 <= 64 * 1024;
+}
+
+int wgrad_thin_chunks(int B, int H, int W) {
+    int TR, ipw, ntile;
+    wgrad_thin_shape(B, H, W, TR, ipw, ntile);
+    return ntile * ((B + ipw - 1) / ipw);
+}
+
+void launch_wgrad_thin(const WGradArgs& a, hipStream_t st) {
+    int TR, ipw, ntile;
+    wgrad_thin_shape(a.B, a.H, a.W, TR, ipw, ntile);
+    if (a.chunks != ntile * ((a.B + ipw - 1) / ipw)) throw std::logic_error("k_wgrad_thin: chunk count mismatch");
+    const size_t lds = ((size_t)(TR + 2) * (a.W + 2) * a.CI + (size_t)TR * a.W * a.CO) * 4;
+    const dim3 g(a.chunks), blk(256);
+    switch (a.CO) {
+        case 1: hipLaunchKernelGGL((k_wgrad_thin<1>), g, blk, lds, st, a, TR, ipw, ntile); break;
+        case 2: hipLaunchKernelGGL((k_wgrad_thin<2>), g, blk, lds, st, a, TR, ipw, ntile); break;
+        case 3: hipLaunchKernelGGL((k_wgrad_thin<3>), g, blk, lds, st, a, TR, ipw, ntile); break;
+        case 4: hipLaunchKernelGGL((k_wgrad_thin<4>), g, blk, lds, st, a, TR, ipw, ntile); break;
+        default: throw std::invalid_argument("k_wgrad_thin: CO out of range");
+    }
 }
 
 // rows per work unit (about 128 pixels) and the unit count of a wgrad launch
