@@ -391,11 +391,15 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
         // band: quads of KC channels (zero beyond KC / outside the image), LN on load
         const int nq = BH * BW * cq;
         const uint32_t m_cq = udiv_magic(cq);
-        for (int e0 = threadIdx.x; e0 < nq; e0 += 256 * 4) {
-            f4 v[4];
-            int lo[4];
+#ifndef CNF_TB_U
+#define CNF_TB_U 4
+#endif
+        constexpr int TBU = CNF_TB_U;   // band quads per thread and load batch
+        for (int e0 = threadIdx.x; e0 < nq; e0 += 256 * TBU) {
+            f4 v[TBU];
+            int lo[TBU];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < TBU; u++) {
                 const int e = e0 + 256 * u;
                 v[u] = f4{0.f, 0.f, 0.f, 0.f};
                 const int pb = udiv(e, m_cq), q = e - pb * cq;
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < TBU; u++)
                 if (e0 + 256 * u < nq) *reinterpret_cast<f4*>(band + lo[u]) = v[u];
         }
         // weights of the chunk: [tap][gq = 4g + kq'][j][s], k = kc + 16g + 4kq' + s, gq < GQ = 4 * the
