@@ -255,6 +255,8 @@ struct Plan {
     std::vector<std::string> dry_launches;   // dry runs: the launch names in issue order (cnf_debug_schedule)
     bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
     bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
+    int out_law = 0;          // CNF_OUT_LAW=1: that conv_out and the law as one k_out_law launch (opt-in, slower)
+    int out_law_ks = 0;       // CNF_OUT_LAW_KS=1 / 2: only its 128- / 64-pixel tiles
     std::vector<Recorded> recorded;
     // in-stream launch timing (bench.py): a HIP event pair around every recorded launch
     bool timing = false;

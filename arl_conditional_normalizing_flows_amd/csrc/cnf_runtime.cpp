@@ -112,18 +112,11 @@ static uint32_t udiv_magic_host(uint32_t d) { return d <= 1 ? 0u : 0xFFFFFFFFu /
 // k_out_law tile (TR rows x TW columns of compressed pixels) of a streamed layer with a tap-format
 // conv_out, or false (tap GEMM + k_coupling): 64-pixel tiles (K split over two waves per net) first,
 // then 128-pixel tiles, as long as the image's tiles fit its np log-det slots. Opt-in, CNF_OUT_LAW=1
-// (measured slower than the pair, see cnf_kernels.h OutLawArgs); CNF_OUT_LAW_KS=1 / 2: only 128- /
-// 64-pixel tiles
-static bool out_law_tiles(const Coupling& c, int np, int& TR, int& TW) {
-    static const int mode = [] {
-        const char* e = std::getenv("CNF_OUT_LAW");
-        return e ? std::atoi(e) : 0;
-    }();
-    static const int force_ks = [] {
-        const char* e = std::getenv("CNF_OUT_LAW_KS");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (mode == 0) return false;
+// at plan creation (measured slower than the pair, see cnf_kernels.h OutLawArgs); CNF_OUT_LAW_KS=1 / 2:
+// only 128- / 64-pixel tiles
+static bool out_law_tiles(const Plan& p, const Coupling& c, int np, int& TR, int& TW) {
+    const int force_ks = p.out_law_ks;
+    if (p.out_law == 0) return false;
     for (int ks = 2; ks >= 1; ks--) {
         if (force_ks != 0 && ks != force_ks) continue;
         const int cap = 128 / ks;
@@ -1042,7 +1035,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         }
         int otr = 0, otw = 0;
         if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2 && !defer &&
-            out_law_tiles(c, L.ld_parts, otr, otw)) {
+            out_law_tiles(E.p, c, L.ld_parts, otr, otw)) {
             // conv_out and the law in one k_out_law launch (no tap planes, no k_coupling)
             OutLawArgs oa;
             std::memset(&oa, 0, sizeof(oa));
@@ -1209,6 +1202,8 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     Plan* p = build_plan(desc);
     if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
     if (const char* e = std::getenv("CNF_TAP_PW")) p->tap_pw = std::atoi(e) != 0;
+    if (const char* e = std::getenv("CNF_OUT_LAW")) p->out_law = std::atoi(e);
+    if (const char* e = std::getenv("CNF_OUT_LAW_KS")) p->out_law_ks = std::atoi(e);
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
     // training: k_net_lds layers whose fused backward fits LDS use it (CNF_LDS_BWD=0: none, A/B knob)

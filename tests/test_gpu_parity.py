@@ -23,8 +23,11 @@ RTOL = 1e-5
 # plan-time knobs of the streamed path's fallback kernels: 'nogc' = no fused k_gc stage (CNF_GC=0: the
 # grouped branches run as k_pw tap-mode launches over their im2col rows); 'conv1' = no k_pw (CNF_PW=0:
 # the per-tile k_conv1 / k_conv<3> kernels, and conv_out as the one-kernel k_convtap, CNF_TAP_PW=0)
+# 'outlaw' = the streamed conv_out and coupling law as one k_out_law launch (CNF_OUT_LAW=1, opt-in: measured
+# slower than the tap GEMM + k_coupling pair, kept parity-tested)
 KNOBS = {'nogc': {'CNF_NETLDS': '0', 'CNF_GC': '0'},
-         'conv1': {'CNF_NETLDS': '0', 'CNF_PW': '0', 'CNF_TAP_PW': '0'}}
+         'conv1': {'CNF_NETLDS': '0', 'CNF_PW': '0', 'CNF_TAP_PW': '0'},
+         'outlaw': {'CNF_OUT_LAW': '1'}, 'outlaw128': {'CNF_OUT_LAW': '1', 'CNF_OUT_LAW_KS': '1'}}
 
 
 def _setup(name, B, group_mode='reference', seed=0, netlds=True):
@@ -97,7 +100,10 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          # BASELINE configs[3] / configs[4] architectures (64x64 4-scale, 128x128 5-scale) at a small batch
          ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True),
          # couplings 2 and 1 pixels wide (squeezed to 2x2 blocks)
-         ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False)]
+         ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False),
+         # the opt-in one-launch conv_out + law of the streamed tap-format layers (dc2 = 2 / 3 / 1)
+         ('cfg2', 2, 'reference', 'outlaw'), ('cfg3', 2, 'reference', 'outlaw'),
+         ('ref_default', 2, 'reference', 'outlaw'), ('cfg2', 2, 'reference', 'outlaw128')]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
