@@ -262,6 +262,13 @@ struct Plan {
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 2 per recorded launch, grown on demand, owned by the plan
     // training: net b's recompute / backward chain runs on a second stream (fork / join events)
+    // forward, opt-in (CNF_GC_CONC=1 at plan creation): the independent launches of one streamed grouped
+    // stage (k_gc groups, tap-mode branches) spread over the caller's stream and two side streams, behind
+    // a fork event and joined before conv_b. Measured slower (cfg4 B=32 3.55 -> 3.74 ms, cfg5 B=64
+    // 29.5 -> 30.7 ms): each launch is sized to fill the GPU on its own
+    hipStream_t fside[2] = {nullptr, nullptr};
+    hipEvent_t fev_fork = nullptr, fev_join[2] = {nullptr, nullptr};
+    int gc_conc = 0;
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_device = -1;

@@ -204,6 +204,7 @@ struct Exec {
     WsLayout L;
     int B;
     hipStream_t st;
+    hipStream_t route = nullptr;   // non-null: the next records launch there (a side stream of a forked stage)
 
     template <class T>
     T* at(size_t off) const {
@@ -226,7 +227,7 @@ struct Exec {
             launch_timing() = LaunchTiming{p.ev[2 * k], p.ev[2 * k + 1]};
         }
         try {
-            fn(st);
+            fn(route != nullptr ? route : st);
         } catch (...) {
             launch_timing() = LaunchTiming{};
             throw;
@@ -890,6 +891,38 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         // Each launch's LN3 partial slots follow the previous ones'.
         int base = 0;
         std::vector<char> done(nbr, 0);
+        // the stage's launches are independent (disjoint t2 slices and LN3 slot ranges): with several,
+        // they alternate between the caller's stream and the plan's two side streams
+        int nstage = (int)c.gcg.size(), nrest0 = 0;
+        {
+            std::vector<char> ing(nbr, 0);
+            for (const Coupling::GcGroup& gg : c.gcg)
+                for (int k : gg.br) ing[k] = 1;
+            for (int bi = 0; bi < nbr; bi++)
+                if (!ing[bi]) {
+                    if (E.p.use_pw && c.net[0].rb[r].gpw[bi].size > 0)
+                        nstage++;
+                    else
+                        nrest0 = 1;
+                }
+            nstage += nrest0;
+        }
+        const bool fork = E.p.gc_conc && nstage >= 2 && (E.p.dry || E.p.fside[0] != nullptr);
+        int nused = 0;   // side streams the stage used
+        int li = 0;      // the stage's launch index
+        auto route_next = [&]() {
+            if (!fork) return;
+            const int k = li++ % 3;   // 0: the caller's stream, 1 / 2: side streams
+            E.route = k == 0 ? nullptr : E.p.fside[k - 1];
+            nused = std::max(nused, k);
+        };
+        if (fork) {
+            Plan* pp = &E.p;
+            E.record("fork", 0, 0, [pp](void* st) {
+                hip_check(hipEventRecord(pp->fev_fork, (hipStream_t)st), "hipEventRecord");
+                for (int i = 0; i < 2; i++) hip_check(hipStreamWaitEvent(pp->fside[i], pp->fev_fork, 0), "hipStreamWaitEvent");
+            });
+        }
         for (const Coupling::GcGroup& gg : c.gcg) {
             const int ng = (int)gg.br.size();
             GcArgs ga;
@@ -955,7 +988,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (const GcShape& o : E.p.gc_launch) seen = seen || std::memcmp(&o, &ga.s, sizeof(GcShape)) == 0;
                 if (!seen) E.p.gc_launch.push_back(ga.s);
             }
+            route_next();
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
+            E.route = nullptr;
             base += gcw * ga.s.tiles_per_img;   // one slot per k_gc wave
         }
         {
@@ -974,7 +1009,9 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 TapSrc ts{-1, c.wc, c.t1_pcs[bi], b.cin, c.hc * c.wc * c.t1_cs};
                 ts.dil = b.dil;
                 ts.off = c.t1_off[bi];
+                route_next();
                 base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts, bmap);
+                E.route = nullptr;
                 done[bi] = 1;
             }
             int nrest = 0;
@@ -992,7 +1029,21 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 }
                 nrest = k;
             }
-            if (!pr.empty()) base += nrest * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
+            if (!pr.empty()) {
+                route_next();
+                base += nrest * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
+                E.route = nullptr;
+            }
+            if (fork && nused > 0) {   // the caller's stream waits for the side streams' launches
+                Plan* pp = &E.p;
+                const int nu = nused;
+                E.record("join", 0, 0, [pp, nu](void* st) {
+                    for (int i = 0; i < nu; i++) {
+                        hip_check(hipEventRecord(pp->fev_join[i], pp->fside[i]), "hipEventRecord");
+                        hip_check(hipStreamWaitEvent((hipStream_t)st, pp->fev_join[i], 0), "hipStreamWaitEvent");
+                    }
+                });
+            }
             if (base > L.st_parts) throw std::runtime_error("grouped branches: LN partial slab too small");
             set_parts(2, base);
             save_stats(2, 2 * c.R + 1 + r);
@@ -1173,6 +1224,13 @@ static void ensure_tables(Plan& p) {
     if (!p.aux_map.empty())
         hip_check(hipMemcpy(p.dev_aux_map, p.aux_map.data(), p.aux_map.size() * sizeof(int64_t), hipMemcpyHostToDevice),
                   "hipMemcpy(aux map)");
+    if (p.gc_conc) {   // (a plan moved to another device keeps the old device's streams: never reused)
+        for (int i = 0; i < 2; i++) {
+            hip_check(hipStreamCreateWithFlags(&p.fside[i], hipStreamNonBlocking), "hipStreamCreate");
+            hip_check(hipEventCreateWithFlags(&p.fev_join[i], hipEventDisableTiming), "hipEventCreate");
+        }
+        hip_check(hipEventCreateWithFlags(&p.fev_fork, hipEventDisableTiming), "hipEventCreate");
+    }
     size_t nbw = std::max<size_t>(1, p.bw_map.size()) * sizeof(int64_t);
     hip_check(hipMalloc(&p.dev_bw_map, nbw), "hipMalloc(bw map)");
     if (!p.bw_map.empty())
@@ -1203,6 +1261,7 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
     if (const char* e = std::getenv("CNF_TAP_PW")) p->tap_pw = std::atoi(e) != 0;
     if (const char* e = std::getenv("CNF_OUT_LAW")) p->out_law = std::atoi(e);
+    if (const char* e = std::getenv("CNF_GC_CONC")) p->gc_conc = std::atoi(e) != 0;
     if (const char* e = std::getenv("CNF_OUT_LAW_KS")) p->out_law_ks = std::atoi(e);
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
@@ -1226,6 +1285,11 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
         for (hipEvent_t e : plan->p->ev) (void)hipEventDestroy(e);
         if (plan->p->ev_fork) (void)hipEventDestroy(plan->p->ev_fork);
+        if (plan->p->fev_fork) (void)hipEventDestroy(plan->p->fev_fork);
+        for (int i = 0; i < 2; i++) {
+            if (plan->p->fev_join[i]) (void)hipEventDestroy(plan->p->fev_join[i]);
+            if (plan->p->fside[i]) (void)hipStreamDestroy(plan->p->fside[i]);
+        }
         if (plan->p->ev_join) (void)hipEventDestroy(plan->p->ev_join);
         if (plan->p->side) (void)hipStreamDestroy(plan->p->side);
         for (hipStream_t s : plan->p->wside)

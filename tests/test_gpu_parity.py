@@ -27,7 +27,9 @@ RTOL = 1e-5
 # slower than the tap GEMM + k_coupling pair, kept parity-tested)
 KNOBS = {'nogc': {'CNF_NETLDS': '0', 'CNF_GC': '0'},
          'conv1': {'CNF_NETLDS': '0', 'CNF_PW': '0', 'CNF_TAP_PW': '0'},
-         'outlaw': {'CNF_OUT_LAW': '1'}, 'outlaw128': {'CNF_OUT_LAW': '1', 'CNF_OUT_LAW_KS': '1'}}
+         'outlaw': {'CNF_OUT_LAW': '1'}, 'outlaw128': {'CNF_OUT_LAW': '1', 'CNF_OUT_LAW_KS': '1'},
+         # the grouped stage's launches forked over three streams (CNF_GC_CONC=1, opt-in, measured slower)
+         'gcconc': {'CNF_GC_CONC': '1'}}
 
 
 def _setup(name, B, group_mode='reference', seed=0, netlds=True):
@@ -103,7 +105,8 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False),
          # the opt-in one-launch conv_out + law of the streamed tap-format layers (dc2 = 2 / 3 / 1)
          ('cfg2', 2, 'reference', 'outlaw'), ('cfg3', 2, 'reference', 'outlaw'),
-         ('ref_default', 2, 'reference', 'outlaw'), ('cfg2', 2, 'reference', 'outlaw128')]
+         ('ref_default', 2, 'reference', 'outlaw'), ('cfg2', 2, 'reference', 'outlaw128'),
+         ('cfg4', 2, 'reference', 'gcconc'), ('cfg5', 1, 'reference', 'gcconc')]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
