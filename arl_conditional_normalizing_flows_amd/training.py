@@ -203,7 +203,10 @@ def _agreed_batches(model, data, process_group, what):
     extra all-reduce). A source with len() is checked once per epoch (one all-reduce of two ints);
     any other source (a generator making a device tensor per batch) is streamed one batch at a time
     with a 'have another batch' flag all-reduced before each step, so the epoch is never held in
-    memory at once. Either way a mismatch raises on every rank instead of hanging."""
+    memory at once. Either way a mismatch raises on every rank instead of hanging. Cost of the
+    streamed form on NCCL: reading the flag back (int(n[0])) waits for the device, so each step's
+    host enqueue starts only after the previous step finished — pass a source with len() (a list,
+    a sized dataset) where that per-step sync matters."""
     batches = _batches(data)
     if process_group is None:
         return batches
