@@ -1081,8 +1081,11 @@ __global__ __launch_bounds__(64) void k_ln_final(LnFinalSet a) {
     const int img = blockIdx.x, t = blockIdx.y >> 1, net = blockIdx.y & 1, lane = threadIdx.x;
     const float* q = a.part[t][net] + (size_t)img * a.part_stride * LNP;
     const int nparts = a.nparts[t];
-    float n = 0.f, m = 0.f, M2 = 0.f;
-    for (int i = lane; i < nparts; i += 64) ln_fold(*reinterpret_cast<const f4*>(q + (size_t)LNP * i), n, m, M2);
+    // the lane's slots lane, lane + 64, ... folded in in_ln_finish's order (the first one by
+    // ln_fold_first), so (mu, rstd) are the consumer kernels' bits
+    float n, m, M2;
+    ln_fold_first(lane < nparts ? *reinterpret_cast<const f4*>(q + (size_t)LNP * lane) : f4{0.f, 0.f, 0.f, 0.f}, n, m, M2);
+    for (int i = lane + 64; i < nparts; i += 64) ln_fold(*reinterpret_cast<const f4*>(q + (size_t)LNP * i), n, m, M2);
     float mu, rstd;
     ln_wave_final(n, m, M2, mu, rstd);
     if (lane == 0) {
