@@ -37,7 +37,13 @@ import sys
 import time
 
 import numpy as np
-import torch
+
+# kernel arguments in device memory for eager launches too (set before HIP initialises): graph replay
+# already reads them from device memory, so the eager in-stream timing pass (per_kernel / roofline)
+# then times the same kernels the timed graph runs (with host-memory kernargs the large argument
+# blocks of k_net_lds / k_gc cost 3-4 us per launch there: profiles/sessions/r5_kernarg.sh)
+os.environ.setdefault('HIP_FORCE_DEV_KERNARG', '1')
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
