@@ -249,6 +249,10 @@ class coupling_layer(Layer):
 # ---------------------------------------------------------------------------------------------
 
 class Mean:
+    """keras.metrics.Mean (the loss trackers of :1454-1457): the running mean of update_state values.
+    Fed device tensors (train_step / test_step) it accumulates on the device in float64 — the same
+    double arithmetic as a host float sum — and result() is a 0-d device tensor, as TF's train_step
+    returns tensors: no host read per step (the fit loop reads the epoch's values once, at its end)."""
     def __init__(self, name):
         self.name = name
         self.reset_state()
@@ -258,7 +262,11 @@ class Mean:
         self.count = 0
 
     def update_state(self, v):
-        self.total += float(v)
+        if isinstance(v, torch.Tensor):
+            v = v.detach().to(torch.float64)
+        else:
+            v = float(v)
+        self.total = self.total + v
         self.count += 1
 
     def result(self):
@@ -649,15 +657,15 @@ class cFlow:
 
     def train_step(self, xy, process_group=None):
         """cFlow.train_step (:1850-1880): NLL gradient (GradientTape), optimizer.apply_gradients,
-        Mean trackers; returns {'loss', 'z_loss', 'y_loss', 'detJ_loss'}. Data-parallel with
-        process_group: the loss sums and the gradient are all-reduced over the global batch."""
+        Mean trackers; returns {'loss', 'z_loss', 'y_loss', 'detJ_loss'} as 0-d device tensors (TF
+        returns tensors too; float() reads one). Data-parallel with process_group: the loss sums and
+        the gradient are all-reduced over the global batch."""
         if getattr(self, 'optimizer', None) is None:
             self.compile()
         grads, terms = self.gradients(xy, process_group)
         self.optimizer.apply_flat(self.params, grads)
         check(_lib.load().cnf_pack_params(self._plan, ptr(self.params), ptr(self._aux), _stream()), 'pack params')
-        vals = torch.stack(list(terms)).cpu().tolist()
-        for t, v in zip(self.metrics, vals):
+        for t, v in zip(self.metrics, terms):   # device scalars: no host sync (the trackers stay on the device)
             t.update_state(v)
         return {t.name: t.result() for t in self.metrics}
 
@@ -665,7 +673,6 @@ class cFlow:
         """:1882-1904 — loss without a weight update; updates the Mean trackers. With
         process_group the loss terms are global-batch means (log_loss), the same on every rank."""
         loss, lz, ly, ld = self.log_loss(xy, process_group=process_group)
-        vals = torch.stack([loss, lz, ly, ld]).cpu().tolist()
-        for t, v in zip(self.metrics, vals):
+        for t, v in zip(self.metrics, (loss, lz, ly, ld)):
             t.update_state(v)
         return {t.name: t.result() for t in self.metrics}

@@ -278,14 +278,14 @@ def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Op
             logs = model.train_step(xy, process_group=process_group)
             for cb in cbs:
                 cb.on_train_batch_end(i, logs)
-        logs = dict(logs)
+        logs = {k: float(v) for k, v in logs.items()}   # the epoch's one host read of the trackers
         if validation_data is not None:
             for t in model.metrics:
                 t.reset_state()
             vlogs = {}
             for xy in _agreed_batches(model, validation_data, process_group, 'validation'):
                 vlogs = model.test_step(xy, process_group=process_group)
-            logs.update({'val_' + k: v for k, v in vlogs.items()})
+            logs.update({'val_' + k: float(v) for k, v in vlogs.items()})
         if verbose and rank == 0:
             print(f'Epoch {epoch + 1}/{epochs} ' + ' - '.join(f'{k}: {v:.4f}' for k, v in logs.items()))
         for cb in cbs:
