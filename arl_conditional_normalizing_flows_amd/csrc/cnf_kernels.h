@@ -18,7 +18,10 @@ constexpr double LOG_2PI_D = 1.8378770664093453;
 constexpr int LNP = 4;
 // LN partial slots per image a consumer wave folds from its prologue loads, per lane (cnf_device.h
 // in_ln_fetch); producers of more than 64 * LN_FETCH slots get a k_ln_merge launch (cnf_runtime.cpp)
-constexpr int LN_FETCH = 8;
+#ifndef CNF_LN_FETCH
+#define CNF_LN_FETCH 8
+#endif
+constexpr int LN_FETCH = CNF_LN_FETCH;
 
 constexpr int MAXPROB = 12;
 
