@@ -23,7 +23,7 @@ class cnf_flow_desc(C.Structure):
                 ('num_kernels_list', C.POINTER(C.c_int)),
                 ('cardinality_list', C.POINTER(C.c_int)),
                 ('lambda_y', C.c_float), ('ksize', C.c_int), ('layer_norm', C.c_int),
-                ('dilations', C.c_int), ('group_mode', C.c_int)]
+                ('dilations', C.c_int), ('group_mode', C.c_int), ('debug_options', C.c_char_p)]
 
 
 class cnf_layer_info(C.Structure):

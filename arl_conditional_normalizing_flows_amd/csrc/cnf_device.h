@@ -20,18 +20,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // LeakyReLU(alpha = 0.3): max(x, 0.3 x) == (x >= 0 ? x : 0.3 x) for every finite x, in 2 VALU ops:
 // fmaxf of a loaded x costs a third, the IEEE-mode canonicalisation v_max_f32 x, x, which this form
 // leaves out (it only quiets signalling NaNs). Measured: conv_b 30.6 -> 29.3 us, the cfg2 forward
-// 1.473 -> 1.447 ms (CNF_LRELU_ASM=0 restores fmaxf)
-#ifndef CNF_LRELU_ASM
-#define CNF_LRELU_ASM 1
-#endif
+// 1.473 -> 1.447 ms
 __device__ __forceinline__ float lrelu(float x) {
-#if CNF_LRELU_ASM
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(LRELU_ALPHA * x));
     return r;
-#else
-    return fmaxf(x, LRELU_ALPHA * x);
-#endif
 }
 
 // n / d for n >= 0, n * d < 2^32 as one multiply-high: m = udiv_magic(d) = ceil(2^32 / d) (0 for d == 1)

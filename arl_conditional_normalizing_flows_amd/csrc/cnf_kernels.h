@@ -18,12 +18,39 @@ constexpr double LOG_2PI_D = 1.8378770664093453;
 constexpr int LNP = 4;
 // LN partial slots per image a consumer wave folds from its prologue loads, per lane (cnf_device.h
 // in_ln_fetch); producers of more than 64 * LN_FETCH slots get a k_ln_merge launch (cnf_runtime.cpp)
-#ifndef CNF_LN_FETCH
-#define CNF_LN_FETCH 8
-#endif
-constexpr int LN_FETCH = CNF_LN_FETCH;
+constexpr int LN_FETCH = 8;
 
 constexpr int MAXPROB = 12;
+
+// Debug options of a plan: cnf_flow_desc.debug_options, "NAME=V[,NAME=V...]" (include/cnf.h). They
+// select the alternative code paths the parity tests compare against the default ones; the library
+// reads no environment variable, and the defaults are what bench.py measures.
+struct Options {
+    int netlds = 1;          // NETLDS: 0 = no LDS-resident (k_net_lds) layers, every layer streamed
+    int gc = 1;              // GC: 0 = no fused k_gc stage (grouped branches as k_pw tap mode / k_conv<3>)
+    int pw = 1;              // PW: 0 = the per-tile k_conv1 / k_conv<3> kernels and the one-kernel k_convtap conv_out
+    int generic = 0;         // GENERIC: 1 = never the shape-specialised instantiations (k_pw, k_gc, k_net_lds)
+    int layout = 7;          // LAYOUT bits: 1 compact t1 sub-tensors, 2 mapped t2 sub-tensors, 4 polyphase k_gc tiles
+    int fuse_coupling = 1;   // FUSE_COUPLING: 0 = every coupling layer launches its own k_coupling
+    int lds_bwd = 2;         // LDS_BWD: 0 multi-kernel backward of the k_net_lds layers, 1 fused (one launch), 2 fused split
+    // TRAIN_ALT bits, alternative training kernels: 1 VALU convolutions, 2 LDS-staged band weight gradients
+    // (no k_wgrad_direct), 4 no band-staged transposed conv, 8 no thin-channel kernels, 16 a separate
+    // LN-backward reduction kernel, 32 a zeroed dt1 gradient instead of the LN2 channel mask
+    int train_alt = 0;
+    // TRAIN_SCHED bits: 1 weight gradients on the chain streams, 2 recompute the streamed activations
+    // (no saves), 4 enqueue net A's chain before net b's (no interleaving)
+    int train_sched = 0;
+};
+// parses a debug_options string (null / empty: defaults); throws std::invalid_argument on an unknown
+// name or a malformed value (cnf_runtime.cpp)
+Options parse_options(const char* s);
+// the options of the plan the calling thread's current C-ABI call runs (defaults outside one)
+const Options& opts();
+struct OptScope {   // sets opts() for the duration of one C-ABI call
+    const Options* prev;
+    explicit OptScope(const Options* o);
+    ~OptScope();
+};
 
 // Launch timing (bench.py via cnf_plan_set_launch_timing): while a pair is armed, the launch
 // helpers dispatch through hipExtLaunchKernelGGL, which stores the kernel's own begin / end
@@ -90,9 +117,6 @@ struct ConvArgs {
     // umask < 0: the source is a plain NHWC tensor of the conv's own H x W (uD channels per pixel,
     // taps from channel uoff, dilation udil; LN / LeakyReLU on load as the problem says)
     int udil, uoff;
-    // k_pw shared-tile mode (CNF_PW_SH builds): PW_NS image streams of 4 waves share one workgroup, its
-    // weights and the tile's LN gamma/beta (in LDS at byte gb_off); 0: plain
-    int sh, gb_off;
 };
 
 struct CoupArgs {
@@ -109,27 +133,6 @@ struct CoupArgs {
     const float* tc[2];
     const float* tbias[2];
     float* so_w[2];
-};
-
-// Streamed conv_out and the coupling law in one launch (k_out_law, cnf_kernels.hip): one workgroup
-// per (image, TR x TW tile of compressed pixels) stages LN_out(LReLU(y)) of both nets over the tile
-// and its 1-pixel halo in LDS, runs the two 3x3 convs (nk -> dc2) on the vector ALUs and applies the
-// affine law to the tile's pixels (the tile is the log-det slot). Replaces the tap-GEMM k_pw + k_coupling
-// pair of the streamed layers whose conv_out is in tap format — opt-in (CNF_OUT_LAW=1): measured
-// slower (cfg2: 28 us against 12.3 + 7.2 us; every workgroup re-reads the per-element LN gamma / beta
-// and the halo rows through its CU's L1, 3x the pair's bytes into the CUs).
-struct OutLawArgs {
-    ConvProb p[2];             // per net: in = y, in_part / in_nparts / part_stride (LN_out), gamma, beta
-    const float* w[2];         // raw conv_out kernels [3][3][nk][dc2] (params)
-    const float* b[2];         // [dc2]
-    float* so_w[2];            // raw conv_out of each net, [B][hc][wc][dc2] (s pre-tanh / t)
-    const float* u;
-    float* v;
-    const float* tanh_w;
-    double* ld_part;           // [B][np] or null
-    int H, W, D, mask, mask_c, hc, wc, dc1, dc2, dir;
-    int TR, TW, tiles_r, tiles_c, np;
-    uint32_t tw_mag, twp_mag;  // magic divisors (cnf_device.h udiv) for TW and TW + 2
 };
 
 // Whole s,t network of one coupling layer in LDS (cnf_netlds.hip); grid (B, 2 nets).
@@ -359,18 +362,11 @@ inline bool pw_shape_of(int nr, int gm, bool ln, bool res, bool tap, const ConvA
 }
 void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 int pw_num_shapes();
-bool pw_shared_tile();   // built with the shared-tile k_pw mode (CNF_PW_SH)
-int pw_streams();        // its image streams per workgroup
-int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS=SID): [2048 workgroups][12]   // shape-specialised k_pw instantiations compiled in
+int read_pw_stamps(long long* host);   // diagnostic builds (CNF_PW_STAMPS=SID): [2048 workgroups][12]
 void launch_convtap(int mt, bool vec, const ConvArgs& a, int grid_x, int lds, hipStream_t st);
 void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, int mask, int hc, int wc, int dc1,
                        hipStream_t st);
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st);
-// k_out_law over B * tiles_r * tiles_c workgroups: nk == 64, dc2 <= 3 (the tap-format layers of the presets), ks = 128 / (TR * TW) in {1, 2}
-// (K split over ks waves per net); returns false for a shape it has no instantiation for
-bool out_law_supported(int nk, int dc2, int TR, int TW);
-size_t out_law_lds_bytes(int dc2, int TR, int TW);
-void launch_out_law(const OutLawArgs& a, int B, hipStream_t st);
 void launch_ld_reduce(const double* part, float* out, int B, int nl, int np, int accumulate, hipStream_t st);
 // LN partial slots [B][part_stride][LNP] of one tensor (two nets: part0, part1 or null) merged into
 // slot 0 of each image (k_ln_merge): consumers then read nparts = 1

@@ -522,181 +522,6 @@ __global__ __launch_bounds__(256) void k_coupling(CoupArgs a) {
     }
 }
 
-// Streamed conv_out (:1076-1213, LN_out(LReLU(y)) -> 3x3 conv, nk -> dc2, zero padding) of both nets
-// and the affine law of k_coupling in one launch (OutLawArgs). One workgroup per (image, tile of
-// TR x TW compressed pixels): waves 2n, 2n + 1 stage net n's LN_out(LReLU(y)) over the tile and its
-// 1-pixel halo in LDS (zeros outside the image: the conv's padding), then each thread sums the 3x3
-// taps of one pixel (KS = 2: half of K per wave) on the vector ALUs with the wave-uniform weights
-// from the scalar cache; the partials meet in LDS and the tile's elements get the law, the raw
-// conv_out (so_w, as k_coupling's tap mode writes it) and the copy of the conditioning half. The
-// tile is the image's log-det slot (fixed order: deterministic and batch-invariant). Removes the
-// tap GEMM's 9 * dc2 columns per pixel written to and read back from HBM and one launch.
-template <int DC2, int KS>
-__global__ __launch_bounds__(256) void k_out_law(OutLawArgs a) {
-    constexpr int NK = 64, S = NK + 4, NK4 = NK / 4, PXW = 128 / KS;
-    extern __shared__ f4 sm4[];
-    float* sm = reinterpret_cast<float*>(sm4);
-    __shared__ double sred[4];
-    const int ntile = a.tiles_r * a.tiles_c;
-    int bid = blockIdx.x;
-    const int nb = gridDim.x;
-    // consecutive tiles of one image on one XCD (workgroups are dealt round-robin over the 8 XCDs):
-    // the halo rows two tiles share come from the same L2
-    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);
-    const int img = bid / ntile, tile = bid - img * ntile;
-    const int tr = tile / a.tiles_c, tcl = tile - tr * a.tiles_c;
-    const int r0 = tr * a.TR, c0 = tcl * a.TW;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int net = wave >> 1;
-    const int t128 = threadIdx.x & 127;
-    const ConvProb& P = a.p[net];
-    const int TWp = a.TW + 2, TRp = a.TR + 2;
-    float* tl = sm + (size_t)net * TRp * TWp * S;
-    float* res = sm + (size_t)2 * TRp * TWp * S;   // [net][kp][PXW][DC2]
-    const size_t npx_img = (size_t)a.hc * a.wc;
-
-    // one memory round trip for the prologue: the LN_out partial slots, every staged element of the
-    // tile + halo (y, gamma, beta: buffer loads, 0 outside the image) and u of this thread's first law
-    // elements are all issued before the first wait
-    const LnSlots slot0 = in_ln_fetch(P, img);
-    const bool ln = P.in_part != nullptr;
-    const uint32_t ybytes = (uint32_t)(npx_img * NK * 4);
-    const auto ry = buf_rsrc(P.in + (size_t)img * npx_img * NK, ybytes);
-    const auto rg = buf_rsrc(ln ? P.gamma : P.in, ybytes), rb = buf_rsrc(ln ? P.beta : P.in, ybytes);
-    const int HWD = a.H * a.W * a.D;
-    const float* __restrict__ ub = a.u + (size_t)img * HWD;
-    float* __restrict__ vb = a.v + (size_t)img * HWD;
-    const int npx = a.TR * a.TW;
-    auto law_pos = [&](int e, int dc, int m, int& p) {   // element e = (tile pixel, channel) -> u index, or -1
-        const int px = e / dc, c = e - px * dc;
-        const int pr = udiv(px, a.tw_mag), pc = px - pr * a.TW;
-        const int gr = r0 + pr, gc = c0 + pc;
-        p = gr * a.wc + gc;
-        return gr < a.hc && gc < a.wc ? mask_pos(m, p, c, a.wc, a.W, a.D) : -1;
-    };
-    int p2f, p1f;
-    const int e2f = threadIdx.x, e1f = threadIdx.x;
-    const int q2f = e2f < npx * DC2 ? law_pos(e2f, DC2, a.mask_c, p2f) : -1;
-    const int q1f = e1f < npx * a.dc1 ? law_pos(e1f, a.dc1, a.mask, p1f) : -1;
-    const float u2f = q2f >= 0 ? ub[q2f] : 0.f;
-    const float u1f = q1f >= 0 ? ub[q1f] : 0.f;
-    const int nel = TRp * TWp * NK4;
-#ifndef CNF_OL_U
-#define CNF_OL_U 9
-#endif
-    // staged elements per thread and batch: 18 covers the 64-pixel tiles' 4 x 34 x 16 / 128 in one
-    // batch but needs 286 VGPRs (one workgroup per CU: 43 us per cfg2 launch); 9 (two batches): 28 us
-    constexpr int U = CNF_OL_U;
-    float mu = 0.f, rs = 1.f;
-    for (int e0 = t128; e0 < nel; e0 += 128 * U) {
-        uint32_t off[U];
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const int e = e0 + 128 * j;
-            const int pix = e / NK4, k4 = e - pix * NK4;
-            const int lr = udiv(pix, a.twp_mag), lc = pix - lr * TWp;
-            const int gr = r0 - 1 + lr, gc = c0 - 1 + lc;
-            const bool ok = e < nel && gr >= 0 && gr < a.hc && gc >= 0 && gc < a.wc;
-            off[j] = ok ? (uint32_t)((gr * a.wc + gc) * NK + 4 * k4) * 4u : BUF_OOB;
-        }
-        f4 yv[U], gv[U], bv[U];
-#pragma unroll
-        for (int j = 0; j < U; j++) yv[j] = buf_load4(ry, off[j]);
-        if (ln) {
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                gv[j] = buf_load4(rg, off[j]);
-                bv[j] = buf_load4(rb, off[j]);
-            }
-        }
-        if (e0 == t128) in_ln_finish(P, img, slot0, mu, rs);   // identity without LN
-        const float nmr = -mu * rs;
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const int e = e0 + 128 * j;
-            if (e < nel) {
-                f4 o;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const float v = lrelu(yv[j][q]);
-                    // (outside the image y, gamma and beta load as 0: the padded value is exactly 0)
-                    o[q] = ln ? fmaf(fmaf(v, rs, nmr), gv[j][q], bv[j][q]) : v;
-                }
-                *reinterpret_cast<f4*>(tl + (e / NK4) * S + 4 * (e % NK4)) = o;
-            }
-        }
-    }
-    __syncthreads();
-
-    // 3x3 taps of one pixel per thread (KS = 2: this wave's half of K)
-    const float* __restrict__ wn = a.w[net];
-    const int kp = KS == 2 ? (wave & 1) : 0;
-    {
-        const int px = KS == 2 ? (t128 & 63) : t128;
-        if (px < npx) {
-            const int pr = udiv(px, a.tw_mag), pc = px - pr * a.TW;
-            float acc[DC2];
-#pragma unroll
-            for (int c = 0; c < DC2; c++) acc[c] = 0.f;
-#pragma unroll
-            for (int kh = 0; kh < 3; kh++)
-#pragma unroll
-                for (int kw = 0; kw < 3; kw++) {
-                    const float* row = tl + ((pr + kh) * TWp + pc + kw) * S + kp * (NK / KS);
-                    const float* wt = wn + ((kh * 3 + kw) * NK + kp * (NK / KS)) * DC2;
-#pragma unroll
-                    for (int k4 = 0; k4 < NK4 / KS; k4++) {
-                        const f4 yv = *reinterpret_cast<const f4*>(row + 4 * k4);
-#pragma unroll
-                        for (int j = 0; j < 4; j++)
-#pragma unroll
-                            for (int c = 0; c < DC2; c++) acc[c] = fmaf(yv[j], wt[(4 * k4 + j) * DC2 + c], acc[c]);
-                    }
-                }
-#pragma unroll
-            for (int c = 0; c < DC2; c++) res[((net * KS + kp) * PXW + px) * DC2 + c] = acc[c];
-        }
-    }
-    __syncthreads();
-
-    // the affine law on the tile's transformed elements, then the copy of its conditioning half
-    const float w = *a.tanh_w;
-    float lsum = 0.f;
-    for (int e = threadIdx.x; e < npx * DC2; e += 256) {
-        int p;
-        const int q = e == e2f ? q2f : law_pos(e, DC2, a.mask_c, p);
-        if (e == e2f) p = p2f;
-        if (q >= 0) {
-            const int px = e / DC2, c = e - px * DC2;
-            float sp = a.b[0][c], t = a.b[1][c];
-#pragma unroll
-            for (int k = 0; k < KS; k++) {
-                sp += res[(k * PXW + px) * DC2 + c];
-                t += res[((KS + k) * PXW + px) * DC2 + c];
-            }
-            a.so_w[0][((size_t)img * npx_img + p) * DC2 + c] = sp;
-            a.so_w[1][((size_t)img * npx_img + p) * DC2 + c] = t;
-            const float s = w * cpl_tanh(sp);
-            vb[q] = cpl_law(s, e == e2f ? u2f : ub[q], t, a.dir);   // k_coupling's expression
-            if (a.dir > 0) lsum += s;
-        }
-    }
-    for (int e = threadIdx.x; e < npx * a.dc1; e += 256) {
-        int p;
-        const int q = e == e1f ? q1f : law_pos(e, a.dc1, a.mask, p);
-        if (q >= 0) vb[q] = e == e1f ? u1f : ub[q];
-    }
-    if (a.ld_part != nullptr) {
-        const double ws = wave_sum((double)lsum);
-        if ((threadIdx.x & 63) == 0) sred[threadIdx.x >> 6] = ws;
-        __syncthreads();
-        double* dst = a.ld_part + (size_t)img * a.np;
-        if (threadIdx.x == 0) dst[tile] = sred[0] + sred[1] + sred[2] + sred[3];
-        if (tile == 0)
-            for (int j = ntile + threadIdx.x; j < a.np; j += 256) dst[j] = 0.0;
-    }
-}
-
 // Merge of one tensor's per-wave LN partial slots into slot 0 (in place), for tensors of the large
 // streamed layers whose producers write more slots per image than a consumer wave folds in one pass
 // (> 64): every consumer workgroup would otherwise re-read all of them for each of its images.
@@ -1045,33 +870,6 @@ void launch_gather_u1c(const float* u, float* u1c, int B, int H, int W, int D, i
 
 void launch_coupling(const CoupArgs& a, int B, int nparts, hipStream_t st) {
     CNF_LAUNCH(k_coupling, dim3(nparts, B), dim3(256), 0, st, a);
-}
-
-bool out_law_supported(int nk, int dc2, int TR, int TW) {
-    const int npx = TR * TW;
-    return nk == 64 && dc2 >= 1 && dc2 <= 3 && TR >= 1 && TW >= 1 && npx <= 128 &&
-           out_law_lds_bytes(dc2, TR, TW) <= 160 * 1024 - 64;
-}
-
-size_t out_law_lds_bytes(int dc2, int TR, int TW) {
-    return ((size_t)2 * (TR + 2) * (TW + 2) * 68 + 256 * (size_t)dc2) * 4;
-}
-
-void launch_out_law(const OutLawArgs& a, int B, hipStream_t st) {
-    const int ks = a.TR * a.TW <= 64 ? 2 : 1;
-    const dim3 g(B * a.tiles_r * a.tiles_c), b(256);
-    const size_t lds = out_law_lds_bytes(a.dc2, a.TR, a.TW);
-#define CNF_OL_CASE(D_)                                                                                 \
-    if (a.dc2 == D_) {                                                                                  \
-        if (ks == 2)                                                                                    \
-            CNF_LAUNCH((k_out_law<D_, 2>), g, b, lds, st, a);                                          \
-        else                                                                                            \
-            CNF_LAUNCH((k_out_law<D_, 1>), g, b, lds, st, a);                                          \
-        return;                                                                                         \
-    }
-    CNF_OL_CASE(1) CNF_OL_CASE(2) CNF_OL_CASE(3)
-#undef CNF_OL_CASE
-    throw std::invalid_argument("k_out_law: dc2 out of range");
 }
 
 // Training forward of a streamed layer: (mean, rstd) of one LN tensor per (image, net) from its

@@ -1343,22 +1343,19 @@ bool launch_shape(int sid, const NetLdsArgs& a, dim3 grid, dim3 block, int lds, 
 int netlds_num_shapes() { return CNF_NETLDS_NSHAPES; }
 
 void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
-    static const bool stamps = [] {
+#ifdef CNF_DIAG
+    static const bool stamps = [] {   // diagnostic builds: phase stamps (profiles/diag/diag_stamps.py)
         const char* e = std::getenv("CNF_STAMPS");
         return e && std::atoi(e) != 0;
     }();
-    static const bool wide = [] {   // A/B knob: always the generic instantiation
-        const char* e = std::getenv("CNF_NETLDS_WIDE");
-        return e && std::atoi(e) != 0;
-    }();
-    static const bool generic = [] {   // A/B knob: never the shape-specialised instantiations
-        const char* e = std::getenv("CNF_NETLDS_GENERIC");
-        return e && std::atoi(e) != 0;
-    }();
-    const bool narrow = a.maxnr <= 2 && !wide;
+#else
+    constexpr bool stamps = false;
+#endif
+    const bool generic = opts().generic != 0;   // never the shape-specialised instantiations
+    const bool narrow = a.maxnr <= 2;
     const bool ks = a.off_ks != 0;
     const dim3 grid(B, 2), block(NT);
-    if (!generic && !wide) {
+    if (!generic) {
         int w[NETSHAPE_WORDS];
         netshape_words(a, w);
         for (int sid = 0; sid < CNF_NETLDS_NSHAPES; sid++) {

@@ -153,6 +153,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
     Plan& p = *P;
     try {
         p.desc = *d;
+        p.opts = parse_options(d->debug_options);
+        p.desc.debug_options = nullptr;   // (the caller's string: not kept)
         const int nb = d->num_blocks;
         require(nb > 0 && d->squeeze_factor_block_list && d->resnext_block_list && d->num_kernels_list &&
                     d->cardinality_list,
@@ -363,9 +365,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
         // prefer PK_Q4 for its 3x3 convs (channel-quad ds_read_b128 A reads), fall back to PK_KN
         // when the Q4 images do not fit the 160 KiB LDS image, else stream the layer.
         {
-            bool allow = true, allow_gc = true;
-            if (const char* e = std::getenv("CNF_NETLDS")) allow = std::atoi(e) != 0;
-            if (const char* e = std::getenv("CNF_GC")) allow_gc = std::atoi(e) != 0;
+            const bool allow = p.opts.netlds != 0, allow_gc = p.opts.gc != 0;
             for (auto& c : p.couplings) {
                 const int tapco = 9 * c.dc2 <= 64 ? PK_TAP : PK_KN;
                 c.ci_fmt = PK_KN;
@@ -373,16 +373,13 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 c.gc_fmt.assign(c.br.size(), PK_KN);
                 c.use_lds = false;
                 if (!allow) continue;
-                if (const char* e = std::getenv("CNF_NETLDS_MAXHW"))   // tuning: stream layers above this size
-                    if (c.hc * c.wc > std::atoi(e)) continue;
                 const int ci9 = c.dc1 % 4 == 0 ? PK_Q4 : PK_KN;
                 // conv_out: the tap-decomposed form (1x1 GEMM to 9*dc2 columns, computed in 32-column
                 // chunks, + a 9-point shifted sum) when it needs fewer MFMAs than the quad-packed 3x3
                 // (ceil(nk/16) * ceil(9 dc2/16) against ceil(9 nk/16) * ceil(dc2/16) 16x16 blocks)
                 const int tap_cost = (c.nk + 15) / 16 * ((9 * c.dc2 + 15) / 16);
                 const int q4_cost = (9 * c.nk + 15) / 16 * ((c.dc2 + 15) / 16);
-                bool tap = tap_cost < q4_cost;
-                if (const char* e = std::getenv("CNF_CO_TAPMAX")) tap = 9 * c.dc2 <= std::atoi(e);   // tuning
+                const bool tap = tap_cost < q4_cost;
                 const int coq = c.nk % 4 == 0 ? PK_Q4 : PK_KN;
                 std::vector<int> gc9;
                 for (const Branch& b : c.br) gc9.push_back(b.cin % 4 == 0 && b.cin_off % 4 == 0 ? PK_Q4 : PK_KN);
@@ -470,9 +467,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     return true;
                 };
                 auto fit = [&](const std::vector<int>& sel, int TW, int TP, Coupling::GcGroup& out) -> bool {
-                    int TH = std::max(1, std::min(c.hc, TP / TW));   // TP-pixel tiles
-                    if (TW == c.wc)
-                        if (const char* e = std::getenv("CNF_GC_TH")) TH = std::max(1, std::min(c.hc, std::atoi(e)));   // tuning
+                    const int TH = std::max(1, std::min(c.hc, TP / TW));   // TP-pixel tiles
                     if (!fit_geo(sel, TH, TW, 0, 1, out)) return false;
                     out.TP = TP;
                     return true;
@@ -485,11 +480,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     return false;
                 };
                 // a large dilation that does not fit the current group opens a group of its own
-                // (cfg5: 485 -> 437 ms/step against tap mode; CNF_GC_TAPGROUP=0 is the A/B knob)
-                static const int tap_group = [] {
-                    const char* e = std::getenv("CNF_GC_TAPGROUP");
-                    return e ? std::atoi(e) : 1;
-                }();
+                // (cfg5: 485 -> 437 ms/step against tap mode)
                 std::vector<int> order;
                 for (size_t bi = 0; bi < c.br.size(); bi++) order.push_back((int)bi);
                 std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return c.br[x].dil < c.br[y].dil; });
@@ -508,7 +499,6 @@ Plan* build_plan(const cnf_flow_desc* d) {
                             continue;
                         }
                     }
-                    if (have && tap_able && !tap_group) continue;   // tap mode
                     if (fit_any({bi}, g)) {
                         if (have) c.gcg.push_back(cur);
                         cur = g;
@@ -519,11 +509,8 @@ Plan* build_plan(const cnf_flow_desc* d) {
                 // a group of one large-dilation branch on polyphase tiles when its phase grids are whole
                 // (H, W divisible by the dilation): bands of (TH+2) x (TW+2) per grid instead of
                 // (TH + 2d) x (TW + 2d) (cfg5's dilation-16 branch: 400 staged pixels per 256 outputs
-                // instead of 1920 per 128); CNF_GC_POLY=0 is the A/B knob
-                const bool poly = [] {   // read per plan: tests compare both tilings in one process
-                    const char* e = std::getenv("CNF_GC_POLY");
-                    return !(e && std::atoi(e) == 0);
-                }();
+                // instead of 1920 per 128); debug option LAYOUT without bit 4: none
+                const bool poly = (p.opts.layout & 4) != 0;
                 for (auto& gg : c.gcg) {
                     if (!poly || gg.br.size() != 1) continue;
                     const Branch& b = c.br[gg.br[0]];
@@ -547,15 +534,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
                     // four 4-wave workgroups per CU when the band is small (these branches have little
                     // MFMA work per image: their time is per-image latency, which co-resident
                     // workgroups hide; tiles down to 128 pixels for it), else one 16-wave workgroup
-                    const int poly_nw = [] {
-                        const char* e = std::getenv("CNF_GC_POLY_NW");   // A/B knob
-                        return e ? std::atoi(e) : 4;
-                    }();
                     Coupling::GcGroup g;
                     int nbk = 1, TH = hs, tpp = 1;
                     bool ok = false;
                     for (int TP : {256, 128}) {
-                        if (poly_nw != 4) break;
                         tile_for(TP, nbk, TH, tpp);
                         if ((ok = fit_geo(gg.br, TH, wsb, 1, nbk, g, 4))) break;
                     }
@@ -582,12 +564,9 @@ Plan* build_plan(const cnf_flow_desc* d) {
             // k_gc group (and each branch launched on its own) reads only its windows, 16-byte aligned,
             // instead of a few channels out of every 256-byte pixel. conv_a runs as k_pw for it (CNF_PW=0
             // selects k_conv1, which stores the plain layout), and no branch may be left to k_conv<3>
-            // (plain layout only); CNF_T1_COMPACT=0 is the A/B knob
-            bool allow_c = true;
-            if (const char* e = std::getenv("CNF_PW")) allow_c = allow_c && std::atoi(e) != 0;
-            if (const char* e = std::getenv("CNF_T1_COMPACT")) allow_c = allow_c && std::atoi(e) != 0;
-            int tap_dmin = 4;
-            if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin = std::atoi(e);   // as the packing below
+            // (plain layout only); debug option LAYOUT without bit 1: the plain layout
+            const bool allow_c = p.opts.pw != 0 && (p.opts.layout & 1) != 0;
+            constexpr int tap_dmin = 4;   // as the packing below
             for (auto& c : p.couplings) {
                 c.t1_cs = c.nk;
                 c.t1_compact = false;
@@ -673,13 +652,10 @@ Plan* build_plan(const cnf_flow_desc* d) {
         }
 
         // t2 split into its producers' sub-tensors when there are several (cfg4 / cfg5: k_gc groups of one
-        // branch each); CNF_T2_MAP=0 is the A/B knob
+        // branch each); debug option LAYOUT without bit 2: the plain layout
         {
-            bool allow_t2 = true;
-            if (const char* e = std::getenv("CNF_PW")) allow_t2 = allow_t2 && std::atoi(e) != 0;
-            if (const char* e = std::getenv("CNF_T2_MAP")) allow_t2 = allow_t2 && std::atoi(e) != 0;
-            int tap_dmin2 = 4;
-            if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin2 = std::atoi(e);
+            const bool allow_t2 = p.opts.pw != 0 && (p.opts.layout & 2) != 0;
+            constexpr int tap_dmin2 = 4;
             for (auto& c : p.couplings) {
                 c.t2_mapped = false;
                 c.t2_cs = c.gc;
@@ -868,8 +844,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         // (dilations >= 4 only: below that the staged band's halo is cheap and k_conv<3>'s
                         // coalesced band loads beat the row's strided gathers)
                         PackedConv pw;
-                        int tap_dmin = 4;
-                        if (const char* e = std::getenv("CNF_GC_TAP_DMIN")) tap_dmin = std::atoi(e);   // tuning
+                        constexpr int tap_dmin = 4;
                         const bool in_gc = c.in_gc((int)bi);
                         if (!c.use_lds && !in_gc && ks == 3 && 9 * b.cin <= 128 && b.cout <= 64 && b.dil >= tap_dmin)
                             pack(pw, PK_1X1, 9 * b.cin, b.cout, dense, [=](int n) { return gb[n / b.width] + (n % b.width); });

@@ -253,22 +253,14 @@ struct Plan {
     std::vector<PwShape> pw_shapes;   // k_pw launch shapes seen by a dry run
     std::vector<GcShape> gc_launch;   // dry runs: the k_gc launch shapes (GcArgs::s) as run_coupling issues them
     std::vector<std::string> dry_launches;   // dry runs: the launch names in issue order (cnf_debug_schedule)
-    bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (CNF_PW=0: per-tile k_conv1)
-    bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (CNF_TAP_PW=0: k_convtap)
-    int out_law = 0;          // CNF_OUT_LAW=1: that conv_out and the law as one k_out_law launch (opt-in, slower)
-    int out_law_ks = 0;       // CNF_OUT_LAW_KS=1 / 2: only its 128- / 64-pixel tiles
+    Options opts;             // cnf_flow_desc.debug_options (parsed by build_plan)
+    bool use_pw = true;       // image-looping k_pw for streamed 1x1 convs (option PW=0: per-tile k_conv1)
+    bool tap_pw = true;       // streamed tap conv_out as a 1x1 tap GEMM + sums in k_coupling (PW=0: k_convtap)
     std::vector<Recorded> recorded;
     // in-stream launch timing (bench.py): a HIP event pair around every recorded launch
     bool timing = false;
     std::vector<hipEvent_t> ev;   // 2 per recorded launch, grown on demand, owned by the plan
     // training: net b's recompute / backward chain runs on a second stream (fork / join events)
-    // forward, opt-in (CNF_GC_CONC=1 at plan creation): the independent launches of one streamed grouped
-    // stage (k_gc groups, tap-mode branches) spread over the caller's stream and two side streams, behind
-    // a fork event and joined before conv_b. Measured slower (cfg4 B=32 3.55 -> 3.74 ms, cfg5 B=64
-    // 29.5 -> 30.7 ms): each launch is sized to fill the GPU on its own
-    hipStream_t fside[2] = {nullptr, nullptr};
-    hipEvent_t fev_fork = nullptr, fev_join[2] = {nullptr, nullptr};
-    int gc_conc = 0;
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int side_device = -1;
@@ -279,9 +271,13 @@ struct Plan {
     size_t tev_next = 0;
     // cnf_nll's completion counters: NLL_SLOTS ints past the device table, one per stream that has
     // called cnf_nll on this plan (host-side assignment, so concurrent calls on different streams
-    // never share a counter and a call inside graph capture needs no allocation)
+    // never share a counter and a call inside graph capture needs no allocation). A 65th stream takes
+    // the least recently used slot behind a wait on that slot's last launch (nll_ev)
     static constexpr int NLL_SLOTS = 64;
     std::vector<void*> nll_streams;
+    std::vector<hipEvent_t> nll_ev;
+    std::vector<uint64_t> nll_last;
+    uint64_t nll_clock = 0;
     std::shared_ptr<std::mutex> nll_mu = std::make_shared<std::mutex>();
     WsLayout layout(int B) const;
     TrainLayout train_layout(int B) const;

@@ -63,6 +63,57 @@ namespace cnf {
 // error reporting for the entry points defined outside this file (cnf_transforms.hip)
 int set_error(int code, const char* msg) { return fail(code, msg); }
 
+// ----------------------------------------------------------------------------------------------
+// debug options (cnf_flow_desc.debug_options)
+// ----------------------------------------------------------------------------------------------
+Options parse_options(const char* s) {
+    Options o;
+    if (s == nullptr) return o;
+    struct Field {
+        const char* name;
+        int Options::*f;
+    };
+    static const Field fields[] = {{"NETLDS", &Options::netlds},           {"GC", &Options::gc},
+                                   {"PW", &Options::pw},                   {"GENERIC", &Options::generic},
+                                   {"LAYOUT", &Options::layout},           {"FUSE_COUPLING", &Options::fuse_coupling},
+                                   {"LDS_BWD", &Options::lds_bwd},         {"TRAIN_ALT", &Options::train_alt},
+                                   {"TRAIN_SCHED", &Options::train_sched}};
+    std::string str(s);
+    size_t pos = 0;
+    while (pos < str.size()) {
+        size_t end = str.find(',', pos);
+        if (end == std::string::npos) end = str.size();
+        const std::string item = str.substr(pos, end - pos);
+        pos = end + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) throw std::invalid_argument("debug_options: expected NAME=VALUE, got '" + item + "'");
+        const std::string key = item.substr(0, eq), val = item.substr(eq + 1);
+        char* endp = nullptr;
+        const long v = std::strtol(val.c_str(), &endp, 10);
+        if (val.empty() || *endp != '\0') throw std::invalid_argument("debug_options: bad value in '" + item + "'");
+        bool found = false;
+        for (const Field& f : fields)
+            if (key == f.name) {
+                o.*(f.f) = (int)v;
+                found = true;
+            }
+        if (!found) throw std::invalid_argument("debug_options: unknown option '" + key + "'");
+    }
+    if (o.lds_bwd < 0 || o.lds_bwd > 2) throw std::invalid_argument("debug_options: LDS_BWD is 0, 1 or 2");
+    return o;
+}
+
+namespace {
+thread_local const Options* g_opts = nullptr;
+const Options kDefaultOptions{};
+}  // namespace
+const Options& opts() { return g_opts != nullptr ? *g_opts : kDefaultOptions; }
+OptScope::OptScope(const Options* o) : prev(g_opts) {
+    if (o != nullptr) g_opts = o;
+}
+OptScope::~OptScope() { g_opts = prev; }
+
 LaunchTiming& launch_timing() {
     thread_local LaunchTiming t;
     return t;
@@ -108,29 +159,6 @@ static ConvGeom1 conv1_geo(int h, int w) {
 static int ld_parts_for(int npx) { return std::max(1, std::min(16, (npx + 63) / 64)); }
 
 static uint32_t udiv_magic_host(uint32_t d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }   // cnf_device.h udiv
-
-// k_out_law tile (TR rows x TW columns of compressed pixels) of a streamed layer with a tap-format
-// conv_out, or false (tap GEMM + k_coupling): 64-pixel tiles (K split over two waves per net) first,
-// then 128-pixel tiles, as long as the image's tiles fit its np log-det slots. Opt-in, CNF_OUT_LAW=1
-// at plan creation (measured slower than the pair, see cnf_kernels.h OutLawArgs); CNF_OUT_LAW_KS=1 / 2:
-// only 128- / 64-pixel tiles
-static bool out_law_tiles(const Plan& p, const Coupling& c, int np, int& TR, int& TW) {
-    const int force_ks = p.out_law_ks;
-    if (p.out_law == 0) return false;
-    for (int ks = 2; ks >= 1; ks--) {
-        if (force_ks != 0 && ks != force_ks) continue;
-        const int cap = 128 / ks;
-        const int tw = std::min(c.wc, 32);
-        const int tr = std::max(1, cap / tw);
-        if (tr * tw > cap) continue;
-        const int tiles = ((c.hc + tr - 1) / tr) * ((c.wc + tw - 1) / tw);
-        if (tiles > np || !out_law_supported(c.nk, c.dc2, tr, tw)) continue;
-        TR = tr;
-        TW = tw;
-        return true;
-    }
-    return false;
-}
 
 WsLayout Plan::layout(int B) const {
     WsLayout L;
@@ -204,7 +232,6 @@ struct Exec {
     WsLayout L;
     int B;
     hipStream_t st;
-    hipStream_t route = nullptr;   // non-null: the next records launch there (a side stream of a forked stage)
 
     template <class T>
     T* at(size_t off) const {
@@ -227,7 +254,7 @@ struct Exec {
             launch_timing() = LaunchTiming{p.ev[2 * k], p.ev[2 * k + 1]};
         }
         try {
-            fn(route != nullptr ? route : st);
+            fn(st);
         } catch (...) {
             launch_timing() = LaunchTiming{};
             throw;
@@ -389,13 +416,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
             // k_pw loads every channel quad the input window starts with 16 bytes at a time: a window
             // that is not quad-aligned (conv_b over the 62- / 30-channel concat of cfg5's grouped
             // stages) reads past its last channel into the next pixel (or 0 past the image), which
-            // meets zero weight rows (the packed image pads K with zeros). CNF_PW_ALIGNED=1: the
-            // quad-aligned windows only (the rest as k_conv1)
-            static const bool pw_aligned = [] {
-                const char* e = std::getenv("CNF_PW_ALIGNED");
-                return e && std::atoi(e) != 0;
-            }();
-            if (!tap && pw_aligned && (s.cin % 4 || s.in_cs % 4 || s.in_off % 4)) vec = false;
+            // meets zero weight rows (the packed image pads K with zeros)
             pw_nr = std::max(pw_nr, q.nr);
             pw_gm = std::max(pw_gm, G);
         }
@@ -442,24 +463,7 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         for (int i = 0; i < a.nprob; i++) a.p[i].out_part_base = probs[i].out_part_base;
         const int64_t units = (int64_t)tiles * a.nprob * E.B;
         const bool lnf = probs[0].in_st.part != nullptr;
-        // shared-tile mode (CNF_PW_SH builds; CNF_PW_SH=0 at run time: off): one workgroup per CU,
-        // pw_streams() images of the tile at a time, gamma / beta staged once in LDS behind the weights
-        a.sh = pw_shared_tile() && lnf && tap == nullptr && a.p[0].out2 == nullptr && !(std::getenv("CNF_PW_SH") &&
-               std::atoi(std::getenv("CNF_PW_SH")) == 0) ? 1 : 0;
-        int ilds_pw = ilds;
-        if (a.sh) {
-            const int ns = pw_streams();
-            a.ipw = (int)std::min<int64_t>(32, std::max<int64_t>(ns, (units + 255) / 256));
-            a.gb_off = (int)align_up(lds, 16);
-            ilds_pw = a.gb_off + pw_gm * 4 * 64 * 16 * 2;
-            if (ilds_pw > 160 * 1024) {   // gamma / beta do not fit beside the weights: plain mode
-                a.sh = 0;
-                ilds_pw = ilds;
-            }
-        }
-        if (!a.sh) a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
-        if (const char* e = std::getenv(resf ? "CNF_PW_IPW_RES" : "CNF_PW_IPW"))   // tuning override
-            a.ipw = std::max(1, std::min(a.sh ? 32 : 16, std::atoi(e)));
+        a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool tapf = tap != nullptr;
@@ -482,8 +486,8 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         }
         std::string name = std::string("k_pw<") + std::to_string(nr) + "," + std::to_string(gm) + "," +
                            role_name(role) + ">";
-        E.record(name, flops, bytes, [nr, gm, lnf, resf, tapf, a, grid_x, ilds_pw](void* st) {
-            launch_pw(nr, gm, lnf, resf, tapf, a, grid_x, ilds_pw, (hipStream_t)st);
+        E.record(name, flops, bytes, [nr, gm, lnf, resf, tapf, a, grid_x, ilds](void* st) {
+            launch_pw(nr, gm, lnf, resf, tapf, a, grid_x, ilds, (hipStream_t)st);
         });
         return nw * tiles;
     } else {
@@ -633,6 +637,7 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     // the tap-decomposed conv_out runs in chunks of at most two 16-column blocks
     a.maxnr = std::max(nr(c.nk), c.co_fmt == PK_TAP ? std::min(2, nr(9 * c.dc2)) : nr(c.dc2));
     for (const Branch& b : c.br) a.maxnr = std::max(a.maxnr, nr(b.cout));
+#ifdef CNF_DIAG
     if (const char* e = std::getenv("CNF_NETLDS_DUMP")) {   // diagnostics: every shape field, as C
         if (std::atoi(e)) {
             const int* w = reinterpret_cast<const int*>(&a.offs_per_net);
@@ -647,6 +652,7 @@ static size_t netlds_setup(const Plan& p, const Coupling& c, NetLdsArgs& a) {
     if (const char* e = std::getenv("CNF_NETLDS_VERBOSE"))
         if (std::atoi(e)) std::fprintf(stderr, "netlds layer hc=%d wc=%d nk=%d dc2=%d co_fmt=%d maxnr=%d\n", c.hc, c.wc,
                                        c.nk, c.dc2, c.co_fmt, a.maxnr);
+#endif
     return (size_t)g.bytes;
 }
 
@@ -779,10 +785,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // more slots than a consumer wave fetches in its prologue (64 x LN_FETCH = 512: the 128x128 layers):
     // merged once per image by k_ln_merge instead of by every consumer workgroup for each of its images
     // (the 64x64 layers' slots are folded by the consumers: 70 fewer launches per cfg4 step)
-    static const int ln_merge_over = [] {   // A/B knob: CNF_LN_MERGE=0 never merges, =64 the round-4 rule
-        const char* e = std::getenv("CNF_LN_MERGE");
-        return e ? (std::atoi(e) == 0 ? 1 << 30 : std::atoi(e)) : 64 * LN_FETCH;
-    }();
+    constexpr int ln_merge_over = 64 * LN_FETCH;
     auto set_parts = [&](int k, int nparts) {
         if (ln && nparts > ln_merge_over) {
             float* p0 = sl[0][k].part;
@@ -891,38 +894,6 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
         // Each launch's LN3 partial slots follow the previous ones'.
         int base = 0;
         std::vector<char> done(nbr, 0);
-        // the stage's launches are independent (disjoint t2 slices and LN3 slot ranges): with several,
-        // they alternate between the caller's stream and the plan's two side streams
-        int nstage = (int)c.gcg.size(), nrest0 = 0;
-        {
-            std::vector<char> ing(nbr, 0);
-            for (const Coupling::GcGroup& gg : c.gcg)
-                for (int k : gg.br) ing[k] = 1;
-            for (int bi = 0; bi < nbr; bi++)
-                if (!ing[bi]) {
-                    if (E.p.use_pw && c.net[0].rb[r].gpw[bi].size > 0)
-                        nstage++;
-                    else
-                        nrest0 = 1;
-                }
-            nstage += nrest0;
-        }
-        const bool fork = E.p.gc_conc && nstage >= 2 && (E.p.dry || E.p.fside[0] != nullptr);
-        int nused = 0;   // side streams the stage used
-        int li = 0;      // the stage's launch index
-        auto route_next = [&]() {
-            if (!fork) return;
-            const int k = li++ % 3;   // 0: the caller's stream, 1 / 2: side streams
-            E.route = k == 0 ? nullptr : E.p.fside[k - 1];
-            nused = std::max(nused, k);
-        };
-        if (fork) {
-            Plan* pp = &E.p;
-            E.record("fork", 0, 0, [pp](void* st) {
-                hip_check(hipEventRecord(pp->fev_fork, (hipStream_t)st), "hipEventRecord");
-                for (int i = 0; i < 2; i++) hip_check(hipStreamWaitEvent(pp->fside[i], pp->fev_fork, 0), "hipStreamWaitEvent");
-            });
-        }
         for (const Coupling::GcGroup& gg : c.gcg) {
             const int ng = (int)gg.br.size();
             GcArgs ga;
@@ -969,7 +940,6 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + slots - 1) / slots));
             ga.s.band_bytes = gg.band_bytes;
             ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
-            if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::max(1, std::min(16, std::atoi(e)));   // tuning override
             const int gcw = gc_waves(ga);
             if (base + gcw * ga.s.tiles_per_img > L.st_parts) throw std::runtime_error("k_gc: LN partial slab too small");
             const int grid_x = ga.s.tiles_per_img * ((B + ga.ipw - 1) / ga.ipw);
@@ -988,9 +958,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 for (const GcShape& o : E.p.gc_launch) seen = seen || std::memcmp(&o, &ga.s, sizeof(GcShape)) == 0;
                 if (!seen) E.p.gc_launch.push_back(ga.s);
             }
-            route_next();
             E.record("k_gc", fl, by, [ga, grid_x, ilds](void* st) { launch_gc(ga, grid_x, ilds, (hipStream_t)st); });
-            E.route = nullptr;
             base += gcw * ga.s.tiles_per_img;   // one slot per k_gc wave
         }
         {
@@ -1009,9 +977,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 TapSrc ts{-1, c.wc, c.t1_pcs[bi], b.cin, c.hc * c.wc * c.t1_cs};
                 ts.dil = b.dil;
                 ts.off = c.t1_off[bi];
-                route_next();
                 base += conv_launch(E, 1, ROLE_GC, c.hc, c.wc, pt, ~0ull, &ts, bmap);
-                E.route = nullptr;
                 done[bi] = 1;
             }
             int nrest = 0;
@@ -1030,19 +996,7 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
                 nrest = k;
             }
             if (!pr.empty()) {
-                route_next();
                 base += nrest * conv_launch(E, 3, ROLE_GC, c.hc, c.wc, pr);
-                E.route = nullptr;
-            }
-            if (fork && nused > 0) {   // the caller's stream waits for the side streams' launches
-                Plan* pp = &E.p;
-                const int nu = nused;
-                E.record("join", 0, 0, [pp, nu](void* st) {
-                    for (int i = 0; i < nu; i++) {
-                        hip_check(hipEventRecord(pp->fev_join[i], pp->fside[i]), "hipEventRecord");
-                        hip_check(hipStreamWaitEvent((hipStream_t)st, pp->fev_join[i], 0), "hipStreamWaitEvent");
-                    }
-                });
             }
             if (base > L.st_parts) throw std::runtime_error("grouped branches: LN partial slab too small");
             set_parts(2, base);
@@ -1083,54 +1037,6 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             pr.push_back(ProbSpec{y[n], c.nk, 0, c.nk, in_slab(n, 0), ln ? P + np.ln_out_g : none,
                                   ln ? P + np.ln_out_b : none, 1, X + np.co.w, X + np.co.b, so[n], c.dc2, 0, c.dc2,
                                   none, Slab{}, 0, 1});
-        }
-        int otr = 0, otw = 0;
-        if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2 && !defer &&
-            out_law_tiles(E.p, c, L.ld_parts, otr, otw)) {
-            // conv_out and the law in one k_out_law launch (no tap planes, no k_coupling)
-            OutLawArgs oa;
-            std::memset(&oa, 0, sizeof(oa));
-            for (int n = 0; n < 2; n++) {
-                const NetParams& np = c.net[n];
-                ConvProb& q = oa.p[n];
-                const Slab s = in_slab(n, 0);
-                q.in = y[n];
-                q.in_part = s.part;
-                q.in_nparts = s.nparts;
-                q.part_stride = L.st_parts;
-                q.gamma = ln ? P + np.ln_out_g : none;
-                q.beta = ln ? P + np.ln_out_b : none;
-                oa.w[n] = P + np.conv_out_k;
-                oa.b[n] = P + np.conv_out_b;
-                oa.so_w[n] = n == 0 ? so0 : so1;
-            }
-            oa.u = u;
-            oa.v = v;
-            oa.tanh_w = P + c.net[0].tanh_w;
-            oa.ld_part = ld_part;
-            oa.H = c.H;
-            oa.W = c.W;
-            oa.D = c.D;
-            oa.mask = c.mask;
-            oa.mask_c = c.mask_c;
-            oa.hc = c.hc;
-            oa.wc = c.wc;
-            oa.dc1 = c.dc1;
-            oa.dc2 = c.dc2;
-            oa.dir = dir;
-            oa.TR = otr;
-            oa.TW = otw;
-            oa.tiles_r = (c.hc + otr - 1) / otr;
-            oa.tiles_c = (c.wc + otw - 1) / otw;
-            oa.np = L.ld_parts;
-            oa.tw_mag = udiv_magic_host((uint32_t)otw);
-            oa.twp_mag = udiv_magic_host((uint32_t)otw + 2);
-            const double npx = (double)c.hc * c.wc;
-            const double fl = 2.0 * B * npx * 9.0 * c.nk * c.dc2 * 2;
-            const double by = 4.0 * (B * (npx * c.nk * 2 + 2.0 * c.H * c.W * c.D + 2 * npx * c.dc2) +
-                                     (ln ? 4.0 * npx * c.nk : 0.0));
-            E.record("k_out_law", fl, by, [oa, B](void* st) { launch_out_law(oa, B, (hipStream_t)st); });
-            return;
         }
         if (c.net[0].co.fmt == PK_TAP && E.p.tap_pw && 9 * c.dc2 <= c.nk && pr.size() == 2) {
             // tap GEMM C = LN_out(LReLU(y)) . W_tap as a streamed 1x1 conv into the dead t1 buffer;
@@ -1224,13 +1130,6 @@ static void ensure_tables(Plan& p) {
     if (!p.aux_map.empty())
         hip_check(hipMemcpy(p.dev_aux_map, p.aux_map.data(), p.aux_map.size() * sizeof(int64_t), hipMemcpyHostToDevice),
                   "hipMemcpy(aux map)");
-    if (p.gc_conc) {   // (a plan moved to another device keeps the old device's streams: never reused)
-        for (int i = 0; i < 2; i++) {
-            hip_check(hipStreamCreateWithFlags(&p.fside[i], hipStreamNonBlocking), "hipStreamCreate");
-            hip_check(hipEventCreateWithFlags(&p.fev_join[i], hipEventDisableTiming), "hipEventCreate");
-        }
-        hip_check(hipEventCreateWithFlags(&p.fev_fork, hipEventDisableTiming), "hipEventCreate");
-    }
     size_t nbw = std::max<size_t>(1, p.bw_map.size()) * sizeof(int64_t);
     hip_check(hipMalloc(&p.dev_bw_map, nbw), "hipMalloc(bw map)");
     if (!p.bw_map.empty())
@@ -1257,17 +1156,13 @@ int cnf_plan_create(const cnf_flow_desc* desc, cnf_plan** out) {
     if (!out) return fail(CNF_E_INVALID, "null out");
     *out = nullptr;
     CNF_TRY
-    Plan* p = build_plan(desc);
-    if (const char* e = std::getenv("CNF_PW")) p->use_pw = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CNF_TAP_PW")) p->tap_pw = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CNF_OUT_LAW")) p->out_law = std::atoi(e);
-    if (const char* e = std::getenv("CNF_GC_CONC")) p->gc_conc = std::atoi(e) != 0;
-    if (const char* e = std::getenv("CNF_OUT_LAW_KS")) p->out_law_ks = std::atoi(e);
+    Plan* p = build_plan(desc);   // (parses desc->debug_options into p->opts)
+    OptScope os(&p->opts);
+    p->use_pw = p->tap_pw = p->opts.pw != 0;
     // validate tiling / LDS budget for every layer up-front
     for (const auto& c : p->couplings) (void)conv_geo(c.hc, c.wc);
-    // training: k_net_lds layers whose fused backward fits LDS use it (CNF_LDS_BWD=0: none, A/B knob)
-    bool lds_bwd = true;
-    if (const char* e = std::getenv("CNF_LDS_BWD")) lds_bwd = std::atoi(e) != 0;
+    // training: k_net_lds layers whose fused backward fits LDS use it (debug option LDS_BWD=0: none)
+    const bool lds_bwd = p->opts.lds_bwd != 0;
     for (auto& c : p->couplings) {
         LdsBwdArgs a;
         c.lds_bwd = lds_bwd && c.use_lds && ldsbwd_setup(*p, c, a) > 0;
@@ -1285,16 +1180,13 @@ void cnf_plan_destroy(cnf_plan* plan) {
         if (plan->p->dev_bw_map) (void)hipFree(plan->p->dev_bw_map);
         for (hipEvent_t e : plan->p->ev) (void)hipEventDestroy(e);
         if (plan->p->ev_fork) (void)hipEventDestroy(plan->p->ev_fork);
-        if (plan->p->fev_fork) (void)hipEventDestroy(plan->p->fev_fork);
-        for (int i = 0; i < 2; i++) {
-            if (plan->p->fev_join[i]) (void)hipEventDestroy(plan->p->fev_join[i]);
-            if (plan->p->fside[i]) (void)hipStreamDestroy(plan->p->fside[i]);
-        }
         if (plan->p->ev_join) (void)hipEventDestroy(plan->p->ev_join);
         if (plan->p->side) (void)hipStreamDestroy(plan->p->side);
         for (hipStream_t s : plan->p->wside)
             if (s) (void)hipStreamDestroy(s);
         for (hipEvent_t e : plan->p->tev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : plan->p->nll_ev)
+            if (e) (void)hipEventDestroy(e);
         delete plan->p;
     }
     delete plan;
@@ -1303,6 +1195,7 @@ void cnf_plan_destroy(cnf_plan* plan) {
 int cnf_plan_num_layers(const cnf_plan* plan) { return plan ? (int)plan->p->layers.size() : -1; }
 
 int cnf_plan_layer_info(const cnf_plan* plan, int layer, cnf_layer_info* out) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !out) return fail(CNF_E_INVALID, "null argument");
     const Plan& p = *plan->p;
     if (layer < 0 || layer >= (int)p.layers.size()) return fail(CNF_E_INVALID, "layer index out of range");
@@ -1337,6 +1230,7 @@ int cnf_plan_num_param_tensors(const cnf_plan* plan) { return plan ? (int)plan->
 
 int cnf_plan_param_tensor(const cnf_plan* plan, int index, char* name, int name_cap, int64_t* offset, int* ndim,
                           int shape[4]) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan) return fail(CNF_E_INVALID, "null plan");
     const Plan& p = *plan->p;
     if (index < 0 || index >= (int)p.params.size()) return fail(CNF_E_INVALID, "param index out of range");
@@ -1354,6 +1248,7 @@ int cnf_plan_param_tensor(const cnf_plan* plan, int index, char* name, int name_
 int64_t cnf_plan_aux_floats(const cnf_plan* plan) { return plan ? std::max<int64_t>(1, plan->p->n_aux) : -1; }
 
 int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux) return fail(CNF_E_INVALID, "null argument");
     CNF_TRY
     Plan& p = *plan->p;
@@ -1365,6 +1260,7 @@ int cnf_pack_params(cnf_plan* plan, const float* params, float* aux, void* strea
 }
 
 size_t cnf_plan_workspace_bytes(const cnf_plan* plan, int B) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || B <= 0) return 0;
     return plan->p->layout(B).total;
 }
@@ -1401,10 +1297,7 @@ static void flow_forward(Plan& p, const float* params, const float* aux, const f
     }
     // a k_net_lds layer followed directly by another one leaves its coupling law to that layer's
     // kernel (CoupPend): no k_coupling launch for it. Not when saving layer inputs (training).
-    static const bool fuse = [] {   // A/B knob
-        const char* e = std::getenv("CNF_FUSE_COUPLING");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool fuse = p.opts.fuse_coupling != 0;   // (debug option FUSE_COUPLING=0: a k_coupling per layer)
     CoupPend pend;
     bool have_pend = false;
     // training: a layer whose output is the next coupling's input writes it straight into that coupling's
@@ -1506,6 +1399,7 @@ extern "C" {
 
 int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
                      float* logdet_per_image, void* workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy) return fail(CNF_E_INVALID, "xy and zy must not alias (out-of-place only)");
@@ -1518,6 +1412,7 @@ int cnf_flow_forward(cnf_plan* plan, const float* params, const float* aux, cons
 int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux, const float* xy, float logit_a,
                            float alpha, uint64_t seed, uint64_t offset, float* xy_noisy, float* zy,
                            float* logdet_per_image, void* workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !xy || !xy_noisy || !zy || !logdet_per_image || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy || xy_noisy == zy || xy_noisy == xy)
@@ -1541,6 +1436,7 @@ int cnf_flow_forward_noise(cnf_plan* plan, const float* params, const float* aux
 }
 
 size_t cnf_plan_train_workspace_bytes(const cnf_plan* plan, int B) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || B <= 0) return 0;
     try {
         return plan->p->train_layout(B).total;
@@ -1551,6 +1447,7 @@ size_t cnf_plan_train_workspace_bytes(const cnf_plan* plan, int B) {
 
 int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux, const float* xy, float* zy,
                            float* logdet_per_image, void* train_workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !xy || !zy || !logdet_per_image || !train_workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy) return fail(CNF_E_INVALID, "xy and zy must not alias (out-of-place only)");
@@ -1562,6 +1459,7 @@ int cnf_flow_forward_train(cnf_plan* plan, const float* params, const float* aux
 
 int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, const float* zy, void* train_workspace,
                       int B, float inv_batch, float* dparams, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !xy || !zy || !train_workspace || !dparams || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     CNF_TRY
@@ -1575,6 +1473,7 @@ int cnf_flow_backward(cnf_plan* plan, const float* params, const float* xy, cons
 int cnf_flow_backward_ex(cnf_plan* plan, const float* params, const float* xy, const float* zy, void* train_workspace,
                          int B, const float* global_count, float* dparams, cnf_layer_done_fn layer_done, void* user,
                          void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !xy || !zy || !train_workspace || !dparams || !global_count || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     CNF_TRY
@@ -1588,6 +1487,7 @@ int cnf_flow_backward_ex(cnf_plan* plan, const float* params, const float* xy, c
 
 int cnf_coupling_backward(cnf_plan* plan, int layer, const float* params, const float* u, const float* dv, float* du,
                           float dlogdet, void* train_workspace, int B, float* dparams, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !u || !dv || !du || !train_workspace || !dparams || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     CNF_TRY
@@ -1619,6 +1519,7 @@ static void flow_inverse(Plan& p, const float* params, const float* aux, const f
 
 int cnf_flow_inverse(cnf_plan* plan, const float* params, const float* aux, const float* zy, float* xy,
                      void* workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !xy || !zy || !workspace || B <= 0)
         return fail(CNF_E_INVALID, "null argument or B <= 0");
     if (xy == zy) return fail(CNF_E_INVALID, "zy and xy must not alias (out-of-place only)");
@@ -1657,10 +1558,7 @@ static void flow_inverse(Plan& p, const float* params, const float* aux, const f
     // deferred inverse law (as the forward's, CoupPend::dir = -1): an LDS layer whose successor in
     // the inverse order (the previous layer by index) launches k_net_lds or the boundary maps leaves
     // its law to that kernel — no k_coupling launch for it
-    static const bool fuse = [] {   // A/B knob (shared with the forward)
-        const char* e = std::getenv("CNF_FUSE_COUPLING");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool fuse = p.opts.fuse_coupling != 0;   // (debug option FUSE_COUPLING=0: a k_coupling per layer)
     CoupPend pend;
     bool have_pend = false;
     int bi = (int)p.boundaries.size() - 1;
@@ -1720,6 +1618,7 @@ extern "C" {
 
 int cnf_coupling_forward(cnf_plan* plan, int layer, const float* params, const float* aux, const float* u, float* v,
                          float* logdet_accum, void* workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !u || !v || !workspace || B <= 0) return fail(CNF_E_INVALID, "null argument");
     CNF_TRY
     Plan& p = *plan->p;
@@ -1743,6 +1642,7 @@ int cnf_coupling_forward(cnf_plan* plan, int layer, const float* params, const f
 
 int cnf_coupling_inverse(cnf_plan* plan, int layer, const float* params, const float* aux, const float* v, float* u,
                          void* workspace, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !params || !aux || !u || !v || !workspace || B <= 0) return fail(CNF_E_INVALID, "null argument");
     CNF_TRY
     Plan& p = *plan->p;
@@ -1783,28 +1683,49 @@ int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out
 
 int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image, float* per_image,
             float* sums, int B, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !xy || !zy || !logdet_per_image || !per_image || !sums || B <= 0)
         return fail(CNF_E_INVALID, "null argument");
     CNF_TRY
     Plan& p = *plan->p;
     ensure_tables(p);
     const cnf_flow_desc& d = p.desc;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    hip_check(hipStreamIsCapturing((hipStream_t)stream, &cap), "hipStreamIsCapturing");
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    std::lock_guard<std::mutex> lk(*p.nll_mu);
     int slot = -1;
-    {
-        std::lock_guard<std::mutex> lk(*p.nll_mu);
-        for (size_t i = 0; i < p.nll_streams.size(); i++)
-            if (p.nll_streams[i] == stream) slot = (int)i;
-        if (slot < 0) {
-            if ((int)p.nll_streams.size() == Plan::NLL_SLOTS)
-                throw std::runtime_error("cnf_nll: more than 64 streams on one plan");
-            p.nll_streams.push_back(stream);
-            slot = (int)p.nll_streams.size() - 1;
-        }
+    for (size_t i = 0; i < p.nll_streams.size(); i++)
+        if (p.nll_streams[i] == stream) slot = (int)i;
+    if (slot < 0 && (int)p.nll_streams.size() < Plan::NLL_SLOTS) {
+        p.nll_streams.push_back(stream);
+        p.nll_ev.push_back(nullptr);
+        p.nll_last.push_back(0);
+        slot = (int)p.nll_streams.size() - 1;
     }
+    if (slot < 0) {
+        // every slot has its stream: take the least recently used one. Its counter is back at 0 once that
+        // stream's last cnf_nll has completed, so this launch waits for it (stream-ordered, no host wait)
+        slot = 0;
+        for (int i = 1; i < Plan::NLL_SLOTS; i++)
+            if (p.nll_last[i] < p.nll_last[slot]) slot = i;
+        if (p.nll_ev[slot] != nullptr && hipEventQuery(p.nll_ev[slot]) != hipSuccess)
+            hip_check(hipStreamWaitEvent((hipStream_t)stream, p.nll_ev[slot], 0), "hipStreamWaitEvent");
+        else if (p.nll_ev[slot] == nullptr && capturing)
+            throw std::runtime_error("cnf_nll: a 65th stream on one plan during graph capture (reuse needs an "
+                                     "uncaptured call on the slot's stream first)");
+        p.nll_streams[slot] = stream;
+    }
+    p.nll_last[slot] = ++p.nll_clock;
     unsigned* done = reinterpret_cast<unsigned*>(p.dev_table + p.host_table.size()) + slot;
     launch_nll(xy, zy, logdet_per_image, per_image, sums, done, B, d.io_h * d.io_w, d.io_d, d.x_d, d.lambda_y,
                (hipStream_t)stream);
     check_launch();
+    if (!capturing) {   // (the slot's completion point, for a later reuse by another stream)
+        if (p.nll_ev[slot] == nullptr)
+            hip_check(hipEventCreateWithFlags(&p.nll_ev[slot], hipEventDisableTiming), "hipEventCreate");
+        hip_check(hipEventRecord(p.nll_ev[slot], (hipStream_t)stream), "hipEventRecord");
+    }
     return CNF_OK;
     CNF_CATCH
 }
@@ -1894,6 +1815,7 @@ int cnf_toy_nll_sums(const float* per_sample, float* sums, int B, void* stream) 
 // shape words of coupling `coupling`'s k_net_lds launch (0 if the layer is streamed); host only, used
 // by csrc/gen_netlds_shapes.py to generate the shape-specialised instantiations' table
 int cnf_debug_netlds_shape(const cnf_plan* plan, int coupling, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words || cap < NETSHAPE_WORDS) return -1;
     const Plan& p = *plan->p;
     if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
@@ -1911,6 +1833,7 @@ int cnf_debug_netlds_nshapes() { return netlds_num_shapes(); }
 int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap);
 // k_gc launch shapes of a B-image forward (host-only dry run, as cnf_debug_pw_shapes)
 int cnf_debug_gc_launch_shapes(cnf_plan* plan, int B, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words || B <= 0) return -1;
     const int n = cnf_debug_pw_shapes(plan, B, words, cap);   // the dry run also records the k_gc shapes
     if (n < 0) return -1;
@@ -1923,6 +1846,7 @@ int cnf_debug_gc_launch_shapes(cnf_plan* plan, int B, int* words, int cap) {
 // launch names of a B-image forward (direction +1) or inverse (-1) from a host-only dry run, one per
 // line into out (cap bytes, NUL-terminated); returns the number of launches, -1 on error
 int cnf_debug_schedule(cnf_plan* plan, int B, int direction, char* out, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !out || cap <= 0 || B <= 0 || (direction != 1 && direction != -1)) return -1;
     Plan& p = *plan->p;
     CNF_TRY
@@ -1951,6 +1875,7 @@ int cnf_debug_schedule(cnf_plan* plan, int B, int direction, char* out, int cap)
 }
 
 int cnf_debug_pw_shapes(cnf_plan* plan, int B, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words || B <= 0) return -1;
     Plan& p = *plan->p;
     CNF_TRY
@@ -1980,6 +1905,7 @@ int cnf_debug_pw_words() { return PWSHAPE_WORDS; }
 
 // shape words of coupling `coupling`'s k_gc launches, one GcShape per group (0 if it has none)
 int cnf_debug_gc_shape(const cnf_plan* plan, int coupling, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words) return -1;
     const Plan& p = *plan->p;
     if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
@@ -2019,6 +1945,7 @@ int cnf_debug_gc_words() { return GCSHAPE_WORDS; }
 // t2 layout of a coupling (Coupling::t2_*): [mapped, floats per pixel of the image, gc, then per branch
 // (slice offset of pixel 0, pixel stride, out_off, cout), then conv_b's quad map (gc / 4 pairs, mapped only)]
 int cnf_debug_t2_layout(const cnf_plan* plan, int coupling, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words) return -1;
     const Plan& p = *plan->p;
     if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
@@ -2037,6 +1964,7 @@ int cnf_debug_t2_layout(const cnf_plan* plan, int coupling, int* words, int cap)
 }
 
 int cnf_debug_t1_layout(const cnf_plan* plan, int coupling, int* words, int cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !words) return -1;
     const Plan& p = *plan->p;
     if (coupling < 0 || coupling >= (int)p.couplings.size()) return -1;
@@ -2064,6 +1992,7 @@ int cnf_plan_num_recorded_launches(const cnf_plan* plan) { return plan ? (int)pl
 
 int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int name_cap, double* flops,
                                   double* bytes) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan) return fail(CNF_E_INVALID, "null plan");
     const Plan& p = *plan->p;
     if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");
@@ -2074,12 +2003,14 @@ int cnf_plan_recorded_launch_info(const cnf_plan* plan, int i, char* name, int n
 }
 
 int cnf_plan_set_launch_timing(cnf_plan* plan, int on) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan) return fail(CNF_E_INVALID, "null plan");
     plan->p->timing = on != 0;
     return CNF_OK;
 }
 
 int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || !ms) return fail(CNF_E_INVALID, "null argument");
     const Plan& p = *plan->p;
     if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");
@@ -2095,6 +2026,7 @@ int cnf_plan_launch_time_ms(const cnf_plan* plan, int i, float* ms) {
 }
 
 int64_t cnf_plan_weight_map(const cnf_plan* plan, int which, int64_t* out, int64_t cap) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan || (which != 0 && which != 1)) return fail(CNF_E_INVALID, "null plan or which not in {0, 1}");
     const std::vector<int64_t>& m = which == 0 ? plan->p->aux_map : plan->p->bw_map;
     if (out)
@@ -2103,6 +2035,7 @@ int64_t cnf_plan_weight_map(const cnf_plan* plan, int which, int64_t* out, int64
 }
 
 int cnf_plan_relaunch(cnf_plan* plan, int i, void* stream) {
+    OptScope os_(plan ? &plan->p->opts : nullptr);
     if (!plan) return fail(CNF_E_INVALID, "null plan");
     Plan& p = *plan->p;
     if (i < 0 || i >= (int)p.recorded.size()) return fail(CNF_E_INVALID, "launch index out of range");

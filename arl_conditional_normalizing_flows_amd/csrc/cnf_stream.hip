@@ -33,7 +33,11 @@ constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 // diagnostic per-workgroup stamps (CNF_PW_STAMPS=SID builds only; never in timed runs): thread 0 of
 // every workgroup of the instantiation SID records s_memrealtime at its start (0), before (1) and
 // after (2) the prologue barrier and after each of its images (3 + i)
+#if defined(CNF_PW_STAMPS) || defined(CNF_GC_WGSTAMPS)
 constexpr int PW_ST_WG = 2048, PW_ST_N = 12;
+#else
+constexpr int PW_ST_WG = 1, PW_ST_N = 1;   // (no stamps in this build: a placeholder, never written)
+#endif
 __device__ long long g_pw_stamps[PW_ST_WG][PW_ST_N];
 #ifdef CNF_PW_STAMPS
 #define PWSTAMP(i)                                                                                       \
@@ -49,39 +53,16 @@ int read_pw_stamps(long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pw_stamps), sizeof(g_pw_stamps)) == hipSuccess ? 0 : -1;
 }
 
-// images of a wave in flight ahead of the one being computed (a ring of D buffers): one. Deeper
-// rings for the narrow non-residual convs measured slower at cfg2 B=64 (CNF_PW_DEPTH=2 / 4: conv_a
-// 19.1 -> 20.8 / 21.0 us, conv_out 11.9 -> 14.1 us; issuing them with the prologue's loads,
-// CNF_PW_EARLY=1, slower still), and for the residual conv_b in round 2
-#ifndef CNF_PW_DEPTH
-#define CNF_PW_DEPTH 1
-#endif
-#ifndef CNF_PW_EARLY
-#define CNF_PW_EARLY 0
-#endif
-#ifndef CNF_PW_BQD
-#define CNF_PW_BQD 1   // B-quad read distance in groups (specialised k_pw)
-#endif
-constexpr int pw_depth(int gm, bool res) { return res ? 1 : gm <= 4 ? CNF_PW_DEPTH : (CNF_PW_DEPTH < 2 ? CNF_PW_DEPTH : 2); }
-
+// images of a wave in flight ahead of the one being computed: one. Deeper rings measured slower at
+// cfg2 B=64 (two / four images: conv_a 19.1 -> 20.8 / 21.0 us, conv_out 11.9 -> 14.1 us; issued with
+// the prologue's loads, slower still), and for the residual conv_b in round 2
+//
 // DUAL (generic non-tap instantiations of the training forward only): every output element is also
 // stored densely ([HW][cout]) to P.out2 -- conv_a's full t1 saved for the backward in the same launch
-//
-// SH (shared-tile mode, CNF_PW_SH builds, LN on load, not tap mode): NS = PW_NS image streams of NW
-// waves share the workgroup -- wave w computes pixel subtile w % NW of images ii = w / NW, + NS, ...
-// -- and the tile's LN gamma / beta live once in LDS instead of in every wave's registers: half the
-// prologue bytes per CU (one workgroup per CU loads the weights and gamma/beta once for NS x the
-// images) and 56 fewer VGPRs at conv_b. The LN partial slots stay per (tile, subtile): bitwise the
-// plain mode's partition.
-#ifndef PW_NS
-#define PW_NS 2
-#endif
-template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false, bool SH = false>
-__global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_MINW) void k_pw(ConvArgs a) {
+template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false>
+__global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = PW_NW;
-    constexpr int NS = SH ? PW_NS : 1;
-    static_assert(!SH || (LN && !TAP && !DUAL), "shared-tile k_pw: LN on load, no tap mode, no dual store");
     PWSTAMP(0);
     const ConvProb P = a.p[blockIdx.y];
     const int HW = PA(H) * PA(W);
@@ -89,11 +70,10 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
     const int img0 = (blockIdx.x / PA(tiles_per_img)) * a.ipw;
     const int nimg = min(a.ipw, a.B - img0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int sub = SH ? wave % NW : wave, strm = SH ? wave / NW : 0;   // pixel subtile, image stream
+    const int sub = wave;   // pixel subtile
     const int i16 = lane & 15, kq = lane >> 4;
     const int cin = PP(cin), G = (cin + 15) >> 4, cout = PP(cout);
     constexpr int NSJ = 16 * NR;
-    f4* lgb = reinterpret_cast<f4*>(smem + a.gb_off);   // SH: gamma [GM][NW][64] then beta
     float* lw = reinterpret_cast<float*>(smem + PP(lds_w_off));
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
@@ -143,10 +123,9 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
         const bool st = all_st || ((ch < 32 ? (PP(st_mask_lo) >> ch) : (PP(st_mask_hi) >> (ch - 32))) & 1u) != 0u;
         return (pv(r) && chv(n) && st) ? obase + (uint32_t)(r * PP(out_cs) + 16 * n) * 4u : BUF_OOB;
     };
-    // image activations (+ residual) in registers, a ring of D images (pw_depth)
-    constexpr int D = pw_depth(GM, RES);
-    f4 x[D][GM];
-    float rv[D][NR][4];
+    // image activations (+ residual) in registers: the current image and the next
+    f4 x[GM];
+    float rv[NR][4];
     // tap mode: element k = 16g + 4kq + j of the lane's im2col row -> offset inside one image of u
     auto toff = [&](int g, int j) -> uint32_t {
         const int k = 16 * g + 4 * kq + j;
@@ -194,15 +173,9 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
                 }
         }
     };
-    if (strm < nimg) load_img(strm, x[0], rv[0]);
+    if (0 < nimg) load_img(0, x, rv);
     f4 gm[GM], bt[GM];
-    if (SH) {   // stream 0 stages gamma, stream 1 beta (NS >= 2), each for its subtile's lanes
-        if (strm < 2) {
-            const auto rg = buf_rsrc(strm == 0 ? P.gamma : P.beta, in_img);
-#pragma unroll
-            for (int g = 0; g < GM; g++) gm[g] = buf_load4(rg, gok(g) ? aoffg(g) : BUF_OOB);
-        }
-    } else if (LN) {
+    if (LN) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
 #pragma unroll
         for (int g = 0; g < GM; g++) {
@@ -234,23 +207,12 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
     // memory round trip as the loads above and the weights below (folded after the weight copy)
     const bool lnpre = LN && wave < nimg;   // (image wave: the LN table below is per workgroup)
     const LnSlots slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : LnSlots{};
-    // the rest of the ring's first images: in flight with the prologue's loads (CNF_PW_EARLY) or
-    // issued once the weights are in LDS
-    if (CNF_PW_EARLY) {
-#pragma unroll
-        for (int j = 1; j < D; j++)
-            if (j < nimg) load_img(j, x[j], rv[j]);
-    }
     // weights -> LDS; per-image input LN (mean, rstd) -> LDS
     int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
     asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
-    copy_to_lds<64 * NW * NS>(P.wt, lw, nwf);
-    if (SH && strm < 2) {
-#pragma unroll
-        for (int g = 0; g < GM; g++) lgb[((strm * GM + g) * NW + sub) * 64 + lane] = gm[g];
-    }
+    copy_to_lds<64 * NW>(P.wt, lw, nwf);
     if (LN) {
-        for (int i = wave; i < nimg; i += NW * NS) {
+        for (int i = wave; i < nimg; i += NW) {
             float mu, rs;
             if (i == wave && lnpre)
                 in_ln_finish(P, img0 + i, slot0, mu, rs);
@@ -265,11 +227,6 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
     PWSTAMP(1);
     __syncthreads();
     PWSTAMP(2);
-    if (!CNF_PW_EARLY) {
-#pragma unroll
-        for (int j = 1; j < D; j++)
-            if (strm + j * NS < nimg) load_img(strm + j * NS, x[j], rv[j]);
-    }
 
     const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
     // one image: A operand from xc / rc, which then receive image pf (when it exists)
@@ -280,10 +237,6 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
         float av[GM][4];
 #pragma unroll
         for (int g = 0; g < GM; g++) {
-            if (SH) {
-                gm[g] = lgb[(g * NW + sub) * 64 + lane];
-                bt[g] = lgb[((GM + g) * NW + sub) * 64 + lane];
-            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float v = !TAP || P.act ? lrelu(xc[g][j]) : xc[g][j];   // conv_in reads raw u
@@ -307,10 +260,9 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
         // compiler from hoisting every group's LDS reads (NR quads each) into live registers
         // (the generic instantiations keep the plain per-group loop: their runtime group bound already
         // limits the hoisting, and the extra buffer costs them registers)
-        // B quads of the specialised instantiations in a ring of BQD + 1 groups, read BQD groups ahead
-        // (the scheduler sinks a group's reads to the previous group's last MFMA: at distance 1 the LDS
-        // latency is exposed once per group)
-        constexpr int BQD = CNF_PW_BQD;
+        // B quads of the specialised instantiations read one group ahead (two groups ahead measured
+        // no better: the LDS reads are not what each MFMA group waits on)
+        constexpr int BQD = 1;
         f4 bq[BQD + 1][NR];
 #pragma unroll
         for (int j = 0; j < BQD; j++)
@@ -367,41 +319,21 @@ __global__ __launch_bounds__(64 * PW_NW * (SH ? PW_NS : 1), SH ? PW_NS : CNF_PW_
             ln_partial(vals, valid,
                        P.out_part + ((size_t)img * PP(part_stride) + P.out_part_base + tile * NW + sub) * LNP);
     };
-    // this wave's images strm, strm + NS, ... in a ring of D buffers
-    for (int i0 = strm; i0 < nimg; i0 += D * NS) {
-#pragma unroll
-        for (int j = 0; j < D; j++) {
-            const int ii = i0 + j * NS;
-            if (ii >= nimg) break;
-            step(ii, x[j], rv[j], ii + D * NS);   // buffer j then receives image ii + D * NS
-            PWSTAMP(3 + ii);
-        }
+    // this wave's images: the buffers then receive image ii + 1
+    for (int ii = 0; ii < nimg; ii++) {
+        step(ii, x, rv, ii + 1);
+        PWSTAMP(3 + ii);
     }
 }
 
 #undef PP
 #undef PA
 
-#ifndef CNF_PW_SH
-#define CNF_PW_SH 0
-#endif
-bool pw_shared_tile() { return CNF_PW_SH != 0; }
-int pw_streams() { return PW_NS; }
-
 template <int S>
 bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStream_t st) {
     if constexpr (S < CNF_PW_NSHAPES) {
         if (sid == S) {
             constexpr PwShape k = kPwShapes[S];
-#if CNF_PW_SH
-            if constexpr (k.ln != 0 && k.tap == 0) {
-                if (a.sh) {
-                    CNF_LAUNCH((k_pw<k.nr, k.gm, true, k.res != 0, S, false, false, true>), g, dim3(64 * PW_NW * PW_NS),
-                               lds, st, a);
-                    return true;
-                }
-            }
-#endif
             CNF_LAUNCH((k_pw<k.nr, k.gm, k.ln != 0, k.res != 0, S, k.tap != 0>), g, b, lds, st, a);
             return true;
         }
@@ -414,7 +346,7 @@ int pw_num_shapes() { return CNF_PW_NSHAPES; }
 
 void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
-    const bool generic = std::getenv("CNF_PW_GENERIC") != nullptr;   // A/B knob (read per launch: tests switch it)
+    const bool generic = opts().generic != 0;   // debug option GENERIC=1
     bool dual = false;
     for (int i = 0; i < a.nprob; i++) dual |= a.p[i].out2 != nullptr;
     if (dual) {   // training forward conv_a with the dense t1 copy: generic instantiations only
@@ -450,22 +382,6 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
 #undef CNF_PW_TCASE
         throw std::invalid_argument("k_pw tap mode: no instantiation for this shape");
     }
-#if CNF_PW_SH
-    if (a.sh) {   // shared-tile generic instantiations
-        if (!ln || tap) throw std::invalid_argument("k_pw shared tile: LN on load, no tap mode");
-#define CNF_PW_SCASE(NR_, GM_, RES_)                                                                  \
-        if (nr == NR_ && gm == GM_ && res == RES_) {                                                  \
-            CNF_LAUNCH((k_pw<NR_, GM_, true, RES_, -1, false, false, true>), g, dim3(64 * PW_NW * PW_NS), lds, st, a); \
-            return;                                                                                   \
-        }
-#define CNF_PW_SNR(GM_, RES_) CNF_PW_SCASE(1, GM_, RES_) CNF_PW_SCASE(2, GM_, RES_) CNF_PW_SCASE(3, GM_, RES_) CNF_PW_SCASE(4, GM_, RES_)
-        CNF_PW_SNR(1, false) CNF_PW_SNR(2, false) CNF_PW_SNR(4, false) CNF_PW_SNR(8, false)
-        CNF_PW_SNR(1, true) CNF_PW_SNR(2, true) CNF_PW_SNR(4, true) CNF_PW_SNR(8, true)
-#undef CNF_PW_SNR
-#undef CNF_PW_SCASE
-        throw std::invalid_argument("k_pw shared tile: no instantiation for this shape");
-    }
-#endif
 #define CNF_PW_CASE(NR_, GM_, LN_, RES_)                                              \
     if (nr == NR_ && gm == GM_ && ln == LN_ && res == RES_) {                          \
         CNF_LAUNCH((k_pw<NR_, GM_, LN_, RES_, -1>), g, b, lds, st, a);             \
@@ -890,8 +806,7 @@ int gc_num_shapes() { return CNF_GC_NSHAPES; }
 
 // table entry matching a's shape, -1 for the generic instantiation
 static int gc_shape_id(const GcArgs& a) {
-    const char* e = std::getenv("CNF_GC_GENERIC");   // A/B knob (read per launch: tests switch it)
-    const bool generic = e && std::atoi(e) != 0;
+    const bool generic = opts().generic != 0;   // debug option GENERIC=1
     if (!generic)
         for (int sid = 0; sid < CNF_GC_NSHAPES; sid++)
             if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0) return sid;

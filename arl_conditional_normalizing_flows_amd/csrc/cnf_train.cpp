@@ -41,17 +41,12 @@ struct LnIn {
     int act = 0;
 };
 
-// CNF_LN2_MASK=0: zero dt1's gradient buffer before the grouped branches' data gradients instead of
-// masking the channels outside their windows in the LN2 backward (A/B; read per call: tests switch it)
-bool ln2_mask() {
-    const char* e = std::getenv("CNF_LN2_MASK");
-    return !(e && std::atoi(e) == 0);
-}
+// debug option TRAIN_ALT bit 32: zero dt1's gradient buffer before the grouped branches' data gradients
+// instead of masking the channels outside their windows in the LN2 backward
+bool ln2_mask() { return (opts().train_alt & 32) == 0; }
 
-bool fused_lnr() {   // A/B knob: the LN backward's reduction in the producing data-gradient kernel (per call)
-    const char* e = std::getenv("CNF_LNR_FUSE");
-    return !(e && std::atoi(e) == 0);
-}
+// the LN backward's reduction in the producing data-gradient kernel (TRAIN_ALT bit 16: k_lnb_reduce)
+bool fused_lnr() { return (opts().train_alt & 16) == 0; }
 
 int wgrad_chunks(int B, int npx) {
     const long long total = (long long)B * npx;
@@ -243,12 +238,11 @@ TrainLayout Plan::train_layout(int B) const {
             for (int n = 0; n < 2; n++) T.dso_l[par][n] = take(Bz * m_so * 4);
         }
     }
-    // streamed layers' saved activations, when all of them fit 16 GiB (CNF_TRAIN_SAVE=0: recompute)
+    // streamed layers' saved activations, when all of them fit 16 GiB (TRAIN_SCHED bit 2: recompute)
     T.ssave.assign(couplings.size(), TrainLayout::StreamSave{});
     T.has_ssave.assign(couplings.size(), 0);
     {
-        bool on = true;
-        if (const char* e = std::getenv("CNF_TRAIN_SAVE")) on = std::atoi(e) != 0;
+        const bool on = (opts.train_sched & 2) == 0;
         size_t need = 0;
         for (const Coupling& c : couplings) {
             if (c.use_lds || c.t2_mapped) continue;
@@ -376,10 +370,7 @@ int conv_dgrad(TExec& E, int h, int w, const float* dy, int dy_cs, int dy_off, i
 
 // dW, db of a conv: X (cin channels at x_cs/x_off, LN-on-load) and dY (cout at dy_cs/dy_off)
 hipEvent_t tevent(Plan& p) {
-    static const int flags = [] {   // diagnostics: CNF_TRAIN_EVFLAGS=0 -> timing events
-        const char* e = std::getenv("CNF_TRAIN_EVFLAGS");
-        return e && std::atoi(e) == 0 ? (int)hipEventDefault : (int)hipEventDisableTiming;
-    }();
+    constexpr int flags = (int)hipEventDisableTiming;
     if (p.tev_next == p.tev.size()) {
         hipEvent_t e;
         hchk(hipEventCreateWithFlags(&e, flags), "hipEventCreate");
@@ -453,13 +444,10 @@ hipEvent_t conv_wgrad_impl(TExec& E, int h, int w, const float* x, int x_cs, int
         launch_grad_scatter(a.part, a.chunks, nw + cout, map + pc.dw, E.dparams, E.st);
         return nullptr;
     }
-    // k_wgrad_direct (k_wgrad_band with CNF_WGRAD_DIRECT=0): rows of [weights | bias]; the dense image
+    // k_wgrad_direct (k_wgrad_band with TRAIN_ALT bit 2): rows of [weights | bias]; the dense image
     // keeps the bias right after the weights (pc.db == pc.dw + taps * cin * cout), so one scatter
     // reduces both
-    const bool direct = [] {   // (read per call: tests switch it)
-        const char* e = std::getenv("CNF_WGRAD_DIRECT");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool direct = (opts().train_alt & 2) == 0;
     if (direct && wgrad_direct_ok(h, w, pc.taps)) {
         a.chunks = wgrad_direct_chunks(E.B, h);
         a.chunk_px = -1;
@@ -568,10 +556,14 @@ hipEvent_t coupling_backward_lds(TExec& E, const Coupling& c, const float* u, co
     a.offs = E.p.dev_table + c.dev_bwd_offs;
     a.part = E.at<float>(split && par == 1 ? E.T.rows2 : E.T.rows);
     a.row = E.T.row_max;
-    static const bool stamps = [] {   // diagnostics
+#ifdef CNF_DIAG
+    static const bool stamps = [] {   // diagnostic builds: phase stamps (profiles/diag/diag_bwd_stamps.py)
         const char* e = std::getenv("CNF_LDSBWD_STAMPS");
         return e && std::atoi(e) != 0;
     }();
+#else
+    constexpr bool stamps = false;
+#endif
     a.stamps = stamps ? 1 : 0;
     const NetParams& n0 = c.net[0];
     const NetParams& n1 = c.net[1];
@@ -606,10 +598,7 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     const bool ln = E.p.desc.layer_norm != 0;
     const float* P = E.params;
     ensure_side(E.p);
-    const bool wstreams = [] {   // A/B knob: weight gradients on the chain streams (read per call: tests switch it)
-        const char* e = std::getenv("CNF_TRAIN_WSTREAM");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool wstreams = (opts().train_sched & 1) == 0;   // TRAIN_SCHED bit 1: weight gradients on the chain streams
     TExec E0 = E;
     E0.wst = wstreams ? E.p.wside[0] : nullptr;
     TExec E1 = E;
@@ -696,11 +685,8 @@ void coupling_backward(TExec& E, const Coupling& c, const float* u, const float*
     // the branches + LN2, conv_a + LN1; conv_in): the GPU starts a stream's kernels in about the order
     // the host submitted them across streams (measured: no kernel ran more than ~15 submissions ahead of
     // the newest finished one), so a chain enqueued whole after the other only overlapped it at the end.
-    // CNF_TRAIN_INTERLEAVE=0 enqueues net A's chain, then net b's (A/B).
-    const bool interleave = [] {
-        const char* e = std::getenv("CNF_TRAIN_INTERLEAVE");
-        return !(e && std::atoi(e) == 0);
-    }();
+    // Debug option TRAIN_SCHED bit 4 enqueues net A's chain, then net b's.
+    const bool interleave = (opts().train_sched & 4) == 0;
     hipEvent_t ev_gc[2] = {nullptr, nullptr}, ev_ca[2] = {nullptr, nullptr}, ev_cb[2] = {nullptr, nullptr};
     // phase k of net n: 0 conv_out + LN_out; 1 + 3j + {0, 1, 2} residual block r = R - 1 - j: conv_b + LN3,
     // the grouped branches + LN2, conv_a + LN1; 1 + 3R conv_in
@@ -829,10 +815,7 @@ void flow_backward(Plan& p, const float* params, const float* xy, const float* z
     // split LDS layers: their weight gradients finish behind the next layers on a side stream; a layer's
     // buffer set (parity of its LDS-layer count) is reused two LDS layers later, when the caller's stream
     // first waits for them — that is also when the layer's gradients are complete for `done`
-    const bool split = [] {   // (read per call: tests switch it)
-        const char* e = std::getenv("CNF_LDS_SPLIT");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool split = opts().lds_bwd == 2;   // (debug option LDS_BWD=1: one launch per layer)
     struct Pending {
         int ci = -1;
         hipEvent_t ev = nullptr;

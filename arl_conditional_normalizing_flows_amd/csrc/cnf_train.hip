@@ -391,10 +391,7 @@ __global__ __launch_bounds__(256) void k_tconv_band(TConvArgs a, int TH, int all
         // band: quads of KC channels (zero beyond KC / outside the image), LN on load
         const int nq = BH * BW * cq;
         const uint32_t m_cq = udiv_magic(cq);
-#ifndef CNF_TB_U
-#define CNF_TB_U 4
-#endif
-        constexpr int TBU = CNF_TB_U;   // band quads per thread and load batch
+        constexpr int TBU = 4;   // band quads per thread and load batch (8 / 16 measured slower)
         for (int e0 = threadIdx.x; e0 < nq; e0 += 256 * TBU) {
             f4 v[TBU];
             int lo[TBU];
@@ -689,18 +686,11 @@ __global__ __launch_bounds__(256, 2) void k_tconv_thin(TConvArgs a, int TR) {
     if (lnr) lnr_finish(a, sg, sgh, b);
 }
 
-static bool tconv_thin_on() {   // A/B knob: CNF_TCONV_THIN=0 sends the thin-K convolutions to the MFMA kernels
-    static const bool v = [] {
-        const char* e = std::getenv("CNF_TCONV_THIN");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
+// debug option TRAIN_ALT bit 8: no thin-K convolutions (the MFMA kernels take them)
+static bool tconv_thin_on() { return (opts().train_alt & 8) == 0; }
 
-static bool train_valu() {   // A/B knob: the register-blocked VALU kernels (read per call: tests switch it)
-    const char* e = std::getenv("CNF_TRAIN_VALU");
-    return e && std::atoi(e) != 0;
-}
+// debug option TRAIN_ALT bit 1: the register-blocked VALU kernels
+static bool train_valu() { return (opts().train_alt & 1) != 0; }
 bool train_valu_kernels() { return train_valu(); }
 
 int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
@@ -711,10 +701,7 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
         if (a.lnr_part != nullptr && a.lnr_base + (int)(g.x * g.z) > a.lnr_stride) a.lnr_part = nullptr;
         return a.lnr_part != nullptr ? (int)(g.x * g.z) : 0;
     };
-    static const bool band_off = [] {   // A/B knob: no band-staged 3x3 kernel
-        const char* e = std::getenv("CNF_TCONV_BAND");
-        return e && std::atoi(e) == 0;
-    }();
+    const bool band_off = (opts().train_alt & 4) != 0;   // debug option TRAIN_ALT bit 4: no band-staged 3x3 kernel
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (!train_valu() && tconv_thin_on() && a.taps == 9 && a.dil == 1 && a.K >= 1 && a.K <= 4 &&
         a.stats == nullptr && (a.N == 64 || a.N == 32 || a.N == 16) && a.W >= 1 && (a.out_cs & 3) == 0 &&
@@ -751,19 +738,13 @@ int launch_tconv(const TConvArgs& a_in, hipStream_t st) {
             // (measured at cfg2 B=64, train step, same box: minimum 1024 workgroups 12.17 ms, 512 12.10,
             // 256 11.79 -- the 32x32 branch dgrads then run SUB=4, 256 workgroups of 8 rows, a quarter of
             // the per-workgroup weight staging and halo rows)
-            static const long long minwg = [] {   // A/B knob
-                const char* e = std::getenv("CNF_TBAND_MINWG");
-                return e ? std::atoll(e) : 256LL;
-            }();
+            constexpr long long minwg = 256;
             if (64 * s <= a.H * a.W && wgs >= minwg && band + w1 <= 160 * 1024) sub = s;
         }
         const int TH = std::max(1, std::min(a.H, 64 * sub / a.W));
         const size_t band = (size_t)(TH + 2 * a.dil) * (a.W + 2 * a.dil) * TB_KS * 4;
-        static const long long at_kb = [] {   // A/B knob: LDS budget (KiB) for staging every tap's weights at once
-            const char* e = std::getenv("CNF_TBAND_ALLTAPS_KB");
-            return e ? std::atoll(e) : -1LL;
-        }();
-        const long long at_lim = at_kb >= 0 ? at_kb : (sub > 1 ? 156 : 80);
+        // LDS budget (KiB) for staging every tap's weights at once
+        const long long at_lim = sub > 1 ? 156 : 80;
         const int all_taps = (long long)(band + 9 * w1) <= at_lim * 1024 ? 1 : 0;
         const size_t lds = band + (all_taps ? 9 : 1) * w1;
         if (lds <= 160 * 1024) {
@@ -919,13 +900,10 @@ __host__ __device__ constexpr int wg_stride(int c) {   // LDS row stride == 16 (
 
 // (at least 3 waves per SIMD: the launch fits 2-3 workgroups per CU by LDS, and without the bound the
 // 8-deep staging loads took 266 registers, one wave per SIMD)
-#ifndef CNF_WG_U
-#define CNF_WG_U 4
-#endif
-constexpr int WG_U = CNF_WG_U;   // staging loads in flight per thread and array
+constexpr int WG_U = 4;   // staging loads in flight per thread and array
 template <int TR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_wgrad_band(WGradArgs a, int RB,
-                                                                                          int nunits, int abl) {
+                                                                                          int nunits) {
     extern __shared__ __attribute__((aligned(16))) float wsm[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i16 = lane & 15, kq = lane >> 4;
     const int H = a.H, W = a.W, npx = H * W;
@@ -968,8 +946,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         // (float4 loads, 8 quads in flight per thread) when the windows are quad aligned.
         const float* xb = a.x + (size_t)b * npx * a.x_cs + a.x_off + ci0;
         const float* db = a.dy + (size_t)b * npx * a.dy_cs + a.dy_off + co0;
-        if (abl & 1) {
-        } else if (qx) {
+        if (qx) {
             const int cq = CIB >> 2, nxq = RB * WB * cq;
             for (int e0 = t; e0 < nxq; e0 += 256 * WG_U) {
                 f4 v[WG_U];
@@ -1034,8 +1011,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     if (e0 + 256 * u < nx) Xs[lo[u]] = v[u];
             }
         }
-        if (abl & 1) {
-        } else if (qd) {
+        if (qd) {
             const int cq = COB >> 2, ndq = RB * W * cq;
             for (int e0 = t; e0 < ndq; e0 += 256 * WG_U) {
                 f4 v[WG_U];
@@ -1079,7 +1055,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         // K = the unit's pixels, 4 per k-step: lane (i16, kq) reads pixel p = s + kq of the unit, row
         // pr = p / W from a float reciprocal (the 1x1 band has no halo: its pixel is p); past the unit's
         // last pixel dY is zero (padded rows) and X pixel 0 (finite)
-        if (kact && !(abl & 2)) {   // column blocks past the outputs have nothing to compute
+        if (kact) {   // column blocks past the outputs have nothing to compute
             const int nk = RB * W, nk4 = (nk + 3) & ~3;
             const float invW = 1.f / (float)W;
             const float* xl = Xs + 16 * cw + i16;
@@ -1464,10 +1440,7 @@ static void wgrad_thin_shape(int B, int H, int W, int& TR, int& ipw, int& ntile)
 }
 
 bool wgrad_thin_ok(int H, int W, int taps, int dil, int CI, int CO) {
-    static const bool on = [] {   // A/B knob: CNF_WGRAD_THIN=0 sends them to k_wgrad_direct / k_wgrad_band
-        const char* e = std::getenv("CNF_WGRAD_THIN");
-        return !(e && std::atoi(e) == 0);
-    }();
+    const bool on = (opts().train_alt & 8) == 0;   // debug option TRAIN_ALT bit 8: k_wgrad_direct / k_wgrad_band take them
     if (!on || taps != 9 || dil != 1 || CO < 1 || CO > 4 || CI < 4 || CI > 64 || (CI & 3) != 0 || W < 1 || W > 128)
         return false;
     int TR, ipw, ntile;
@@ -1532,14 +1505,6 @@ size_t wgrad_band_lds(int H, int W, int taps, int dil, int CI, int CO) {
     return stage > red ? stage : red;
 }
 
-static int wg_abl() {   // diagnostics: CNF_WG_ABL bit 0 skips the X/dY staging, bit 1 the MFMA loop
-    static const int v = [] {
-        const char* e = std::getenv("CNF_WG_ABL");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
 bool wgrad_band_ok(int H, int W, int taps, int dil, int CI, int CO) {
     return (taps == 1 || taps == 9) && W >= 4 && wgrad_band_lds(H, W, taps, dil, CI, CO) <= 160 * 1024;
 }
@@ -1562,9 +1527,9 @@ void launch_wgrad(const WGradArgs& a, hipStream_t st) {
     if (lds > 160 * 1024) throw std::invalid_argument("k_wgrad_band: band exceeds the LDS budget");
     const dim3 g(a.chunks, a.taps == 9 ? 3 : 1, ((a.CI + 63) / 64) * ((a.CO + 63) / 64)), blk(256);
     if (a.taps == 9)
-        hipLaunchKernelGGL(k_wgrad_band<3>, g, blk, lds, st, a, RB, nunits, wg_abl());
+        hipLaunchKernelGGL(k_wgrad_band<3>, g, blk, lds, st, a, RB, nunits);
     else
-        hipLaunchKernelGGL(k_wgrad_band<1>, g, blk, lds, st, a, RB, nunits, wg_abl());
+        hipLaunchKernelGGL(k_wgrad_band<1>, g, blk, lds, st, a, RB, nunits);
 }
 
 // 32 elements per workgroup (one 128-byte line of a partial row per half-wave), 32 slices of the

@@ -270,7 +270,10 @@ class Mean:
         self.count += 1
 
     def result(self):
-        return self.total / self.count if self.count else 0.0
+        """Always a 0-d float64 tensor (on the device the values came from; a CPU zero before any update)."""
+        if not self.count:
+            return torch.zeros((), dtype=torch.float64)
+        return torch.as_tensor(self.total / self.count, dtype=torch.float64)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -282,11 +285,13 @@ class cFlow:
 
     Extra keyword arguments (not in the reference): `group_mode` ('reference' reproduces the
     late-bound Lambda closure of conv_cINN_base_functions.py:402, 'intended' the textbook
-    grouped convolution), `device`, `seed` (parameter init)."""
+    grouped convolution), `device`, `seed` (parameter init), `debug_options` (a dict or a
+    "NAME=V,..." string selecting the alternative code paths the parity tests compare against:
+    include/cnf.h cnf_flow_desc.debug_options; None = the defaults, which are what is benchmarked)."""
 
     def __init__(self, io_shape, x_d, squeeze_factor_block_list, ResNeXt_block_list, num_kernels_list,
                  cardinality_list, lambda_y=100, ksize=3, LAYER_NORM=True, DILATIONS=True, init=None,
-                 group_mode='reference', device=None, seed=0):
+                 group_mode='reference', device=None, seed=0, debug_options=None):
         lib = _lib.load()
         self.io_shape = [int(v) for v in io_shape]
         self.x_d = int(x_d)
@@ -314,6 +319,11 @@ class cFlow:
                                   self._keep[0], self._keep[1], self._keep[2], self._keep[3],
                                   self.lambda_y, self.ksize, int(self.LAYER_NORM), int(self.DILATIONS),
                                   GROUP_MODES[group_mode])
+        if isinstance(debug_options, dict):
+            debug_options = ','.join(f'{k}={int(v)}' for k, v in debug_options.items())
+        self.debug_options = debug_options or ''
+        self._opts_buf = C.create_string_buffer(self.debug_options.encode())
+        desc.debug_options = C.cast(self._opts_buf, C.c_char_p)
         plan = C.c_void_p()
         check(lib.cnf_plan_create(C.byref(desc), C.byref(plan)), 'cFlow')
         self._plan = plan
@@ -582,7 +592,7 @@ class cFlow:
             self._cranges = r
         return r
 
-    def gradients(self, xy, process_group=None):
+    def gradients(self, xy, process_group=None, overlap=None):
         """tape.gradient(loss, trainable_variables) of train_step (:1863-1869) as one flat
         vector in the canonical parameter order, plus the 4 loss terms (batch means, device
         scalars). With process_group (True = default group) the loss sums and the gradient are
@@ -590,8 +600,7 @@ class cFlow:
         between forward and backward with no host read of its result (the backward takes the
         global image count from the device buffer), and each coupling layer's gradient range is
         all-reduced asynchronously as soon as that layer's backward is enqueued, overlapping the
-        backward of the layers before it (the default on RCCL; CNF_GRAD_OVERLAP=0/1 forces it off/on)."""
-        import os
+        backward of the layers before it (the default on RCCL; overlap=False / True forces it off / on)."""
         from .distributed import allreduce_grads, pack_nll_sums
         xy = _as_input(xy, 'xy')
         if tuple(xy.shape[1:]) != tuple(self.io_shape):
@@ -618,8 +627,9 @@ class cFlow:
         # the per-layer asynchronous all-reduce overlaps on RCCL (stream-ordered); gloo copies every range
         # through the host with a device sync per call, which the measured 1-GPU 2-rank rehearsal ran 33x
         # slower than one all-reduce after the backward: overlap by default on 'nccl' only
-        default = '1' if dist is not None and dist.get_backend(grp) == 'nccl' else '0'
-        overlap = dist is not None and os.environ.get('CNF_GRAD_OVERLAP', default) != '0'
+        if overlap is None:
+            overlap = dist is not None and dist.get_backend(grp) == 'nccl'
+        overlap = bool(overlap) and dist is not None
         works = []
         errors = []
         reported = []
@@ -655,14 +665,14 @@ class cFlow:
         m = buf[:4] / buf[4]
         return self._grads, (m[0], m[1], m[2], m[3])
 
-    def train_step(self, xy, process_group=None):
+    def train_step(self, xy, process_group=None, overlap=None):
         """cFlow.train_step (:1850-1880): NLL gradient (GradientTape), optimizer.apply_gradients,
         Mean trackers; returns {'loss', 'z_loss', 'y_loss', 'detJ_loss'} as 0-d device tensors (TF
         returns tensors too; float() reads one). Data-parallel with process_group: the loss sums and
         the gradient are all-reduced over the global batch."""
         if getattr(self, 'optimizer', None) is None:
             self.compile()
-        grads, terms = self.gradients(xy, process_group)
+        grads, terms = self.gradients(xy, process_group, overlap)
         self.optimizer.apply_flat(self.params, grads)
         check(_lib.load().cnf_pack_params(self._plan, ptr(self.params), ptr(self._aux), _stream()), 'pack params')
         for t, v in zip(self.metrics, terms):   # device scalars: no host sync (the trackers stay on the device)

@@ -58,6 +58,10 @@ def load_weights(model, path):
 
 
 class Callback:
+    """keras.callbacks.Callback subset. on_train_batch_end receives train_step's logs: 0-d float64
+    DEVICE tensors (the running loss means, as TF's train_step returns tensors), so that the step
+    needs no host read; float(v) there costs a device sync per batch. on_epoch_end receives host
+    floats (the epoch's one read)."""
     # callbacks that write files run on rank 0 only in a data-parallel fit
     writes_files = False
 
@@ -253,7 +257,8 @@ def _agreed_batches(model, data, process_group, what):
 def fit(model, x, epochs=1, initial_epoch=0, validation_data=None, callbacks: Optional[List[Callback]] = None,
         verbose=0, process_group=None):
     """keras Model.fit over train_step / test_step. Logs per epoch: loss, z_loss, y_loss, detJ_loss
-    (+ val_ prefixed on validation_data); returns a History.
+    (+ val_ prefixed on validation_data), host floats; per batch (on_train_batch_end) the same keys
+    as 0-d device tensors (Callback). Returns a History.
 
     Data-parallel (process_group given, True = the default group): every rank passes its own
     shard of the batches; train_step and test_step all-reduce over the global batch, so the

@@ -418,7 +418,8 @@ def serving_inflight(flow, lib, xy, B, nl, steps, dev, noise=None, logit=0.0):
                 L['g'].replay()
     torch.cuda.synchronize()
     lat = float(np.median([a.elapsed_time(b) for a, b in evs]))
-    ok = all(torch.equal(L['sums'], lanes[0]['sums']) for L in lanes[1:]) if noise is None else True
+    # (with --noise every lane draws its own noise: no comparison runs, and the field says so)
+    ok = all(torch.equal(L['sums'], lanes[0]['sums']) for L in lanes[1:]) if noise is None else None
     return {'batches_in_flight': nl, 'value': round(B * steps / el, 2), 'unit': 'images/s', 'steps': steps,
             'ms_per_step': round(el / steps * 1e3, 4), 'batch_latency_ms_median': round(lat, 4),
             'lanes_bitwise_equal': ok,

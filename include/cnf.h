@@ -61,6 +61,12 @@ typedef struct cnf_flow_desc {
     int layer_norm;                       /* LAYER_NORM, default 1 */
     int dilations;                        /* DILATIONS, default 1 */
     int group_mode;                       /* CNF_GROUP_* (default REFERENCE) */
+    /* Debug options, NULL or "" for the defaults (what is benchmarked): "NAME=V[,NAME=V...]" selecting
+     * the alternative code paths the parity tests compare against — NETLDS, GC, PW, GENERIC, LAYOUT,
+     * FUSE_COUPLING, LDS_BWD, TRAIN_ALT, TRAIN_SCHED (meanings: csrc/cnf_kernels.h Options). Parsed at
+     * cnf_plan_create (unknown name: CNF_E_INVALID); the string is not kept. The library reads no
+     * environment variable. No reference counterpart (the Keras model has no such switches). */
+    const char* debug_options;
 } cnf_flow_desc;
 
 /* One entry of cFlow.layers_list (conv_cINN_make_model.py:1630-1689). */
@@ -162,8 +168,10 @@ int cnf_channel_copy(const float* in, int in_cs, int in_off, float* out, int out
  * loss_i = -(llz_i + lly_i + logdet_i). Dividing sums by the (global) batch
  * gives the reference's (loss, z_loss, y_loss, detJ_loss). One kernel launch;
  * its last workgroup is found through a completion counter the plan keeps per
- * stream (up to 64 streams per plan), so calls on different streams may run
- * concurrently. The first call on a plan uploads its tables (not capturable:
+ * stream, so calls on different streams may run concurrently. 64 counters per
+ * plan: a 65th stream reuses the least recently used one, its launch ordered
+ * after that counter's last launch (a stream wait, no host wait; inside graph
+ * capture that slot needs one earlier uncaptured call). The first call on a plan uploads its tables (not capturable:
  * cnf_pack_params does the same, call it before graph capture). */
 int cnf_nll(const cnf_plan* plan, const float* xy, const float* zy, const float* logdet_per_image,
             float* per_image, float* sums, int B, void* stream);

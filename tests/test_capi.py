@@ -28,11 +28,12 @@ def test_all_header_symbols_exported(lib):
     assert sorted(_lib.EXPORTED_SYMBOLS) == syms
 
 
-def _plan(lib, kw, group_mode=0):
+def _plan(lib, kw, group_mode=0, options=None):
     arr = lambda v: (C.c_int * len(v))(*v)
     keep = [arr(kw['squeeze_factor_block_list']), arr(kw['ResNeXt_block_list']), arr(kw['num_kernels_list']),
             arr(kw['cardinality_list'])]
-    d = _lib.cnf_flow_desc(*kw['io_shape'], kw['x_d'], len(keep[0]), *keep, 100.0, 3, 1, 1, group_mode)
+    d = _lib.cnf_flow_desc(*kw['io_shape'], kw['x_d'], len(keep[0]), *keep, 100.0, 3, 1, 1, group_mode,
+                           options.encode() if options else None)
     p = C.c_void_p()
     rc = lib.cnf_plan_create(C.byref(d), C.byref(p))
     return rc, p, keep
@@ -198,13 +199,12 @@ def test_version(lib):
 
 def test_fused_net_plan(lib):
     """k_net_lds covers every cfg2 coupling layer whose s,t net fits one CU's 160 KiB LDS image
-    (all but the four 32x32 channel-mask layers); CNF_NETLDS=0 forces the streamed path."""
-    import os
+    (all but the four 32x32 channel-mask layers); the debug option NETLDS=0 forces the streamed path."""
     kw = PRESETS['cfg2'].kwargs()
     kw.pop('group_mode')
 
-    def fused():
-        rc, p, keep = _plan(lib, kw)
+    def fused(options=None):
+        rc, p, keep = _plan(lib, kw, options=options)
         assert rc == 0
         out = []
         for i in range(lib.cnf_plan_num_layers(p)):
@@ -218,11 +218,48 @@ def test_fused_net_plan(lib):
     f = fused()
     assert len(f) == 16
     assert [x[2] for x in f] == [0 if (hw == 1024 and nk == 64) else 1 for hw, nk, _ in f]
-    os.environ['CNF_NETLDS'] = '0'
-    try:
-        assert all(x[2] == 0 for x in fused())
-    finally:
-        os.environ.pop('CNF_NETLDS')
+    assert all(x[2] == 0 for x in fused('NETLDS=0'))
+
+
+# every environment variable an earlier build of the library read (rounds 1-5): the library reads none now
+OLD_KNOBS = ['CNF_CO_TAPMAX', 'CNF_FUSE_COUPLING', 'CNF_GC', 'CNF_GC_CONC', 'CNF_GC_GENERIC', 'CNF_GC_IPW',
+             'CNF_GC_POLY', 'CNF_GC_POLY_NW', 'CNF_GC_TAPGROUP', 'CNF_GC_TAP_DMIN', 'CNF_GC_TH', 'CNF_LDSBWD_STAMPS',
+             'CNF_LDS_BWD', 'CNF_LDS_SPLIT', 'CNF_LN2_MASK', 'CNF_LNR_FUSE', 'CNF_LN_MERGE', 'CNF_NETLDS',
+             'CNF_NETLDS_DUMP', 'CNF_NETLDS_GENERIC', 'CNF_NETLDS_MAXHW', 'CNF_NETLDS_VERBOSE', 'CNF_NETLDS_WIDE',
+             'CNF_OUT_LAW', 'CNF_OUT_LAW_KS', 'CNF_PW', 'CNF_PW_ALIGNED', 'CNF_PW_GENERIC', 'CNF_PW_IPW',
+             'CNF_PW_IPW_RES', 'CNF_PW_SH', 'CNF_STAMPS', 'CNF_T1_COMPACT', 'CNF_T2_MAP', 'CNF_TAP_PW',
+             'CNF_TBAND_ALLTAPS_KB', 'CNF_TBAND_MINWG', 'CNF_TCONV_BAND', 'CNF_TCONV_THIN', 'CNF_TRAIN_EVFLAGS',
+             'CNF_TRAIN_INTERLEAVE', 'CNF_TRAIN_SAVE', 'CNF_TRAIN_VALU', 'CNF_TRAIN_WSTREAM', 'CNF_WGRAD_DIRECT',
+             'CNF_WGRAD_THIN', 'CNF_WG_ABL']
+
+
+def test_library_reads_no_environment():
+    """Configuration is the plan descriptor's (debug_options), never the process environment: the
+    library's sources name no getenv outside the -DCNF_DIAG diagnostic builds (the GPU test
+    test_gpu_parity.py::test_old_knobs_change_nothing runs a forward with every old variable set)."""
+    root = Path(__file__).resolve().parent.parent / 'arl_conditional_normalizing_flows_amd' / 'csrc'
+    for f in sorted(root.glob('*.[ch]*')):
+        depth = 0   # inside '#ifdef CNF_DIAG'
+        for ln, line in enumerate(f.read_text().splitlines(), 1):
+            t = line.strip()
+            if t.startswith('#if'):
+                depth = depth + 1 if (depth or 'CNF_DIAG' in t) else 0
+            elif t.startswith('#endif') and depth:
+                depth -= 1
+            elif 'getenv' in t and not t.startswith('//'):
+                assert depth > 0, f'{f.name}:{ln}: getenv outside a CNF_DIAG build: {t}'
+
+
+def test_debug_options_are_validated(lib):
+    kw = PRESETS['small'].kwargs()
+    kw.pop('group_mode')
+    for bad in ('NOPE=1', 'NETLDS', 'NETLDS=x', 'LDS_BWD=3'):
+        rc, p, keep = _plan(lib, kw, options=bad)
+        assert rc == -1 and not p.value, bad
+        assert b'debug_options' in lib.cnf_last_error()
+    rc, p, keep = _plan(lib, kw, options='NETLDS=0,GC=0,LAYOUT=3')
+    assert rc == 0
+    lib.cnf_plan_destroy(p)
 
 
 def test_netlds_shape_table_is_current(lib):

@@ -20,32 +20,23 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 
-# plan-time knobs of the streamed path's fallback kernels: 'nogc' = no fused k_gc stage (CNF_GC=0: the
-# grouped branches run as k_pw tap-mode launches over their im2col rows); 'conv1' = no k_pw (CNF_PW=0:
-# the per-tile k_conv1 / k_conv<3> kernels, and conv_out as the one-kernel k_convtap, CNF_TAP_PW=0)
-# 'outlaw' = the streamed conv_out and coupling law as one k_out_law launch (CNF_OUT_LAW=1, opt-in: measured
-# slower than the tap GEMM + k_coupling pair, kept parity-tested)
-KNOBS = {'nogc': {'CNF_NETLDS': '0', 'CNF_GC': '0'},
-         'conv1': {'CNF_NETLDS': '0', 'CNF_PW': '0', 'CNF_TAP_PW': '0'},
-         'outlaw': {'CNF_OUT_LAW': '1'}, 'outlaw128': {'CNF_OUT_LAW': '1', 'CNF_OUT_LAW_KS': '1'},
-         # the grouped stage's launches forked over three streams (CNF_GC_CONC=1, opt-in, measured slower)
-         'gcconc': {'CNF_GC_CONC': '1'}}
+# debug options of the streamed path's fallback kernels (cFlow(debug_options=...), include/cnf.h):
+# 'nogc' = no fused k_gc stage (GC=0: the grouped branches run as k_pw tap-mode launches over their
+# im2col rows); 'conv1' = no k_pw (PW=0: the per-tile k_conv1 / k_conv<3> kernels, and conv_out as the
+# one-kernel k_convtap)
+KNOBS = {'nogc': {'NETLDS': 0, 'GC': 0}, 'conv1': {'NETLDS': 0, 'PW': 0}}
 
 
-def _setup(name, B, group_mode='reference', seed=0, netlds=True):
-    """netlds: True / False (CNF_NETLDS), or a KNOBS key (streamed layers with fallback kernels)"""
-    import os
+def _setup(name, B, group_mode='reference', seed=0, netlds=True, options=None):
+    """netlds: True / False (debug option NETLDS), or a KNOBS key (streamed layers with fallback kernels);
+    options: further debug options"""
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
-    env = KNOBS.get(netlds, {'CNF_NETLDS': '0' if netlds is False else '1'})
-    os.environ.update(env)
+    opt = dict(KNOBS.get(netlds, {'NETLDS': 0 if netlds is False else 1}))
+    opt.update(options or {})
     cfg = PRESETS[name]
     kw = cfg.kwargs()
     kw['group_mode'] = group_mode
-    try:
-        flow = cFlow(**kw)
-    finally:
-        for k in env:
-            os.environ.pop(k, None)
+    flow = cFlow(**kw, debug_options=opt)
     ora = OracleCFlow(**kw)
     P = ora.init_params(seed)
     flow.set_weights(P)
@@ -102,11 +93,7 @@ CASES = [('tiny', 2, 'reference', True), ('small', 3, 'reference', True), ('smal
          # BASELINE configs[3] / configs[4] architectures (64x64 4-scale, 128x128 5-scale) at a small batch
          ('cfg4', 2, 'reference', True), ('cfg5', 1, 'reference', True),
          # couplings 2 and 1 pixels wide (squeezed to 2x2 blocks)
-         ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False),
-         # the opt-in one-launch conv_out + law of the streamed tap-format layers (dc2 = 2 / 3 / 1)
-         ('cfg2', 2, 'reference', 'outlaw'), ('cfg3', 2, 'reference', 'outlaw'),
-         ('ref_default', 2, 'reference', 'outlaw'), ('cfg2', 2, 'reference', 'outlaw128'),
-         ('cfg4', 2, 'reference', 'gcconc'), ('cfg5', 1, 'reference', 'gcconc')]
+         ('narrow', 3, 'reference', True), ('narrow', 3, 'reference', False)]
 
 
 @pytest.mark.parametrize('name,B,gm,netlds', CASES)
@@ -188,35 +175,56 @@ def test_layerwise_equals_fused(gpu, name, B):
     assert torch.equal(xi1, xi2)
 
 
+def test_old_knobs_change_nothing(gpu):
+    """Every environment variable an earlier build read (tests/test_capi.py OLD_KNOBS), set to a
+    non-default value around plan creation and the calls, leaves the cfg2 forward and inverse bitwise
+    unchanged: configuration is the plan descriptor's, not the process environment's."""
+    import os
+    from test_capi import OLD_KNOBS
+    flow, ora, P, xy = _setup('cfg2', 4)
+    x = torch.from_numpy(xy).to(gpu)
+    zy0, ld0 = flow(x, 1, per_image_logdet=True)
+    xi0 = flow(zy0, -1)
+    vals = {k: '0' for k in OLD_KNOBS}
+    vals.update({k: '1' for k in ('CNF_GC_CONC', 'CNF_GC_GENERIC', 'CNF_NETLDS_GENERIC', 'CNF_NETLDS_WIDE',
+                                  'CNF_OUT_LAW', 'CNF_PW_GENERIC', 'CNF_PW_SH', 'CNF_PW_ALIGNED', 'CNF_TRAIN_VALU',
+                                  'CNF_STAMPS', 'CNF_NETLDS_DUMP', 'CNF_NETLDS_VERBOSE', 'CNF_LDSBWD_STAMPS')})
+    vals.update({'CNF_PW_IPW': '2', 'CNF_PW_IPW_RES': '8', 'CNF_GC_IPW': '3', 'CNF_GC_TH': '4', 'CNF_CO_TAPMAX': '9',
+                 'CNF_NETLDS_MAXHW': '16', 'CNF_LN_MERGE': '1'})
+    old = {k: os.environ.get(k) for k in vals}
+    os.environ.update(vals)
+    try:
+        f2, _, _, _ = _setup('cfg2', 4)
+        zy, ld = f2(x, 1, per_image_logdet=True)
+        xi = f2(zy0, -1)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert torch.equal(zy, zy0) and torch.equal(ld, ld0) and torch.equal(xi, xi0)
+
+
 @pytest.mark.parametrize('name,B', [('cfg2', 3), ('cfg4', 2), ('cfg5', 1)])
 def test_t1_layout_and_polyphase_tiles_are_neutral(gpu, name, B):
-    """The streamed layers' t1 / t2 sub-tensor layouts (CNF_T1_COMPACT, CNF_T2_MAP) change where values live, never
+    """The streamed layers' t1 / t2 sub-tensor layouts (debug option LAYOUT bits 1, 2) change where values live, never
     the arithmetic: with the generic k_gc / k_pw in both runs (the plain layout has no specialised
     instantiation, and those partition the LN statistics over their own wave counts) zy, the per-image
-    log-det and the inverse are equal bit for bit. The polyphase tiles of large dilations (CNF_GC_POLY,
+    log-det and the inverse are equal bit for bit. The polyphase tiles of large dilations (LAYOUT bit 4,
     cfg4/cfg5) compute every conv output in the same order but gather the LN3 statistics over other
     pixel sets: equal to rounding."""
-    import os
-    flow, ora, P, xy = _setup(name, B)
+    flow, ora, P, xy = _setup(name, B, options={'GENERIC': 1})
     x = torch.from_numpy(xy).to(gpu)
-    for knob in ('CNF_T1_COMPACT', 'CNF_T2_MAP', 'CNF_GC_POLY'):
-        os.environ[knob] = '0'
-        try:
-            f2, _, _, _ = _setup(name, B)
-        finally:
-            os.environ.pop(knob, None)
-        os.environ['CNF_GC_GENERIC'] = '1'
-        os.environ['CNF_PW_GENERIC'] = '1'
-        try:
-            zy0, ld0 = flow(x, 1, per_image_logdet=True)
-            xi0 = flow(zy0, -1)
-            zy, ld = f2(x, 1, per_image_logdet=True)
-            xi = f2(zy0, -1)
-            torch.cuda.synchronize()
-        finally:
-            os.environ.pop('CNF_GC_GENERIC', None)
-            os.environ.pop('CNF_PW_GENERIC', None)
-        if knob != 'CNF_GC_POLY':
+    zy0, ld0 = flow(x, 1, per_image_logdet=True)
+    xi0 = flow(zy0, -1)
+    for knob in (1, 2, 4):
+        f2, _, _, _ = _setup(name, B, options={'GENERIC': 1, 'LAYOUT': 7 & ~knob})
+        zy, ld = f2(x, 1, per_image_logdet=True)
+        xi = f2(zy0, -1)
+        torch.cuda.synchronize()
+        if knob != 4:
             assert torch.equal(zy, zy0) and torch.equal(ld, ld0) and torch.equal(xi, xi0), knob
         else:
             # two fp32 summation orders of every LN3 statistic: a few ulp per layer, well inside the
@@ -287,6 +295,26 @@ def test_nll_matches_oracle(gpu):
     # conditioning: the log-det terms' sum|s| (the NLL terms themselves are sums of one sign)
     for r, g in zip(ref, got):
         assert abs(r - g) <= RTOL * max(abs(r), abs_s.mean())
+
+
+def test_nll_on_more_streams_than_counter_slots(gpu):
+    """cnf_nll keeps 64 completion counters per plan: streams 65.. reuse the least recently used slot
+    behind a wait on its last launch. 70 streams, each with a launch in flight, all give the sums of
+    the default stream bit for bit."""
+    flow, ora, P, xy = _setup('small', 3)
+    x = torch.from_numpy(xy).to(gpu)
+    zy, ld = flow(x, 1, per_image_logdet=True)
+    ref, _ = flow.nll_sums(x, zy, ld)
+    streams = [torch.cuda.Stream() for _ in range(70)]
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(2):
+        for st in streams:
+            with torch.cuda.stream(st):
+                outs.append(flow.nll_sums(x, zy, ld)[0])
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
 
 
 def test_deterministic(gpu):
