@@ -313,6 +313,68 @@ __device__ __forceinline__ void copy_to_lds(const float* __restrict__ src, float
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32 contractions on the bf16 matrix cores (bf16x6). Every fp32 operand x is split exactly into
+// three bf16 terms, x = h + m + l: h = bf16(x), m = bf16(x - h), l = x - h - m (both differences are
+// exact in fp32: they are the low bits of x; l has at most 8 significant bits, so it is a bf16). With
+// |m| <= 2^-8 |x| and |l| <= 2^-16 |x|, a product x w is h H + h M + m H + h L + l H + m M (six bf16
+// MFMA products, each exact in fp32) up to the dropped m L + l M + l L: at most 2^-23 |x w| (one fp32
+// ulp), 2^-26 on average, the size of the rounding of one fp32 product. The sums accumulate in fp32 in
+// the MFMA. One 16x16x32 bf16 MFMA takes
+// 16 cycles against 32 for the 16x16x4 fp32 one: six of them per 32-deep K step are 0.375x the fp32
+// MFMA time of the same contraction.
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+struct Split8 {
+    bf16x8 h, m, l;
+};
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+// the lane's 8 consecutive K elements (a: k 0..3, b: k 4..7) as the three bf16 fragments
+__device__ __forceinline__ Split8 split8(const f4& a, const f4& b) {
+    Split8 s;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        __bf16 h, m, l;
+        split3(a[j], h, m, l);
+        s.h[j] = h;
+        s.m[j] = m;
+        s.l[j] = l;
+        split3(b[j], h, m, l);
+        s.h[4 + j] = h;
+        s.m[4 + j] = m;
+        s.l[4 + j] = l;
+    }
+    return s;
+}
+__device__ __forceinline__ void split4(const f4& a, bf16x4& h, bf16x4& m, bf16x4& l) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        __bf16 x, y, z;
+        split3(a[j], x, y, z);
+        h[j] = x;
+        m[j] = y;
+        l[j] = z;
+    }
+}
+// acc += A . B over one 32-deep K step (16x16x32, A rows / B columns per the lane maps of the bf16
+// MFMA), A = a.h + a.m + a.l, B = bh + bm + bl; the small products first
+__device__ __forceinline__ f4 mfma_x6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                      const bf16x8& bm, const bf16x8& bl, f4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+    return acc;
+}
 
 // masks (conv_cINN_make_model.py:720-759, 896-1071)
 // position in u (per-image element index) of element (compressed pixel p, channel c) of the

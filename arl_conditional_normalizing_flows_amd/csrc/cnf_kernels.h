@@ -7,6 +7,7 @@
 #include <hip/hip_ext.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace cnf {
 
@@ -29,7 +30,7 @@ struct Options {
     int netlds = 1;          // NETLDS: 0 = no LDS-resident (k_net_lds) layers, every layer streamed
     int gc = 1;              // GC: 0 = no fused k_gc stage (grouped branches as k_pw tap mode / k_conv<3>)
     int pw = 1;              // PW: 0 = the per-tile k_conv1 / k_conv<3> kernels and the one-kernel k_convtap conv_out
-    int generic = 0;         // GENERIC: 1 = never the shape-specialised instantiations (k_pw, k_gc, k_net_lds)
+    int generic = 0;         // GENERIC bits: never the shape-specialised instantiations of 1 any kernel, 2 k_pw, 4 k_gc, 8 k_net_lds
     int layout = 7;          // LAYOUT bits: 1 compact t1 sub-tensors, 2 mapped t2 sub-tensors, 4 polyphase k_gc tiles
     int fuse_coupling = 1;   // FUSE_COUPLING: 0 = every coupling layer launches its own k_coupling
     int lds_bwd = 2;         // LDS_BWD: 0 multi-kernel backward of the k_net_lds layers, 1 fused (one launch), 2 fused split
@@ -70,7 +71,17 @@ LaunchTiming& launch_timing();   // per host thread (cnf_runtime.cpp)
         } else {                                                                                    \
             hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                         \
         }                                                                                           \
+        CNF_DIAG_SYNC(S);                                                                           \
     } while (0)
+#ifdef CNF_DIAG   // diagnostic builds: CNF_SYNC_ALL=1 synchronises the stream after every launch
+#define CNF_DIAG_SYNC(S)                                                                            \
+    do {                                                                                            \
+        static const bool sync_ = std::getenv("CNF_SYNC_ALL") != nullptr;                          \
+        if (sync_) (void)hipStreamSynchronize(S);                                                   \
+    } while (0)
+#else
+#define CNF_DIAG_SYNC(S) do { } while (0)
+#endif
 
 // packed weight-image formats (see cnf_plan.h PackedConv)
 enum { PK_1X1 = 0, PK_KN = 1, PK_TAP = 2, PK_Q4 = 3 };
@@ -117,6 +128,7 @@ struct ConvArgs {
     // umask < 0: the source is a plain NHWC tensor of the conv's own H x W (uD channels per pixel,
     // taps from channel uoff, dilation udil; LN / LeakyReLU on load as the problem says)
     int udil, uoff;
+    int diag;   // -DCNF_DIAG builds only: k_pw experiment bits (CNF_PW_DIAG)
 };
 
 struct CoupArgs {
@@ -262,11 +274,17 @@ inline void netshape_words(const NetLdsArgs& a, int* w) {
 // bands with their own dilation halo (LN2 + LeakyReLU applied on the way in, zero padding), so
 // the 3x3 taps need no bounds checks; weights are PK_Q4 over cin padded to a multiple of 4.
 constexpr int GC_MAXBR = 8;
-// waves per k_gc workgroup (one LN partial slot per wave): the shape-specialised instantiations
-// run 16 (one 16-pixel subtile per wave and pass, 4 waves per SIMD within their 128 VGPRs), the
-// generic one 8 (two subtiles per wave sharing every B read; it needs the registers)
+// waves per k_gc workgroup (one LN partial slot per wave): the shape-specialised instantiations run
+// 16 (one 16-pixel subtile per wave and pass, 4 waves per SIMD within 128 VGPRs; 8 waves with two
+// subtiles sharing every weight read measured slower with the bf16x6 contraction: 26.2 -> 29.7 us at
+// cfg2), small polyphase groups 4-wave workgroups, four per CU; the generic one 8 (two subtiles per wave)
 constexpr int GC_NW_GEN = 8, GC_NW_SPEC = 16, GC_NW_MAX = 16;
-constexpr int GC_STAGE_QUADS = 2048;   // staged band quads per workgroup
+constexpr int GC_STAGE_QUADS = 2048;   // staged band units per workgroup (2 per thread at 16 waves)
+// LDS budget and staged band units of a k_gc workgroup of nw waves (1 workgroup per CU at >= 8 waves,
+// 4 at 4)
+constexpr int gc_lds_budget(int nw) { return nw >= 8 ? 160 * 1024 : 40 * 1024; }
+constexpr int gc_stage_units(int nw) { return nw >= 8 ? 2048 : 2 * 64 * nw; }
+constexpr int gc_wg_per_cu(int nw) { return nw >= 8 ? 1 : 4; }
 struct GcBranch {
     int cin_off, cin, cinp, cout, out_off, dil;   // input window (cin_off: floats from the image start to pixel 0's window), padded channels, outputs
     int G;                                        // quad groups of the PK_Q4 image

@@ -1351,7 +1351,7 @@ void launch_net_lds(const NetLdsArgs& a, int B, int lds, hipStream_t st) {
 #else
     constexpr bool stamps = false;
 #endif
-    const bool generic = opts().generic != 0;   // never the shape-specialised instantiations
+    const bool generic = (opts().generic & 9) != 0;   // debug option GENERIC bit 1 (all) or 8 (k_net_lds)
     const bool narrow = a.maxnr <= 2;
     const bool ks = a.off_ks != 0;
     const dim3 grid(B, 2), block(NT);

@@ -426,34 +426,40 @@ Plan* build_plan(const cnf_flow_desc* d) {
                         g.out_off = b.out_off;
                         g.opcs = c.gc;
                         g.dil = dil_eff > 0 ? dil_eff : b.dil;
-                        g.G = (9 * (g.cinp / 4) + 3) / 4;
+                        // bf16x6 contraction (cnf_stream.hip k_gc): the band holds S bf16 channels per pixel
+                        // and plane (2, 4, or a multiple of 8: K = 9 S in 32-deep steps, G of them)
+                        g.S = b.cin <= 2 ? 2 : b.cin <= 4 ? 4 : (b.cin + 7) / 8 * 8;
+                        g.G = (9 * g.S + 31) / 32;
                         g.BW = TW + 2 * g.dil;
                         g.BH = nblk * (TH + 2 * g.dil);
-                        g.S = stride8(g.cinp);
-                        // exact umulhi division for x < 2^16 (x * d < 2^32)
-                        g.cpq_mag = g.cinp == 4 ? 0u : (uint32_t)((((uint64_t)1 << 32) + (g.cinp / 4) - 1) / (g.cinp / 4));
+                        // staged band units per pixel: channel quads up to S (S = 2: one pair); the quads
+                        // past the window (to S) are staged as zeros. Exact umulhi division for x < 2^16
+                        const int cpq = std::max(1, g.S / 4);
+                        g.cpq_mag = cpq == 1 ? 0u : (uint32_t)((((uint64_t)1 << 32) + cpq - 1) / cpq);
                         g.bw_mag = (uint32_t)((((uint64_t)1 << 32) + g.BW - 1) / g.BW);
-                        if ((int64_t)g.BH * g.BW * (g.cinp / 4) >= (1 << 16)) return false;
+                        if ((int64_t)g.BH * g.BW * cpq >= (1 << 16)) return false;
                         if (b.cout > 64) return false;
-                        g.w_off = (int)off;
-                        off = align16(off + (int64_t)g.G * 16 * 16 * ((b.cout + 15) / 16) * 4);
-                        g.q_off = (int)off;
-                        off = align16(off + 16LL * g.G);
-                        g.band_off = (int)off;
-                        off = align16(off + (int64_t)g.BH * g.BW * g.S * 4);
+                        g.w_off = (int)off;   // the weights' three bf16 planes: 1 KiB per (K step, plane, 16 outputs)
+                        off = align16(off + (int64_t)g.G * 3 * ((b.cout + 15) / 16) * 1024);
+                        g.q_off = (int)off;   // per K octet: up to 4 band offsets (int4)
+                        off = align16(off + 64LL * g.G);
+                        g.b_off = (int)off;   // biases (read from LDS in the epilogue: no global load there)
+                        off = align16(off + 4LL * g.cout);
                         gb.push_back(g);
                     }
-                    int64_t quads = 0;   // staged band quads: at most 128 per wave (2 per thread)
-                    for (const GcBranch& g : gb) quads += (int64_t)g.BH * g.BW * (g.cinp / 4);
-                    // two band buffers: the next image is staged while the current one is computed
-                    const int64_t band_bytes = gb.empty() ? 0 : off - gb[0].band_off;
-                    off += band_bytes;
-                    for (GcBranch& g : gb) {   // biases (read from LDS in the epilogue: no global load there)
-                        g.b_off = (int)off;
-                        off = align16(off + 4LL * g.cout);
+                    // the bands (three planes of BH x BW x S bf16 per branch), twice: the next image is
+                    // staged while the current one is computed
+                    const int64_t band0 = off;
+                    int64_t quads = 0;   // staged band units: at most 128 per wave (2 per thread)
+                    for (GcBranch& g : gb) {
+                        g.band_off = (int)off;
+                        off = align16(off + 3 * align16((int64_t)g.BH * g.BW * g.S * 2));
+                        quads += (int64_t)g.BH * g.BW * std::max(1, g.S / 4);
                     }
+                    const int64_t band_bytes = off - band0;
+                    off += band_bytes;
                     // nw < 16: 16 / nw workgroups share a CU, so its LDS
-                    if (off > 160 * 1024 / (GC_NW_SPEC / nw) || quads > 128LL * nw) return false;
+                    if (off > gc_lds_budget(nw) || quads > gc_stage_units(nw)) return false;
                     out.nw = nw;
                     out.br = sel;
                     out.gcb = gb;

@@ -412,7 +412,10 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
             const int G = (s.cin + 15) / 16;
             if (off < 512) off = 512;   // k_pw keeps its per-image LN table at bytes [256, 384)
             q.lds_w_off = (int)off;
-            off = align_up(off + (size_t)G * 16 * 16 * q.nr * 4, 16);
+            // k_pw stages the weights as the three bf16 planes of 32-deep K steps (1 KiB per plane, step and
+            // 16-column block); k_conv1 reads the fp32 image, G x 16 x 16 x nr floats, which fits in it
+            const size_t wx6 = (size_t)((s.cin + 31) / 32) * 3 * q.nr * 1024;
+            off = align_up(off + std::max(wx6, (size_t)G * 16 * 16 * q.nr * 4), 16);
             // k_pw loads every channel quad the input window starts with 16 bytes at a time: a window
             // that is not quad-aligned (conv_b over the 62- / 30-channel concat of cfg5's grouped
             // stages) reads past its last channel into the next pixel (or 0 past the image), which
@@ -430,6 +433,10 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
                         (double)K * s.cout + s.cout);
     }
     if (lds > 160 * 1024) throw std::invalid_argument("conv tile exceeds the 160 KiB LDS budget");
+    if (ks == 1)   // k_pw stages every problem's weights as pw_nr column blocks: the workgroup's LDS covers them
+        for (int i = 0; i < a.nprob; i++)
+            if ((size_t)a.p[i].lds_w_off + (size_t)((a.p[i].cin + 31) / 32) * 3 * pw_nr * 1024 > lds || a.p[i].nr != pw_nr)
+                throw std::logic_error("k_pw launch: problems of different widths or LDS short of the weight planes");
     const int ilds = (int)lds;
     if (pw_gm > 0) pw_gm = pw_gm <= 1 ? 1 : pw_gm <= 2 ? 2 : pw_gm <= 4 ? 4 : pw_gm <= 8 ? 8 : 0;
     bool ln_uniform = true;
@@ -936,8 +943,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
             // image's band staged behind the current one's MFMAs
             // (16 / nw workgroups per CU)
             const int64_t units = (int64_t)ga.s.tiles_per_img * 2 * B;
-            const int64_t slots = 256LL * (GC_NW_SPEC / gg.nw);
+            const int64_t slots = 256LL * gc_wg_per_cu(gg.nw);
             ga.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + slots - 1) / slots));
+#ifdef CNF_DIAG
+            if (const char* e = std::getenv("CNF_GC_IPW")) ga.ipw = std::atoi(e);   // diagnostics
+#endif
             ga.s.band_bytes = gg.band_bytes;
             ga.s.lnst = (ga.in_part[0] ? 1 : 0) | (ga.out_part[0] ? 2 : 0);
             const int gcw = gc_waves(ga);

@@ -11,6 +11,11 @@
 // image's activations (and residual) are loaded into registers before the current image's MFMAs,
 // so HBM traffic and compute overlap inside the wave. The tile's LN gamma/beta are loaded once and
 // serve every image; weights and the per-image LN (mean, rstd) live in LDS.
+//
+// The contraction runs on the bf16 matrix cores as the exact three-term split of cnf_device.h
+// (bf16x6, fp32-accurate): K in 32-deep steps, lane (i16, kq) of a wave holding channels
+// 32c + 8kq .. +7 of its pixel at step c; the weights are staged once per workgroup as their three
+// bf16 planes (stage_w_x6).
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -28,6 +33,10 @@ constexpr int PW_NW = 4;   // waves per k_pw workgroup (two workgroups per CU)
 #define CNF_PW_MINW 2
 #endif
 // shape fields: compile-time constants of table entry SID in the shape-specialised instantiations
+// (cin is read at run time in every instantiation: folded to a constant, the specialised builds gave
+// run-to-run different outputs at cfg2 B = 64 and cfg5 (zy 2e-2 .. 6e-2 off the oracle), while
+// builds with the same code and cin read at run time -- every other field still a constant -- were
+// exact; found by bisecting the folded fields, profiles/sessions/r6_x6x.sh)
 #define PP(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : P.f)
 #define PA(f) (SID >= 0 ? kPwShapes[SID >= 0 ? SID : 0].f : a.f)
 // diagnostic per-workgroup stamps (CNF_PW_STAMPS=SID builds only; never in timed runs): thread 0 of
@@ -57,6 +66,40 @@ int read_pw_stamps(long long* host) {
 // cfg2 B=64 (two / four images: conv_a 19.1 -> 20.8 / 21.0 us, conv_out 11.9 -> 14.1 us; issued with
 // the prologue's loads, slower still), and for the residual conv_b in round 2
 //
+// The PK_1X1 fp32 weight image (plan: [g][q][j][s], k = 16g + 4q + s, column j < 16 NR) -> the bf16x6
+// fragment planes in LDS: plane p (h, m, l) of K step c and column block nb at byte
+// ((c * 3 + p) * NR + nb) * 1024 + lane * 16, lane (kq, i16) holding W[k = 32c + 8kq + jj][16nb + i16]
+// (jj < 8); zero past the image's G groups. Four float4 loads in flight per thread.
+template <int NTH, int NR>
+__device__ __forceinline__ void stage_w_x6(const float* __restrict__ src, unsigned char* dst, int G, int C) {
+    constexpr int NSJ = 16 * NR;
+    int n = __builtin_amdgcn_readfirstlane(C * NR * 128);   // float4 slots (c, nb, lane, half)
+    asm volatile("" : "+s"(n));   // opaque count: a constant one unrolls the copy into the live image loads
+    const f4* s4 = reinterpret_cast<const f4*>(src);
+    for (int base = 0; base < n; base += NTH * 4) {
+        f4 v[4];
+        int o[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = base + u * NTH + (int)threadIdx.x;
+            const int c = t / (NR * 128), r = t - c * (NR * 128), nb = r >> 7, ln = (r >> 1) & 63, half = r & 1;
+            const int k0 = 32 * c + 8 * (ln >> 4) + 4 * half, col = 16 * nb + (ln & 15);
+            const int g = k0 >> 4, q = (k0 >> 2) & 3;
+            v[u] = t < n && g < G ? s4[(g * 4 + q) * NSJ + col] : f4{0.f, 0.f, 0.f, 0.f};
+            o[u] = t < n ? (c * 3 * NR + nb) * 1024 + ln * 16 + half * 8 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (o[u] < 0) continue;
+            bf16x4 h, m, l;
+            split4(v[u], h, m, l);
+            *reinterpret_cast<bf16x4*>(dst + o[u]) = h;
+            *reinterpret_cast<bf16x4*>(dst + o[u] + NR * 1024) = m;
+            *reinterpret_cast<bf16x4*>(dst + o[u] + 2 * NR * 1024) = l;
+        }
+    }
+}
+
 // DUAL (generic non-tap instantiations of the training forward only): every output element is also
 // stored densely ([HW][cout]) to P.out2 -- conv_a's full t1 saved for the backward in the same launch
 template <int NR, int GM, bool LN, bool RES, int SID, bool TAP = false, bool DUAL = false>
@@ -72,9 +115,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = wave;   // pixel subtile
     const int i16 = lane & 15, kq = lane >> 4;
-    const int cin = PP(cin), G = (cin + 15) >> 4, cout = PP(cout);
-    constexpr int NSJ = 16 * NR;
-    float* lw = reinterpret_cast<float*>(smem + PP(lds_w_off));
+    const int cin = P.cin, G = (cin + 15) >> 4, C = (cin + 31) >> 5, cout = PP(cout);
+    // quad slots of the lane: slot g holds channels 32 (g / 2) + 8 kq + 4 (g % 2) .. +3 (K step g / 2)
+    constexpr int CM = (GM + 1) / 2, GX = 2 * CM;
+    unsigned char* lwb = smem + PP(lds_w_off);
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
     // buffer resources: out-of-range offsets (BUF_OOB) load 0 / drop the store
     const uint32_t in_img = TAP ? (uint32_t)PA(uimg) * 4u : (uint32_t)HW * PP(in_cs) * 4u;
@@ -85,23 +129,24 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         return buf_rsrc(base + (size_t)img * (bytes >> 2), bytes);
     };
 
-    // A operand: lane (i16, kq) feeds pixel pa, channels 16g + 4kq + s at k-step s of group g. Masks
-    // are evaluated per element from shape fields (folded to constants in the specialised
-    // instantiations, whose offsets then become lane base + immediate)
+    // A operand: lane (i16, kq) feeds pixel pa, the channels of its quad slots. Masks are evaluated
+    // per element from shape fields (folded to constants in the specialised instantiations, whose
+    // offsets then become lane base + immediate)
     const bool full_px = HW % (16 * NW) == 0;
     const int pa = tile * (16 * NW) + sub * 16 + i16;
     const bool pav = full_px || pa < HW;
-    const uint32_t aoff = ((uint32_t)pa * PP(in_cs) + PP(in_off) + 4 * kq) * 4u;
-    // mapped input (conv_b over a t2 split into its producers' sub-tensors): quad 4g + kq of the
+    auto chq = [&](int g) { return 32 * (g >> 1) + 8 * kq + 4 * (g & 1); };   // first channel of slot g
+    const uint32_t aoff = ((uint32_t)pa * PP(in_cs) + PP(in_off)) * 4u;
+    // mapped input (conv_b over a t2 split into its producers' sub-tensors): quad chq(g) / 4 of the
     // lane's pixel at in_map's (offset, pixel stride)
-    uint32_t amap[GM];
+    uint32_t amap[GX];
 #pragma unroll
-    for (int g = 0; g < GM; g++)
-        amap[g] = PP(in_mapped) && 16 * g + 4 * kq < cin
-                      ? (uint32_t)(P.in_map[2 * (4 * g + kq)] + pa * P.in_map[2 * (4 * g + kq) + 1]) * 4u
+    for (int g = 0; g < GX; g++)
+        amap[g] = PP(in_mapped) && chq(g) < cin
+                      ? (uint32_t)(P.in_map[2 * (chq(g) >> 2)] + pa * P.in_map[2 * (chq(g) >> 2) + 1]) * 4u
                       : 0u;
-    auto aoffg = [&](int g) -> uint32_t { return PP(in_mapped) ? amap[g] : aoff + 64u * g; };
-    auto gok = [&](int g) { return pav && g < G && (cin % 16 == 0 || 16 * g + 4 * kq < cin); };
+    auto aoffg = [&](int g) -> uint32_t { return PP(in_mapped) ? amap[g] : aoff + 4u * chq(g); };
+    auto gok = [&](int g) { return pav && chq(g) < cin; };
     // output: acc[n][r] = out[pixel po0 + r][channel 16n + i16]
     const int po0 = tile * (16 * NW) + sub * 16 + kq * 4;
     const uint32_t obase = ((uint32_t)po0 * PP(out_cs) + PP(out_off) + i16) * 4u;
@@ -124,11 +169,11 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         return (pv(r) && chv(n) && st) ? obase + (uint32_t)(r * PP(out_cs) + 16 * n) * 4u : BUF_OOB;
     };
     // image activations (+ residual) in registers: the current image and the next
-    f4 x[GM];
+    f4 x[GX];
     float rv[NR][4];
-    // tap mode: element k = 16g + 4kq + j of the lane's im2col row -> offset inside one image of u
+    // tap mode: element k = chq(g) + j of the lane's im2col row -> offset inside one image of u
     auto toff = [&](int g, int j) -> uint32_t {
-        const int k = 16 * g + 4 * kq + j;
+        const int k = chq(g) + j;
         if (!pav || k >= cin) return BUF_OOB;
         const int tap = k / PA(udc), c = k - tap * PA(udc);
         const int d = PA(udil);
@@ -140,26 +185,26 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // plain-NHWC tap sources with quad-aligned channels: one 16-byte load per (tap, quad) (the
     // row's channel quads never straddle two taps when cin % 4 == 0)
     const bool tquad = TAP && PA(umask) < 0 && PA(udc) % 4 == 0 && PA(uoff) % 4 == 0 && PA(uD) % 4 == 0;
-    auto load_img = [&](int ii, f4 (&xd)[GM], float (&rd)[NR][4]) {
+    auto load_img = [&](int ii, f4 (&xd)[GX], float (&rd)[NR][4]) {
         const auto rin = img_rsrc(P.in, img0 + ii, in_img);
         constexpr uint32_t ib = 0;
         if constexpr (TAP) {
 #pragma unroll
-            for (int g = 0; g < GM; g++) {
+            for (int g = 0; g < GX; g++) {
                 if (tquad) {   // the lane's 4 elements are one channel quad of one tap's pixel
-                    const uint32_t o = g < G ? toff(g, 0) : BUF_OOB;
+                    const uint32_t o = toff(g, 0);
                     xd[g] = buf_load4(rin, o == BUF_OOB ? BUF_OOB : ib + o);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
+                        const uint32_t o = toff(g, j);
                         xd[g][j] = buf_load1(rin, o == BUF_OOB ? BUF_OOB : ib + o);
                     }
                 }
             }
         } else {
 #pragma unroll
-            for (int g = 0; g < GM; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoffg(g) : BUF_OOB);
+            for (int g = 0; g < GX; g++) xd[g] = buf_load4(rin, gok(g) ? ib + aoffg(g) : BUF_OOB);
         }
         if (RES) {
             const auto rres = img_rsrc(RES ? P.res : P.out, img0 + ii, out_img);
@@ -174,20 +219,20 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
         }
     };
     if (0 < nimg) load_img(0, x, rv);
-    f4 gm[GM], bt[GM];
+    f4 gm[GX], bt[GX];
     if (LN) {
         const auto rg = buf_rsrc(P.gamma, in_img), rb = buf_rsrc(P.beta, in_img);
 #pragma unroll
-        for (int g = 0; g < GM; g++) {
+        for (int g = 0; g < GX; g++) {
             if constexpr (TAP) {   // the lane's im2col row: gamma / beta of every tap's pixel (0 outside: zero padding)
                 if (tquad) {
-                    const uint32_t o = g < G ? toff(g, 0) : BUF_OOB;
+                    const uint32_t o = toff(g, 0);
                     gm[g] = buf_load4(rg, o);
                     bt[g] = buf_load4(rb, o);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
-                        const uint32_t o = g < G ? toff(g, j) : BUF_OOB;
+                        const uint32_t o = toff(g, j);
                         gm[g][j] = buf_load1(rg, o);
                         bt[g][j] = buf_load1(rb, o);
                     }
@@ -207,10 +252,8 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     // memory round trip as the loads above and the weights below (folded after the weight copy)
     const bool lnpre = LN && wave < nimg;   // (image wave: the LN table below is per workgroup)
     const LnSlots slot0 = lnpre ? in_ln_fetch(P, img0 + wave) : LnSlots{};
-    // weights -> LDS; per-image input LN (mean, rstd) -> LDS
-    int nwf = __builtin_amdgcn_readfirstlane(G * 16 * NSJ);
-    asm volatile("" : "+s"(nwf));   // opaque count: a constant one unrolls the copy into the live image loads
-    copy_to_lds<64 * NW>(P.wt, lw, nwf);
+    // weights -> their bf16x6 planes in LDS; per-image input LN (mean, rstd) -> LDS
+    stage_w_x6<64 * NW, NR>(P.wt, lwb, G, C);
     if (LN) {
         for (int i = wave; i < nimg; i += NW) {
             float mu, rs;
@@ -228,15 +271,15 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     __syncthreads();
     PWSTAMP(2);
 
-    const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
+    const unsigned char* bl0 = lwb + lane * 16;
     // one image: A operand from xc / rc, which then receive image pf (when it exists)
-    auto step = [&](int ii, f4 (&xc)[GM], float (&rc)[NR][4], int pf) {
+    auto step = [&](int ii, f4 (&xc)[GX], float (&rc)[NR][4], int pf) {
         const int img = img0 + ii;
         const float rs = LN ? lstat[2 * ii + 1] : 1.f;
         const float nmr = LN ? -lstat[2 * ii] * rs : 0.f;
-        float av[GM][4];
+        f4 av[GX];
 #pragma unroll
-        for (int g = 0; g < GM; g++) {
+        for (int g = 0; g < GX; g++) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float v = !TAP || P.act ? lrelu(xc[g][j]) : xc[g][j];   // conv_in reads raw u
@@ -250,48 +293,28 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) res[n][r] = rc[n][r];
         }
-#ifndef CNF_ABL_PW_NOLOAD
-        if (pf < nimg) load_img(pf, xc, rc);   // in flight during this image's MFMAs and stores
+#ifdef CNF_DIAG
+        if (!(a.diag & 2))
 #endif
+        if (pf < nimg) load_img(pf, xc, rc);   // in flight during this image's MFMAs and stores
         f4 acc[NR];
 #pragma unroll
         for (int n = 0; n < NR; n++) acc[n] = f4{0.f, 0.f, 0.f, 0.f};
-        // B quads double-buffered one group ahead; the scheduling fence per group keeps the
-        // compiler from hoisting every group's LDS reads (NR quads each) into live registers
-        // (the generic instantiations keep the plain per-group loop: their runtime group bound already
-        // limits the hoisting, and the extra buffer costs them registers)
-        // B quads of the specialised instantiations read one group ahead (two groups ahead measured
-        // no better: the LDS reads are not what each MFMA group waits on)
-        constexpr int BQD = 1;
-        f4 bq[BQD + 1][NR];
+        // per K step: the lane's 8 activations split into their bf16 planes, then per column block the
+        // weight planes from LDS and six MFMAs; the scheduling fence keeps the compiler from hoisting
+        // every step's LDS reads into live registers
 #pragma unroll
-        for (int j = 0; j < BQD; j++)
-            if (j < GM && (SID >= 0 || j == 0))
+        for (int c = 0; c < CM; c++) {
+            if (c < C) {
+                const Split8 a8 = split8(av[2 * c], av[2 * c + 1]);
 #pragma unroll
-                for (int n = 0; n < NR; n++) bq[j][n] = *reinterpret_cast<const f4*>(brow + (size_t)j * 4 * NSJ * 4 + n * 64);
-#pragma unroll
-        for (int g = 0; g < GM; g++) {
-            if (SID < 0 && g < G) {
-                f4 bp[NR];
-#pragma unroll
-                for (int n = 0; n < NR; n++) bp[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
-#pragma unroll
-                for (int s = 0; s < 4; s++)
-#pragma unroll
-                    for (int n = 0; n < NR; n++)
-                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bp[n][s], acc[n], 0, 0, 0);
-            } else if (SID >= 0 && g < G) {
-                if (g + BQD < GM && g + BQD < G)
-#pragma unroll
-                    for (int n = 0; n < NR; n++)
-                        bq[(g + BQD) % (BQD + 1)][n] =
-                            *reinterpret_cast<const f4*>(brow + (size_t)(g + BQD) * 4 * NSJ * 4 + n * 64);
-#pragma unroll
-                for (int s = 0; s < 4; s++)
-#pragma unroll
-                    for (int n = 0; n < NR; n++)
-                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][s], bq[g % (BQD + 1)][n][s], acc[n], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
+                for (int n = 0; n < NR; n++) {
+                    const unsigned char* bp = bl0 + (c * 3 * NR + n) * 1024;
+                    const bf16x8 bh = *reinterpret_cast<const bf16x8*>(bp);
+                    const bf16x8 bm = *reinterpret_cast<const bf16x8*>(bp + NR * 1024);
+                    const bf16x8 bl = *reinterpret_cast<const bf16x8*>(bp + 2 * NR * 1024);
+                    acc[n] = mfma_x6(a8.h, a8.m, a8.l, bh, bm, bl, acc[n]);
+                }
             }
         }
         // epilogue: bias, residual, masked store, per-wave LN partial of LeakyReLU(out)
@@ -321,6 +344,10 @@ __global__ __launch_bounds__(64 * PW_NW, CNF_PW_MINW) void k_pw(ConvArgs a) {
     };
     // this wave's images: the buffers then receive image ii + 1
     for (int ii = 0; ii < nimg; ii++) {
+#ifdef CNF_DIAG
+        if ((a.diag & 2) && ii > 0) load_img(ii, x, rv);   // (experiment: no prefetch)
+        if (a.diag & 4) __syncthreads();
+#endif
         step(ii, x, rv, ii + 1);
         PWSTAMP(3 + ii);
     }
@@ -344,9 +371,15 @@ bool launch_pw_shape(int sid, const ConvArgs& a, dim3 g, dim3 b, int lds, hipStr
 
 int pw_num_shapes() { return CNF_PW_NSHAPES; }
 
-void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, int grid_x, int lds, hipStream_t st) {
+void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a_in, int grid_x, int lds, hipStream_t st) {
+#ifdef CNF_DIAG
+    ConvArgs a = a_in;
+    if (const char* e = std::getenv("CNF_PW_DIAG")) a.diag = std::atoi(e);
+#else
+    const ConvArgs& a = a_in;
+#endif
     dim3 g(grid_x, a.nprob), b(64 * PW_NW);
-    const bool generic = opts().generic != 0;   // debug option GENERIC=1
+    const bool generic = (opts().generic & 3) != 0;   // debug option GENERIC bit 1 (all) or 2 (k_pw)
     bool dual = false;
     for (int i = 0; i < a.nprob; i++) dual |= a.p[i].out2 != nullptr;
     if (dual) {   // training forward conv_a with the dense t1 copy: generic instantiations only
@@ -365,9 +398,16 @@ void launch_pw(int nr, int gm, bool ln, bool res, bool tap, const ConvArgs& a, i
         throw std::invalid_argument("k_pw dual store: no instantiation for this shape");
     }
     PwShape sh;
+#ifdef CNF_DIAG
+    const char* only = std::getenv("CNF_PW_ONLY_SID");   // diagnostic builds: one specialised instantiation
+#endif
     if (!generic && pw_shape_of(nr, gm, ln, res, tap, a, sh))
-        for (int sid = 0; sid < CNF_PW_NSHAPES; sid++)
+        for (int sid = 0; sid < CNF_PW_NSHAPES; sid++) {
+#ifdef CNF_DIAG
+            if (only && std::atoi(only) != sid) continue;
+#endif
             if (std::memcmp(&sh, &kPwShapes[sid], sizeof(sh)) == 0 && launch_pw_shape<0>(sid, a, g, b, lds, st)) return;
+        }
     if (tap) {   // generic tap mode (streamed conv_in / grouped branches): no residual, K <= 128
         if (res || gm > 8) throw std::invalid_argument("k_pw tap mode: no residual, K <= 128");
 #define CNF_PW_TCASE(NR_, GM_, LN_)                                                     \
@@ -431,6 +471,56 @@ __device__ __forceinline__ int gc_out_pixel(const GcArgs& a, int po, int px0, in
     return px0 + por * GS(W) + poc;
 }
 
+// The branch's PK_Q4 fp32 weight image (plan: quads qd = tap * cinp / 4 + ch / 4, [qd][16 nr][4]) ->
+// its bf16x6 planes in LDS (as k_pw's stage_w_x6, rows = outputs): lane (kq, i16) of K step c, output
+// block nb holds W[k = 32c + 8kq + jj][16nb + i16], k = tap * S + ch; zero past the taps / channels
+template <int NTH>
+__device__ __forceinline__ void stage_gcw_x6(const float* __restrict__ src, unsigned char* dst, const GcBranch& br,
+                                             int nr) {
+    const int n = br.G * nr * 128, ns = 16 * nr, cpq4 = br.cinp >> 2;   // float4 slots (c, nb, lane, half)
+    for (int base = 0; base < n; base += NTH * 2) {
+        f4 v[2];
+        int o[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int t = base + u * NTH + (int)threadIdx.x;
+            const int c = t / (nr * 128), r = t - c * (nr * 128), nb = r >> 7, ln = (r >> 1) & 63, half = r & 1;
+            const int k0 = 32 * c + 8 * (ln >> 4) + 4 * half, col = 16 * nb + (ln & 15);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int tap = (k0 + j) / br.S, ch = k0 + j - tap * br.S;
+                v[u][j] = t < n && tap < 9 && ch < br.cin && col < br.cout
+                              ? src[((tap * cpq4 + (ch >> 2)) * ns + col) * 4 + (ch & 3)]
+                              : 0.f;
+            }
+            o[u] = t < n ? (c * 3 * nr + nb) * 1024 + ln * 16 + half * 8 : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            if (o[u] < 0) continue;
+            bf16x4 h, m, l;
+            split4(v[u], h, m, l);
+            *reinterpret_cast<bf16x4*>(dst + o[u]) = h;
+            *reinterpret_cast<bf16x4*>(dst + o[u] + nr * 1024) = m;
+            *reinterpret_cast<bf16x4*>(dst + o[u] + 2 * nr * 1024) = l;
+        }
+    }
+}
+
+// one plane of a subtile lane's K octet (8 consecutive k = tap * S + ch of its im2col row) from the
+// band: S >= 8 one 16-byte read, S = 4 two 8-byte reads (two taps), S = 2 four 4-byte reads
+__device__ __forceinline__ bf16x8 gc_octet(const unsigned char* p, int S, const int4& o) {
+    if (S >= 8) return *reinterpret_cast<const bf16x8*>(p + 2 * o.x);
+    if (S == 4) {
+        const bf16x4 u = *reinterpret_cast<const bf16x4*>(p + 2 * o.x), v = *reinterpret_cast<const bf16x4*>(p + 2 * o.y);
+        return __builtin_shufflevector(u, v, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    const bf16x2 u0 = *reinterpret_cast<const bf16x2*>(p + 2 * o.x), u1 = *reinterpret_cast<const bf16x2*>(p + 2 * o.y);
+    const bf16x2 u2 = *reinterpret_cast<const bf16x2*>(p + 2 * o.z), u3 = *reinterpret_cast<const bf16x2*>(p + 2 * o.w);
+    const bf16x4 lo = __builtin_shufflevector(u0, u1, 0, 1, 2, 3), hi = __builtin_shufflevector(u2, u3, 0, 1, 2, 3);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 template <int NR, int SID, int BI>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, const unsigned char* smem,
                                           const float* bias, float* __restrict__ outp, int npx,
@@ -438,10 +528,12 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     const GcBranch& br = BI >= 0 ? kGcShapes[SID >= 0 ? SID : 0].br[BI >= 0 ? BI : 0] : brx;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, kq = lane >> 4;
-    constexpr int NSJ = 16 * NR;
-    const float* band = reinterpret_cast<const float*>(smem + br.band_off + boff);
-    const float* lw = reinterpret_cast<const float*>(smem + br.w_off);
-    const int* qo = reinterpret_cast<const int*>(smem + br.q_off);
+    // bf16x6 contraction (cnf_device.h): the band's three planes (S bf16 channels per pixel), the weights'
+    // three planes (1 KiB per K step, plane and 16 outputs), one int4 of band offsets per K octet
+    const int S = br.S, PB = (br.BH * br.BW * S * 2 + 15) & ~15;
+    const unsigned char* band = smem + br.band_off + boff;
+    const unsigned char* wl = smem + br.w_off + lane * 16;
+    const int4* ot = reinterpret_cast<const int4*>(smem + br.q_off);
     // operands swapped (A = weights, B = activations): lane (i16, kq) ends with pixel i16, channels
     // 16n + 4kq + r (r < 4) of the subtile, i.e. one 16-byte channel quad per n -> f4 stores
     f4 bz[NR];
@@ -455,16 +547,13 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     }
     const bool vq = ((br.opcs | br.out_off) & 3) == 0;
     const int nsub = (npx + 15) >> 4;
-    // two subtiles per wave and pass (s0, s0 + NW) share every B read: two independent MFMA
-    // chains per wave keep the SIMD busy at 2 waves per SIMD; A quads are issued in chunks of GQ
-    constexpr int GQ = 6;
-    const int G = br.G;
-    const float* brow = lw + ((size_t)kq * NSJ + i16) * 4;
+    // two subtiles per wave and pass (s0, s0 + NW) share every weight read
+    const int C = br.G;   // 32-deep K steps
     constexpr int NW = GC_NWS;   // (16 waves cover a 256-pixel tile in one pass: the pair's second half is dead code)
     for (int s0 = wave; s0 < nsub; s0 += 2 * NW) {
         const int s1 = s0 + NW;
         const bool v1 = s1 < nsub;
-        const float* base[2];
+        const unsigned char* base[2];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int pt = (h ? s1 : s0) * 16 + i16;
@@ -474,7 +563,7 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             const int blk = GS(nbk) > 1 ? ptc / tpx : 0;
             const int rem = ptc - blk * tpx;
             const int tr = rem / GS(TW), tc = rem - tr * GS(TW);
-            base[h] = band + ((blk * (GS(TH) + 2 * br.dil) + tr) * br.BW + tc) * br.S;
+            base[h] = band + 2 * ((blk * (GS(TH) + 2 * br.dil) + tr) * br.BW + tc) * S;
         }
         f4 acc0[NR], acc1[NR];   // start at the bias
 #pragma unroll
@@ -482,30 +571,24 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             acc0[n] = bz[n];
             acc1[n] = bz[n];
         }
-        for (int g0 = 0; g0 < G; g0 += GQ) {
-            int qv[GQ];
-#pragma unroll
-            for (int j = 0; j < GQ; j++) qv[j] = g0 + j < G ? qo[4 * (g0 + j) + kq] : 0;
-            f4 a0[GQ], a1[GQ];
-#pragma unroll
-            for (int j = 0; j < GQ; j++) {
-                a0[j] = *reinterpret_cast<const f4*>(base[0] + qv[j]);
-                a1[j] = *reinterpret_cast<const f4*>(base[1] + qv[j]);
+        for (int c = 0; c < C; c++) {
+            const int4 o = ot[4 * c + kq];
+            const bf16x8 xh0 = gc_octet(base[0], S, o), xm0 = gc_octet(base[0] + PB, S, o),
+                         xl0 = gc_octet(base[0] + 2 * PB, S, o);
+            bf16x8 xh1 = xh0, xm1 = xm0, xl1 = xl0;
+            if (v1) {
+                xh1 = gc_octet(base[1], S, o);
+                xm1 = gc_octet(base[1] + PB, S, o);
+                xl1 = gc_octet(base[1] + 2 * PB, S, o);
             }
 #pragma unroll
-            for (int j = 0; j < GQ; j++) {
-                if (g0 + j >= G) break;
-                const int g = g0 + j;
-                f4 bq[NR];
-#pragma unroll
-                for (int n = 0; n < NR; n++) bq[n] = *reinterpret_cast<const f4*>(brow + (size_t)g * 4 * NSJ * 4 + n * 64);
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-#pragma unroll
-                    for (int n = 0; n < NR; n++) {
-                        acc0[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(bq[n][q], a0[j][q], acc0[n], 0, 0, 0);
-                        acc1[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(bq[n][q], a1[j][q], acc1[n], 0, 0, 0);
-                    }
+            for (int n = 0; n < NR; n++) {
+                const unsigned char* wp = wl + (c * 3 * NR + n) * 1024;
+                const bf16x8 wh = *reinterpret_cast<const bf16x8*>(wp);
+                const bf16x8 wm = *reinterpret_cast<const bf16x8*>(wp + NR * 1024);
+                const bf16x8 wlo = *reinterpret_cast<const bf16x8*>(wp + 2 * NR * 1024);
+                acc0[n] = mfma_x6(wh, wm, wlo, xh0, xm0, xl0, acc0[n]);
+                if (v1) acc1[n] = mfma_x6(wh, wm, wlo, xh1, xm1, xl1, acc1[n]);
             }
         }
         if (stats && first) {
@@ -541,9 +624,9 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
     }
 }
 
-// staged band quads per thread: 2 in the specialised instantiations (the plan keeps a group's bands
-// within 128 quads per wave), GC_STAGE_QUADS over the generic kernel's threads
-#define GC_GQS (SID >= 0 ? 2 : GC_STAGE_QUADS / GC_NTS)
+// staged band units per thread: 4 at 8 waves, 2 at 4 (the plan keeps a group's bands within
+// gc_stage_units)
+#define GC_GQS (gc_stage_units(GC_NWS) / GC_NTS)
 #define GC_PDS (SID >= 0 ? kGcShapes[SID >= 0 ? SID : 0].pd : 1)   // band prefetch depth (images)
 
 // the branches of table entry SID, unrolled at compile time
@@ -608,23 +691,25 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     const bool ln = SID >= 0 ? (GS(lnst) & 1) != 0 : a.in_part[net] != nullptr;
     const bool stats = SID >= 0 ? (GS(lnst) & 2) != 0 : a.out_part[net] != nullptr;
     float* lstat = reinterpret_cast<float*>(smem + PW_LDS_STAT);
-    float* lds_f = reinterpret_cast<float*>(smem);
     int gs = 0;
     GSTAMP(gs++);
     GWSTAMP(0);
 
-    // image-independent staging plan of this thread: quad e = tid + GC_NT*u of the concatenated branch
-    // bands -> source offset inside one image, LDS float index, valid channels (0 = zero quad)
-    int soff[GC_GQ], loff[GC_GQ], nv[GC_GQ];
+    // image-independent staging plan of this thread: unit e = tid + GC_NT*u of the concatenated branch
+    // bands (a channel quad of a band pixel, up to the branch's S channels; S = 2: one pair) -> source
+    // offset inside one image, LDS byte offset in plane 0 and plane stride, valid channels (0 = zeros;
+    // bit 3: one 16-byte load, bit 4: a channel pair)
+    int soff[GC_GQ], loff[GC_GQ], lpb[GC_GQ], nv[GC_GQ];
 #pragma unroll
     for (int u = 0; u < GC_GQ; u++) {
         int e = tid + GC_NT * u;
         soff[u] = 0;
         loff[u] = -1;
+        lpb[u] = 0;
         nv[u] = 0;
         for (int bi = 0; bi < GS(nbr); bi++) {
             const GcBranch& br = GS(br)[bi];
-            const int cpq = br.cinp >> 2, nq = br.BH * br.BW * cpq;
+            const int cpq = br.S >= 4 ? br.S >> 2 : 1, nq = br.BH * br.BW * cpq;
             if (e < nq) {
                 const int pix = cpq == 1 ? e : (int)__umulhi((unsigned)e, br.cpq_mag), cq = e - pix * cpq;
                 const int brr = (int)__umulhi((unsigned)pix, br.bw_mag), bc = pix - brr * br.BW;
@@ -637,13 +722,15 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
                     y = pa + sy * GS(ps);
                     x = pb + sx * GS(ps);
                 }
-                loff[u] = br.band_off / 4 + pix * br.S + 4 * cq;
-                if (inb) {
+                loff[u] = br.band_off + 2 * (pix * br.S + 4 * cq);
+                lpb[u] = (br.BH * br.BW * br.S * 2 + 15) & ~15;
+                if (inb && 4 * cq < br.cin) {
                     soff[u] = (y * W + x) * br.pcs + br.cin_off + 4 * cq;
                     const int v = min(4, br.cin - 4 * cq);
                     const bool vec = v == 4 && ((br.cin_off | br.pcs) & 3) == 0;
                     nv[u] = v | (vec ? 8 : 0);
                 }
+                if (br.S == 2) nv[u] |= 16;
                 break;
             }
             e -= nq;
@@ -675,23 +762,35 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
 #pragma unroll
         for (int u = 0; u < GC_GQ; u++) xd[u] = load_q(r, u);
     };
-    // LN2(LeakyReLU(t1)) of the quads in xq -> band buffer (ii & 1); zero outside the image / window
+    // LN2(LeakyReLU(t1)) of the quads in xq -> the three bf16 planes of band buffer (ii & 1); zero
+    // outside the image / window
     auto store_img = [&](int ii, const f4 (&xs)[GC_GQ]) {
         const float rs = ln ? lstat[2 * ii + 1] : 1.f;
         const float nmr = ln ? -lstat[2 * ii] * rs : 0.f;
-        float* dst = lds_f + (ii & 1) * (GS(band_bytes) / 4);
+        unsigned char* dst = smem + (ii & 1) * GS(band_bytes);
 #pragma unroll
         for (int u = 0; u < GC_GQ; u++) {
             if (loff[u] < 0) continue;
             f4 v = f4{0.f, 0.f, 0.f, 0.f};
-            if (nv[u] != 0) {
+            if ((nv[u] & 7) != 0) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const float t = lrelu(xs[u][j]);
                     v[j] = ln ? fmaf(fmaf(t, rs, nmr), gq[u][j], bq[u][j]) : t;
                 }
             }
-            *reinterpret_cast<f4*>(dst + loff[u]) = v;
+            bf16x4 h, m, l;
+            split4(v, h, m, l);
+            unsigned char* d = dst + loff[u];
+            if (nv[u] & 16) {
+                *reinterpret_cast<bf16x2*>(d) = __builtin_shufflevector(h, h, 0, 1);
+                *reinterpret_cast<bf16x2*>(d + lpb[u]) = __builtin_shufflevector(m, m, 0, 1);
+                *reinterpret_cast<bf16x2*>(d + 2 * lpb[u]) = __builtin_shufflevector(l, l, 0, 1);
+            } else {
+                *reinterpret_cast<bf16x4*>(d) = h;
+                *reinterpret_cast<bf16x4*>(d + lpb[u]) = m;
+                *reinterpret_cast<bf16x4*>(d + 2 * lpb[u]) = l;
+            }
         }
     };
     load_img(0, xq[0]);
@@ -703,21 +802,32 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     lnP.part_stride = a.part_stride;
     const bool lnpre = ln && wave < nimg;
     const LnSlots slot0 = lnpre ? in_ln_fetch(lnP, img0 + wave) : LnSlots{};
-    // packed weights and quad-offset tables of every branch (once per workgroup)
+    // weight planes, biases and K-octet offset tables of every branch (once per workgroup)
     for (int bi = 0; bi < GS(nbr); bi++) {
         const GcBranch& br = GS(br)[bi];
         const int nr = (br.cout + 15) >> 4;
-        copy_to_lds<GC_NT>(a.w[net][bi], reinterpret_cast<float*>(smem + br.w_off), br.G * 16 * 16 * nr);
+        stage_gcw_x6<GC_NT>(a.w[net][bi], smem + br.w_off, br, nr);
         for (int i = tid; i < br.cout; i += GC_NT) reinterpret_cast<float*>(smem + br.b_off)[i] = a.b[net][bi][i];
-        int* qo = reinterpret_cast<int*>(smem + br.q_off);
-        const int cpq = br.cinp >> 2, nq = 9 * cpq;
-        for (int qd = tid; qd < 4 * br.G; qd += GC_NT) {
-            int o = 0;   // padding quads have zero weights: any in-band address is fine
-            if (qd < nq) {
-                const int tap = qd / cpq, cq = qd - tap * cpq;
-                o = (((tap / 3) * br.dil) * br.BW + (tap % 3) * br.dil) * br.S + 4 * cq;
+        // K octet e: k = 8e .. 8e + 7, k = tap * S + ch: the band offsets (bf16 elements from the pixel's
+        // tap-(0, 0) origin) of its one (S >= 8), two (S = 4) or four (S = 2) taps; past the 9 taps: 0
+        // (their weights are zero: any in-band address is fine)
+        int4* ot = reinterpret_cast<int4*>(smem + br.q_off);
+        auto tapo = [&](int tap) { return tap < 9 ? (((tap / 3) * br.dil) * br.BW + (tap % 3) * br.dil) * br.S : 0; };
+        for (int e = tid; e < 4 * br.G; e += GC_NT) {
+            int4 o = {0, 0, 0, 0};
+            if (br.S >= 8) {
+                const int t = 8 * e / br.S;
+                o.x = t < 9 ? tapo(t) + 8 * e - t * br.S : 0;
+            } else if (br.S == 4) {
+                o.x = tapo(2 * e);
+                o.y = tapo(2 * e + 1);
+            } else {
+                o.x = tapo(4 * e);
+                o.y = tapo(4 * e + 1);
+                o.z = tapo(4 * e + 2);
+                o.w = tapo(4 * e + 3);
             }
-            qo[qd] = o;
+            ot[e] = o;
         }
     }
     GSTAMP(gs++);   // (diagnostic builds: band / gamma / beta / weight loads landed)
@@ -776,7 +886,15 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
             }
         }
         if (stats) st.write(a.out_part[net] + ((size_t)img * a.part_stride + tile * GC_NW + wave) * LNP);
-        if (ii + 1 < nimg) store_img(ii + 1, xq[(jj + 1) % PD]);   // the other buffer: nobody reads it this iteration
+        // every wave's MFMAs of this image done before any wave stages the next one into the other
+        // buffer. Without this barrier the shape-specialised instantiations whose waves do not all
+        // compute (cfg5's 64-pixel dil-1 tile: 4 of 16 waves) gave run-to-run different t2 on the
+        // second image of a workgroup (cfg5 B >= 2: zy 2e-2 off the oracle); the generic and the
+        // runtime-shape builds of the same code, and this one with the barrier, are exact
+        if (ii + 1 < nimg) {
+            __syncthreads();
+            store_img(ii + 1, xq[(jj + 1) % PD]);
+        }
         __syncthreads();
         GSTAMP(gs++);
         GWSTAMP(2 + ii);
@@ -806,10 +924,17 @@ int gc_num_shapes() { return CNF_GC_NSHAPES; }
 
 // table entry matching a's shape, -1 for the generic instantiation
 static int gc_shape_id(const GcArgs& a) {
-    const bool generic = opts().generic != 0;   // debug option GENERIC=1
+    const bool generic = (opts().generic & 5) != 0;   // debug option GENERIC bit 1 (all) or 4 (k_gc)
+#ifdef CNF_DIAG
+    const char* only = std::getenv("CNF_GC_ONLY_SID");   // diagnostic builds: one specialised instantiation
+#endif
     if (!generic)
-        for (int sid = 0; sid < CNF_GC_NSHAPES; sid++)
+        for (int sid = 0; sid < CNF_GC_NSHAPES; sid++) {
+#ifdef CNF_DIAG
+            if (only && std::atoi(only) != sid) continue;
+#endif
             if (std::memcmp(&a.s, &kGcShapes[sid], sizeof(GcShape)) == 0) return sid;
+        }
     return -1;
 }
 

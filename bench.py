@@ -309,6 +309,42 @@ def cpu_baseline_inverse(cfg, flow, zy_np, B, budget_s=20.0):
                       f'(oracle/cflow_torch_cpu.py), {threads} threads'}
 
 
+def cpu_baseline_train(cfg, flow, xy_np, B, budget_s=20.0):
+    """The torch-CPU fp32 restatement's training step (oracle/cflow_torch_cpu.py: log_loss, autograd
+    backward, torch Adam at the reference's lr 3e-4 / Keras eps 1e-7) on the bench batch and weights,
+    whole batches of B for about budget_s, median per step (rank 0, N=1 only)."""
+    try:
+        from oracle.cflow_torch_cpu import TorchCPUFlow
+    except Exception as e:  # pragma: no cover
+        return {'value': None, 'unit': 'images/s', 'cores': 0, 'kind': 'port', 'sample': f'unavailable: {e}'}
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    tf = TorchCPUFlow(**cfg.kwargs())
+    P = {k: torch.tensor(np.ascontiguousarray(v, np.float32), requires_grad=True) for k, v in flow.get_weights().items()}
+    opt = torch.optim.Adam(list(P.values()), lr=3e-4, eps=1e-7)
+    xy = torch.from_numpy(np.ascontiguousarray(xy_np, np.float32))
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        tf.log_loss(xy, P)[0].backward()
+        opt.step()
+
+    step()   # warm-up
+    times = []
+    t_all = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > budget_s and len(times) >= 3:
+            break
+    med = float(np.median(times))
+    return {'value': round(B / med, 3), 'unit': 'images/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{len(times)} training steps of {B} images of {cfg.name} (log_loss + autograd backward + '
+                      f'Adam, the bench batch and weights), median {med * 1e3:.1f} ms/step over {sum(times):.1f}s, '
+                      f'torch-CPU fp32 restatement (oracle/cflow_torch_cpu.py), {threads} threads'}
+
+
 def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
     """images/s of cFlow.train_step (conv_cINN_make_model.py:1850-1880) on the bench batch: every
     step = cnf_flow_forward_train + cnf_nll + the 5-float loss all-reduce + cnf_flow_backward + the
@@ -339,6 +375,20 @@ def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
         # forward_train (1x the forward convs, activations saved) + the backward's data and weight
         # gradients (2x): 3x the forward FLOPs
         tf = 3.0 * fl_img * G / (ms / 1e3) / 1e12 / world
+        # the step against the FP32 MFMA roof (the training step is MFMA-bound: 3 GFLOP per cfg2 image over
+        # ~0.2 GB of activation saves and gradients); the per-kernel breakdown of the same command is the
+        # committed rocprofv3 summary named in kernel_stats
+        import glob
+        stats = sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*_train_kernel_stats.csv')))
+        roof = {'bound': 'mfma', 'achieved': round(tf, 3), 'peak': FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
+                'frac': round(tf / FP32_MFMA_TFLOPS, 4), 'kernel': 'whole training step (every kernel)',
+                'alg_flops_per_step': 3.0 * fl_img * B,
+                'alg_note': '3x the forward conv FLOPs (SURVEY 8(d)): the forward with saves, the data and the '
+                            'weight gradients', 'traffic': None,
+                'kernel_stats': os.path.relpath(stats[-1], ROOT) if stats else None}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_train(cfg, flow, xy.cpu().numpy(), B)
         out = {'metric': f'images/sec NLL train step (fwd + bwd + Adam), {cfg.name}',
                'value': round(G * args.steps / el, 2), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
                'warmup': args.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': scaling,
@@ -347,6 +397,7 @@ def train_bench(args, cfg, flow, xy, B, G, world, rank, dist, dev, scaling):
                    'model': f'cFlow {cfg.name}', 'global_batch': G, 'per_gpu_batch': B, 'seq_len': None,
                    'parallelism': f'dp{world} (batch shards, gradient all-reduce)'},
                'alg_tflops_per_gpu': round(tf, 3), 'mfma_frac': round(tf / FP32_MFMA_TFLOPS, 4),
+               'roofline': roof, 'cpu_baseline': cpu,
                'loss': float(logs['loss'])}
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -455,6 +506,8 @@ def main():
                          'as many HIP streams, each its own captured step (reported as "serving"; `value` is one '
                          'batch in flight); 1: skip')
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--debug-options', default='', metavar='NAME=V,...',
+                    help='plan debug options (A/B of alternative code paths; the default is what is reported)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     args = ap.parse_args()
@@ -492,7 +545,7 @@ def main():
     if B <= 0:
         raise SystemExit(f'rank {rank}: empty shard of a global batch of {G}')
     from arl_conditional_normalizing_flows_amd.make_model import cFlow
-    flow = cFlow(**cfg.kwargs(), device=dev, seed=0)
+    flow = cFlow(**cfg.kwargs(), device=dev, seed=0, debug_options=args.debug_options or None)
     # one seeded global batch, sliced per rank
     xy_np = synth(cfg, G, 1000, 1.0 if (args.noise is not None and args.mode == 'forward') else 0.98)[lo:hi].copy()
     xy = torch.from_numpy(xy_np).to(dev)

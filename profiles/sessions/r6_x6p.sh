@@ -1,0 +1,4 @@
+set -o pipefail
+out=gpurun_out/x6p; mkdir -p $out; : > $out/d.log
+timeout -k 10 240 python -u profiles/diag/diag_nondet.py cfg5 2 'GENERIC=2' 'GENERIC=2,LAYOUT=1' 'GENERIC=2,LAYOUT=2' 'GENERIC=4' 'GENERIC=4,LAYOUT=1' 'GENERIC=4,LAYOUT=2' >> $out/d.log 2>&1 || exit 1
+cat $out/d.log
