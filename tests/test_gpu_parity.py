@@ -317,13 +317,18 @@ def test_nll_on_more_streams_than_counter_slots(gpu):
         assert torch.equal(o, ref)
 
 
-def test_deterministic(gpu):
-    flow, ora, P, xy = _setup('small', 3)
+@pytest.mark.parametrize('name,B', [('small', 3), ('cfg2', 64), ('cfg4', 32), ('cfg5', 2)])
+def test_deterministic(gpu, name, B):
+    """Three forwards of one batch are equal bit for bit. The batches are ones whose k_pw / k_gc
+    workgroups loop over several images and whose shape-specialised instantiations run (round 6: a
+    constant-cin k_pw build and k_gc staging the next image without a barrier gave run-to-run
+    different outputs at cfg2 B=64 and cfg5 B=2, 2e-2..6e-2 off the oracle)."""
+    flow, ora, P, xy = _setup(name, B)
     x = torch.from_numpy(xy).to(gpu)
-    a = flow(x, 1, per_image_logdet=True)
-    b = flow(x, 1, per_image_logdet=True)
+    runs = [flow(x, 1, per_image_logdet=True) for _ in range(3)]
     torch.cuda.synchronize()
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    for zy, ld in runs[1:]:
+        assert torch.equal(zy, runs[0][0]) and torch.equal(ld, runs[0][1])
 
 
 def test_coupling_layer_api_matches_oracle(gpu):
