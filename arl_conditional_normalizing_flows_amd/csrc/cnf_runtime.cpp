@@ -471,6 +471,9 @@ static int conv_launch(Exec& E, int ks, int role, int h, int w, const std::vecto
         const int64_t units = (int64_t)tiles * a.nprob * E.B;
         const bool lnf = probs[0].in_st.part != nullptr;
         a.ipw = (int)std::min<int64_t>(16, std::max<int64_t>(1, (units + 511) / 512));
+#ifdef CNF_DIAG   // diagnostics: images per workgroup of the residual (conv_b) / other k_pw launches
+        if (const char* e = std::getenv(resf ? "CNF_PW_IPW_RES" : "CNF_PW_IPW")) a.ipw = std::atoi(e);
+#endif
         const int grid_x = tiles * ((E.B + a.ipw - 1) / a.ipw);
         const int nr = pw_nr, gm = pw_gm;
         const bool tapf = tap != nullptr;
