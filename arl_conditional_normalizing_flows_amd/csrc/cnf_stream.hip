@@ -524,9 +524,10 @@ __device__ __forceinline__ bf16x8 gc_octet(const unsigned char* p, int S, const 
 template <int NR, int SID, int BI>
 __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, const unsigned char* smem,
                                           const float* bias, float* __restrict__ outp, int npx,
-                                          int px0, int r0, int ph0, LnAcc& st, bool& first, bool stats, int boff) {
+                                          int px0, int r0, int ph0, LnAcc& st, bool& first, bool stats, int boff,
+                                          int wave) {
     const GcBranch& br = BI >= 0 ? kGcShapes[SID >= 0 ? SID : 0].br[BI >= 0 ? BI : 0] : brx;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const int i16 = lane & 15, kq = lane >> 4;
     // bf16x6 contraction (cnf_device.h): the band's three planes (S bf16 channels per pixel), the weights'
     // three planes (1 KiB per K step, plane and 16 outputs), one int4 of band offsets per K octet
@@ -633,12 +634,12 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
 template <int SID, int BI>
 __device__ __forceinline__ void gc_branches(const GcArgs& a, const unsigned char* smem, float* __restrict__ outp,
                                             int npx, int px0, int r0, int ph0, LnAcc& st, bool& first, bool stats,
-                                            int boff) {
+                                            int boff, int vw) {
     if constexpr (BI < kGcShapes[SID].nbr) {
         constexpr GcBranch br = kGcShapes[SID].br[BI];
         const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
-        gc_branch<(br.cout + 15) / 16, SID, BI>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff);
-        gc_branches<SID, BI + 1>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff);
+        gc_branch<(br.cout + 15) / 16, SID, BI>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff, vw);
+        gc_branches<SID, BI + 1>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff, vw);
     }
 }
 
@@ -673,6 +674,24 @@ __device__ long long g_gc_stamps[64];
 template <int SID>
 __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArgs a) {
     constexpr int GC_NW = GC_NWS, GC_NT = GC_NTS, GC_GQ = GC_GQS, PD = GC_PDS;
+    // image pairs: a specialised tile of at most GC_NW / 4 subtiles (the rows never cut by the image
+    // edge) leaves three quarters of the waves without a subtile, so the two band buffers hold two
+    // images computed at once by two wave sets (cfg5's 64-pixel dil-1 tile: 28.27 -> 27.13 ms per
+    // cfg5 B=64 step; at GC_NW / 2 subtiles, cfg4's 128-pixel tile, it measured slower: 3.51 -> 3.61 ms,
+    // the LDS reads of twice the waves against the staging no longer hidden) (waves w < NSUB: image i0, subtile w; NSUB <= w < 2 NSUB:
+    // image i0 + 1, subtile w - NSUB), staged together before them instead of one behind the other.
+    // Every subtile runs the same instructions as in one-image mode and writes the same LN slot
+    // (subtile s -> slot s, zeros in the slots of waves without a subtile): bitwise the same results
+    constexpr int NSUB = SID >= 0 ? (kGcShapes[SID >= 0 ? SID : 0].nbk * kGcShapes[SID >= 0 ? SID : 0].TH *
+                                        kGcShapes[SID >= 0 ? SID : 0].TW + 15) / 16 : 0;
+#ifdef CNF_GC_NOPAIRS   // (diagnostic builds: one image at a time everywhere, for bitwise A/B)
+    constexpr bool PAIRS = false &&
+#else
+    constexpr bool PAIRS =
+#endif
+                           SID >= 0 && PD == 1 && NSUB > 0 && 4 * NSUB <= GC_NW &&
+                           (kGcShapes[SID >= 0 ? SID : 0].ps > 1 ||
+                            kGcShapes[SID >= 0 ? SID : 0].H % kGcShapes[SID >= 0 ? SID : 0].TH == 0);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int net = blockIdx.y;
     const int tile = blockIdx.x % GS(tiles_per_img);
@@ -794,6 +813,8 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
         }
     };
     load_img(0, xq[0]);
+    f4 xq2[GC_GQ];   // (image pairs: the second image of the group)
+    if (PAIRS && 1 < nimg) load_img(1, xq2);
     // this wave's first LN2 image: partial slots fetched in the same memory round trip as the band
     // and weight loads (folded below)
     ConvProb lnP;
@@ -847,9 +868,40 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     }
     __syncthreads();
     store_img(0, xq[0]);
+    if (PAIRS && 1 < nimg) store_img(1, xq2);
     __syncthreads();
     GSTAMP(gs++);
     GWSTAMP(1);
+
+    if constexpr (PAIRS) {
+        const int jw = wave / NSUB;                       // 0 / 1: image of the pair, >= 2: no subtile
+        const int vw = jw < 2 ? wave - jw * NSUB : NSUB;  // the wave's subtile (NSUB: none)
+        for (int i0 = 0; i0 < nimg; i0 += 2) {
+            // the next pair lands while this one is computed
+            if (i0 + 2 < nimg) load_img(i0 + 2, xq[0]);
+            if (i0 + 3 < nimg) load_img(i0 + 3, xq2);
+            const int ii = i0 + jw;
+            if (jw < 2 && ii < nimg) {
+                LnAcc st;
+                st.reset();
+                bool first = true;
+                float* outp = a.out[net] + (size_t)(img0 + ii) * HW * GS(out_cs);
+                gc_branches<SID, 0>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, jw * GS(band_bytes), vw);
+                if (stats) st.write(a.out_part[net] + ((size_t)(img0 + ii) * a.part_stride + tile * GC_NW + vw) * LNP);
+            }
+            if (stats && wave >= NSUB && lane == 0)   // the slots of the waves without a subtile: empty
+                for (int j = 0; j < 2 && i0 + j < nimg; j++)
+                    *reinterpret_cast<f4*>(a.out_part[net] + ((size_t)(img0 + i0 + j) * a.part_stride + tile * GC_NW + wave) * LNP) =
+                        f4{0.f, 0.f, 0.f, 0.f};
+            if (i0 + 2 < nimg) {
+                __syncthreads();   // both buffers read
+                store_img(i0 + 2, xq[0]);
+                if (i0 + 3 < nimg) store_img(i0 + 3, xq2);
+                __syncthreads();
+            }
+        }
+        return;
+    }
 
     // the ring's other images (PD > 1)
 #pragma unroll
@@ -871,16 +923,16 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
         float* outp = a.out[net] + (size_t)img * HW * GS(out_cs);
         const int boff = (ii & 1) * GS(band_bytes);
         if constexpr (SID >= 0) {
-            gc_branches<SID, 0>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff);
+            gc_branches<SID, 0>(a, smem, outp, npx, px0, r0, ph0, st, first, stats, boff, wave);
         } else {
             for (int bi = 0; bi < GS(nbr); bi++) {
                 const GcBranch& br = GS(br)[bi];
                 const float* bias = reinterpret_cast<const float*>(smem + br.b_off);
                 switch ((br.cout + 15) >> 4) {
-                    case 1: gc_branch<1, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
-                    case 2: gc_branch<2, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
-                    case 3: gc_branch<3, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
-                    default: gc_branch<4, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff); break;
+                    case 1: gc_branch<1, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff, wave); break;
+                    case 2: gc_branch<2, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff, wave); break;
+                    case 3: gc_branch<3, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff, wave); break;
+                    default: gc_branch<4, SID, -1>(a, br, smem, bias, outp, npx, px0, r0, ph0, st, first, stats, boff, wave); break;
                 }
                 GSTAMP(gs++);
             }
