@@ -574,8 +574,12 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
         }
         for (int c = 0; c < C; c++) {
             const int4 o = ot[4 * c + kq];
+#ifdef CNF_ABL_GC_BLDS   // ablation (diagnostic builds only, wrong results): one band plane read from LDS
+            const bf16x8 xh0 = gc_octet(base[0], S, o), xm0 = xh0, xl0 = xh0;
+#else
             const bf16x8 xh0 = gc_octet(base[0], S, o), xm0 = gc_octet(base[0] + PB, S, o),
                          xl0 = gc_octet(base[0] + 2 * PB, S, o);
+#endif
             bf16x8 xh1 = xh0, xm1 = xm0, xl1 = xl0;
             if (v1) {
                 xh1 = gc_octet(base[1], S, o);
@@ -586,8 +590,12 @@ __device__ __forceinline__ void gc_branch(const GcArgs& a, const GcBranch& brx, 
             for (int n = 0; n < NR; n++) {
                 const unsigned char* wp = wl + (c * 3 * NR + n) * 1024;
                 const bf16x8 wh = *reinterpret_cast<const bf16x8*>(wp);
+#ifdef CNF_ABL_GC_WLDS   // ablation (diagnostic builds only, wrong results): one weight plane read from LDS
+                const bf16x8 wm = wh, wlo = wh;
+#else
                 const bf16x8 wm = *reinterpret_cast<const bf16x8*>(wp + NR * 1024);
                 const bf16x8 wlo = *reinterpret_cast<const bf16x8*>(wp + 2 * NR * 1024);
+#endif
                 acc0[n] = mfma_x6(wh, wm, wlo, xh0, xm0, xl0, acc0[n]);
                 if (v1) acc1[n] = mfma_x6(wh, wm, wlo, xh1, xm1, xl1, acc1[n]);
             }
