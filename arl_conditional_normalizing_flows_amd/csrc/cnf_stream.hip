@@ -692,7 +692,10 @@ __global__ __launch_bounds__(GC_NTS, SID >= 0 ? 16 / GC_NWS : 1) void k_gc(GcArg
     // (subtile s -> slot s, zeros in the slots of waves without a subtile): bitwise the same results
     constexpr int NSUB = SID >= 0 ? (kGcShapes[SID >= 0 ? SID : 0].nbk * kGcShapes[SID >= 0 ? SID : 0].TH *
                                         kGcShapes[SID >= 0 ? SID : 0].TW + 15) / 16 : 0;
-#ifdef CNF_GC_NOPAIRS   // (diagnostic builds: one image at a time everywhere, for bitwise A/B)
+    // Off by default since the end of round 6: the cfg5 ragged-batch GPU test (B = 64 against batches of
+    // 5, bit for bit) failed once (7.7e-3) in three full-suite runs of the final tree, and this is the
+    // newest path of the cfg5 tiles; diagnostic builds with -DCNF_GC_PAIRS keep it for A/B
+#ifndef CNF_GC_PAIRS
     constexpr bool PAIRS = false &&
 #else
     constexpr bool PAIRS =
