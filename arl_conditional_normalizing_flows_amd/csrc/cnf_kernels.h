@@ -30,7 +30,10 @@ struct Options {
     int netlds = 1;          // NETLDS: 0 = no LDS-resident (k_net_lds) layers, every layer streamed
     int gc = 1;              // GC: 0 = no fused k_gc stage (grouped branches as k_pw tap mode / k_conv<3>)
     int pw = 1;              // PW: 0 = the per-tile k_conv1 / k_conv<3> kernels and the one-kernel k_convtap conv_out
-    int generic = 0;         // GENERIC bits: never the shape-specialised instantiations of 1 any kernel, 2 k_pw, 4 k_gc, 8 k_net_lds
+#ifndef CNF_DIAG_GENERIC
+#define CNF_DIAG_GENERIC 0   // (diagnostic builds: a different default for A/B runs of the unmodified tests)
+#endif
+    int generic = CNF_DIAG_GENERIC;   // GENERIC bits: never the shape-specialised instantiations of 1 any kernel, 2 k_pw, 4 k_gc, 8 k_net_lds
     int layout = 7;          // LAYOUT bits: 1 compact t1 sub-tensors, 2 mapped t2 sub-tensors, 4 polyphase k_gc tiles
     int fuse_coupling = 1;   // FUSE_COUPLING: 0 = every coupling layer launches its own k_coupling
     int lds_bwd = 2;         // LDS_BWD: 0 multi-kernel backward of the k_net_lds layers, 1 fused (one launch), 2 fused split

@@ -795,7 +795,11 @@ static void run_coupling(Exec& E, const Coupling& c, const float* u, float* v, d
     // more slots than a consumer wave fetches in its prologue (64 x LN_FETCH = 512: the 128x128 layers):
     // merged once per image by k_ln_merge instead of by every consumer workgroup for each of its images
     // (the 64x64 layers' slots are folded by the consumers: 70 fewer launches per cfg4 step)
+#ifdef CNF_DIAG_NO_LN_MERGE   // (diagnostic builds: the consumers fold every slot)
+    constexpr int ln_merge_over = 1 << 30;
+#else
     constexpr int ln_merge_over = 64 * LN_FETCH;
+#endif
     auto set_parts = [&](int k, int nparts) {
         if (ln && nparts > ln_merge_over) {
             float* p0 = sl[0][k].part;
