@@ -64,7 +64,9 @@ typedef struct cnf_flow_desc {
     /* Debug options, NULL or "" for the defaults (what is benchmarked): "NAME=V[,NAME=V...]" selecting
      * the alternative code paths the parity tests compare against — NETLDS, GC, PW, GENERIC, LAYOUT,
      * FUSE_COUPLING, LDS_BWD, TRAIN_ALT, TRAIN_SCHED (meanings: csrc/cnf_kernels.h Options). Parsed at
-     * cnf_plan_create (unknown name: CNF_E_INVALID); the string is not kept. The library reads no
+     * cnf_plan_create (unknown name: CNF_E_INVALID); the string is not kept. Without a GENERIC entry, a
+     * flow on images of 64 x 64 and above runs the generic k_pw / k_gc kernels (GENERIC=6; the
+     * shape-specialised ones showed intermittent differences there). The library reads no
      * environment variable. No reference counterpart (the Keras model has no such switches). */
     const char* debug_options;
 } cnf_flow_desc;
