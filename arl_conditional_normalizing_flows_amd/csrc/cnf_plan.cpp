@@ -148,6 +148,9 @@ bool netlds_geometry(const Coupling& c, int ci_fmt, int co_fmt, const std::vecto
 }
 }  // namespace
 
+#ifndef CNF_AUTO_GENERIC
+#define CNF_AUTO_GENERIC 6   // (diagnostic builds: 2 / 4 to A/B the two kernels)
+#endif
 Plan* build_plan(const cnf_flow_desc* d) {
     require(d != nullptr, "null descriptor");
     auto P = new Plan();
@@ -162,7 +165,7 @@ Plan* build_plan(const cnf_flow_desc* d) {
         // the 32 x 32 and smaller images' instantiations (cfg2, cfg3, ref_default) passed every run.
         if ((int64_t)d->io_h * d->io_w >= 64 * 64 &&
             !(d->debug_options != nullptr && std::strstr(d->debug_options, "GENERIC=") != nullptr))
-            p.opts.generic |= 6;
+            p.opts.generic |= CNF_AUTO_GENERIC;
         p.desc.debug_options = nullptr;   // (the caller's string: not kept)
         const int nb = d->num_blocks;
         require(nb > 0 && d->squeeze_factor_block_list && d->resnext_block_list && d->num_kernels_list &&
